@@ -1,0 +1,184 @@
+/*
+ * mlffpcg.h — C ABI of the MI355X (gfx950) preconditioned-CG solver for the
+ * sGDML kernel linear system  (sigma_K * K + lam * I) x = b.
+ *
+ * This is the drop-in boundary for the hot path of bluecher31/mlff-preconditioner
+ * (reference mounted at /root/reference; citations are relative to it).  The
+ * reference wires its solve through scipy LinearOperators and
+ * scipy.sparse.linalg.cg; every entry point below replaces one of those plug
+ * points:
+ *
+ *   reference interface (file:line)                                   -> entry point here
+ *   ---------------------------------------------------------------------------------------
+ *   Iterative._init_kernel_operator / _K_vec
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:383-445          -> mlff_set_operator + mlff_matvec
+ *   GDMLTrain._assemble_kernel_mat (+ worker)
+ *       src/sGDML/sgdml/train.py:81-236, 1121-1308                   -> mlff_assemble_sgdml
+ *   tools.utils.create_kernel_mat (synthetic RBF)
+ *       src/tools/utils.py:173-187                                   -> mlff_gen_rbf
+ *   set dense K from the caller (K_hat in custom_cg_solver)
+ *       src/tools/custom_cg_solver.py:126-158                        -> mlff_set_matrix_host
+ *   pivoted_cholesky + IterativeCholesky._init_precon_operator
+ *       src/sGDML/sgdml/solvers/incomplete_cholesky.py:24-93
+ *       src/sGDML/sgdml/solvers/iterative_cholesky.py:115-150        -> mlff_precon_pivchol
+ *   Iterative._init_precon_operator (Nystrom, "_P_vec")
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:95-322           -> mlff_precon_nystrom(variant 0)
+ *   Iterative._init_precon_operator_sb ("*_custom")
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:326-381          -> mlff_precon_nystrom(variant 1)
+ *   svd_preconditioner (Woodbury on a supplied low-rank factor)
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:1313-1329        -> mlff_precon_lowrank
+ *   P_op.matvec                                                       -> mlff_precon_apply
+ *   scipy.sparse.linalg.cg(-K_op, y, x0, M=P_op, tol, atol=None, maxiter, callback)
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:995-1005         -> mlff_pcg_start / mlff_pcg_run /
+ *                                                                       mlff_pcg_result
+ *   _lev_scores (numeric part)
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:447-552          -> mlff_lev_scores
+ *
+ * Conventions
+ *  - All matrices are fp64.  Host buffers are C-contiguous, owned by the
+ *    caller, and never retained after a call returns.
+ *  - One context = one GPU = one rank.  With world > 1 the N rows of K (and
+ *    every N-vector) are split into contiguous row blocks, rank r owning rows
+ *    [row0, row0 + nrows) (see mlff_shard_range).  "local" buffers have nrows
+ *    entries, "global" buffers have N entries.
+ *  - Every function returns MLFF_OK (0) or a negative MLFF_ERR_* code;
+ *    mlff_last_error() gives the message.  Non-convergence is not an error:
+ *    it is reported through `info` exactly as scipy does (0 converged,
+ *    maxiter otherwise).
+ */
+#ifndef MLFFPCG_H
+#define MLFFPCG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MLFF_OK 0
+#define MLFF_ERR_ARG (-1)     /* bad argument (reference: ValueError / AssertionError on shapes) */
+#define MLFF_ERR_HIP (-2)     /* HIP runtime failure */
+#define MLFF_ERR_NOT_PSD (-3) /* pivot <= 0 in pivoted Cholesky (incomplete_cholesky.py:62 assert) */
+#define MLFF_ERR_LINALG (-4)  /* Cholesky of a k x k block failed (scipy LinAlgError) */
+#define MLFF_ERR_STATE (-5)   /* call order: e.g. mlff_pcg_start before a matrix is set */
+#define MLFF_ERR_COMM (-6)    /* RCCL failure */
+#define MLFF_ERR_NOMEM (-7)   /* device allocation failed */
+
+/* preconditioner kinds reported by mlff_precon_info */
+#define MLFF_PRECON_NONE 0
+#define MLFF_PRECON_PIVCHOL 1  /* incomplete (pivoted) Cholesky + Woodbury (iterative_cholesky.py:115-150) */
+#define MLFF_PRECON_NYSTROM 2  /* Nystrom, _init_precon_operator (iterative_solver.py:95-322) */
+#define MLFF_PRECON_NYSTROM_SB 3 /* _init_precon_operator_sb (iterative_solver.py:326-381) */
+#define MLFF_PRECON_LOWRANK 4  /* Woodbury on a caller-supplied factor (iterative_solver.py:1313-1329) */
+
+/* pcg status (mlff_pcg_result) */
+#define MLFF_PCG_RUNNING 0
+#define MLFF_PCG_CONVERGED 2
+#define MLFF_PCG_MAXITER 3
+
+typedef struct mlff_ctx mlff_ctx;
+
+/* ---- library / devices ---------------------------------------------------- */
+int mlff_version(void);                       /* 100 * major + minor */
+int mlff_device_count(int *n_out);
+/* RCCL unique id (128 bytes) for a world > 1 context; rank 0 creates it and the
+ * caller broadcasts it (torch.distributed / any channel) to the other ranks. */
+int mlff_comm_unique_id(unsigned char id_out[128]);
+
+/* ---- context --------------------------------------------------------------- */
+/* n_global: kernel size N.  comm_id may be NULL when world == 1. */
+int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_id,
+                    int64_t n_global, mlff_ctx **ctx_out);
+int mlff_ctx_destroy(mlff_ctx *ctx);
+const char *mlff_last_error(mlff_ctx *ctx); /* ctx may be NULL (thread-local last error) */
+int mlff_shard_range(mlff_ctx *ctx, int64_t *row0_out, int64_t *nrows_out);
+/* leading dimension (doubles) of the device copy of K; rows are padded to 64 */
+int mlff_matrix_ld(mlff_ctx *ctx, int64_t *ld_out);
+int mlff_synchronize(mlff_ctx *ctx);
+/* HIP stream the context launches on (hipStream_t as void*) */
+int mlff_stream(mlff_ctx *ctx, void **stream_out);
+
+/* ---- kernel matrix K (device resident, this rank's row block) --------------- */
+/* K_local: nrows x N row-major with leading dimension ld_host (>= N).          */
+int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host);
+/* copy rows [r0, r0+nr) (local indices) x all N columns back to the host */
+int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int64_t ld_out);
+/* synthetic SPD RBF kernel: K_ij = exp(-0.5 * |x_i/ell - x_j/ell|^2) + jitter*delta_ij
+ * (sklearn RBF(length_scale=ell) as used by tools/utils.py:173-187).  X: N x d (all points). */
+int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, double jitter);
+/* sGDML Matern-5/2 Hessian kernel assembly, GDMLTrain._assemble_kernel_mat with
+ * col_idxs = all (train.py:81-236,1121-1308).  R_desc: M x D, R_d_desc: M x D x 3
+ * (Desc.from_R layout, desc.py:292-358), perms: n_perms x n_atoms atom permutations
+ * (task['perms']), sig: length scale.  N must equal 3 * n_atoms * M.           */
+int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc,
+                        int64_t M, int n_atoms, const int32_t *perms, int n_perms, double sig);
+/* sGDML descriptors on the GPU (desc.py:203-358, no cutoff / no PBC):
+ * R: M x n_atoms x 3  ->  R_desc: M x D (1/r_ij), R_d_desc: M x D x 3          */
+int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
+                           double *R_d_desc_out);
+
+/* operator A = sigma_K * K + lam * I.  sGDML: sigma_K = -1 (K is negative
+ * semidefinite, the solved system is (-K + lam I) x = y, iterative_solver.py:995);
+ * RBF: sigma_K = +1. */
+int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam);
+/* y_local = A v_global (one collective-free local GEMV; v_global has N entries) */
+int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local);
+/* diag(sigma_K * K) (local) */
+int mlff_get_diag(mlff_ctx *ctx, double *diag_local);
+
+/* ---- preconditioners ------------------------------------------------------- */
+int mlff_precon_none(mlff_ctx *ctx);
+/* pivoted Cholesky of S = sigma_K*K to rank k (tie rule: first maximum in the
+ * current permuted order, incomplete_cholesky.py:53) then Woodbury with lam:
+ * T = chol(lam I + L^T L)^-1 L^T, apply z = (r - T^T T r) / lam.
+ * index_columns_out (N, int64, optional): the permutation (first k = pivots).
+ * build_woodbury = 0 only computes the pivots (truncated_cholesky selector). */
+int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
+                        double *seconds_out);
+/* Nystrom from sorted column indices idx (k).  variant 0 = _init_precon_operator
+ * (eig-sign diagonal shift, apply (B^T B r - r)/lam), variant 1 = _sb (1e-16
+ * shift, apply -(r - P^T P r)/lam). */
+int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant, double *seconds_out);
+/* Woodbury on a caller-supplied factor L (N x k, given as Lt_local: k x nrows):
+ * T = chol(lam I + L^T L)^-1 L^T, apply z = (r - T^T T r)/lam. */
+int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k);
+int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out);
+/* z_local = M r_local (collective over ranks for the low-rank part) */
+int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local);
+/* the k x nrows Woodbury panel T (or B / P for Nystrom) of this rank */
+int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out);
+
+/* ridge leverage scores of the approximating columns idx (k): numeric part of
+ * _lev_scores (iterative_solver.py:489-552); scores_out: N (global, every rank). */
+int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out);
+
+/* ---- preconditioned CG (scipy 1.7.3 legacy semantics) ---------------------- */
+/* Starts a solve of A x = b with x0 (local parts; x0 may be NULL = zeros).
+ * tol: relative tolerance, atol = tol * ||b|| (scipy `atol=None` legacy mode);
+ * maxiter: iteration cap (reference: 5N).  Returns *early_exit = 1 when scipy's
+ * legacy pre-check ||A x0 - b|| <= tol ends the solve before any iteration. */
+int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local, double tol,
+                   int64_t maxiter, int *early_exit_out);
+/* run up to n_iter more iterations (stops early on convergence / maxiter).
+ * chunk: iterations launched between host status polls (0 = default 32).   */
+int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out);
+/* iterations done, status, last stop-test residual ||r||, scipy info code */
+int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *resid_out,
+                    int *info_out);
+/* x_local of the current iterate */
+int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local);
+/* residual trace: trace_out[0] = ||r_0||, trace_out[j] = stop-test ||r_j||, j = 1..iters */
+int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n);
+
+/* ---- timing (device time of the hot kernels, hipEvents on the ctx stream) --- */
+int mlff_timing_enable(mlff_ctx *ctx, int on);
+/* accumulated milliseconds and launch counts of the K mat-vec (GEMV) and of the
+ * whole PCG iteration since the last reset */
+int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double *iter_ms,
+                     int64_t *iter_count);
+int mlff_timing_reset(mlff_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MLFFPCG_H */

@@ -1,0 +1,867 @@
+// C ABI of libmlffpcg.so (declared in include/mlffpcg.h): context, kernel
+// matrix, preconditioner builds and the scipy-1.7.3-compatible PCG driver.
+//
+// PCG driver (restating scipy.sparse.linalg.cg 1.7.3 = CGREVCOM template + python
+// wrapper, as called at src/sGDML/sgdml/solvers/iterative_solver.py:995-1005):
+//   atol = tol * ||b||                      (legacy atol=None; ||A x0 - b|| <= tol exits early)
+//   r = b - A x0;  if ||r|| < atol: done
+//   ITER = ITER + 1:  z = M r; rho = r.z; p = z + (rho/rho1) p (p = z at ITER 1)
+//                     q = A p; alpha = rho / p.q; x += alpha p; r -= alpha q
+//                     stop test ||r|| <= atol, re-checked with r = b - A x when ITER > 1
+//                     ITER == maxiter -> info = maxiter
+// Every iteration is 5-7 launches on one stream with all scalars kept on the
+// device; the host polls the status word once per chunk of iterations, and
+// kernels of iterations past convergence return immediately (status gating),
+// so the iteration count is exact without a per-iteration host sync.
+#include "common.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+using namespace mlff;
+
+static thread_local std::string g_last_error;
+
+namespace mlff {
+
+int set_error(mlff_ctx *ctx, int code, const std::string &msg) {
+  if (ctx != nullptr) ctx->err = msg;
+  g_last_error = msg;
+  return code;
+}
+
+int hip_check(mlff_ctx *ctx, hipError_t e, const char *what) {
+  const int code = (e == hipErrorOutOfMemory) ? MLFF_ERR_NOMEM : MLFF_ERR_HIP;
+  return set_error(ctx, code, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what) {
+  return set_error(ctx, MLFF_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(e));
+}
+
+}  // namespace mlff
+
+namespace {
+
+constexpr int kTimingPool = 4096;
+
+int ensure_matrix(mlff_ctx *ctx) {
+  if (ctx->K == nullptr) {
+    MLFF_HIP(ctx, hipMalloc(&ctx->K, sizeof(double) * ctx->blk * ctx->ld));
+  }
+  return MLFF_OK;
+}
+
+int dev_free(void *p) {
+  if (p != nullptr) (void)hipFree(p);
+  return MLFF_OK;
+}
+
+// allreduce (sum) of n doubles in place, no-op on one rank
+int allreduce(mlff_ctx *ctx, double *buf, size_t n) {
+  if (ctx->world > 1 && n > 0)
+    MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  return MLFF_OK;
+}
+
+// gather the rank blocks of an ld-long padded vector (in place)
+int allgather_blocks(mlff_ctx *ctx, double *full) {
+  if (ctx->world > 1)
+    MLFF_NCCL(ctx, ncclAllGather(full + ctx->rank * ctx->blk, full, ctx->blk, ncclDouble,
+                                 ctx->comm, ctx->stream));
+  return MLFF_OK;
+}
+
+// scatter a global host vector (N) into a padded device vector (ld)
+int scatter_global(mlff_ctx *ctx, const double *v, double *dev_full) {
+  MLFF_HIP(ctx, hipMemsetAsync(dev_full, 0, sizeof(double) * ctx->ld, ctx->stream));
+  for (int r = 0; r < ctx->world; ++r) {
+    const int64_t g0 = (int64_t)r * ctx->rows_per;
+    if (g0 >= ctx->N) break;
+    const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
+    MLFF_HIP(ctx, hipMemcpyAsync(dev_full + (int64_t)r * ctx->blk, v + g0, sizeof(double) * cnt,
+                                 hipMemcpyHostToDevice, ctx->stream));
+  }
+  return MLFF_OK;
+}
+
+// scalar = sum over ranks of a . b (local), synchronous
+int dot_sync(mlff_ctx *ctx, const double *a, const double *b, double *out) {
+  double *part = ctx->part;  // slot 0 region
+  launch_dot_part(a, b, ctx->nrows, part, nullptr, ctx->stream);
+  MLFF_TRY(allreduce(ctx, part, kVecGrid));
+  launch_reduce_to(part, kVecGrid, &ctx->st->pad0, ctx->stream);
+  MLFF_HIP(ctx, hipMemcpyAsync(out, &ctx->st->pad0, sizeof(double), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+double *rho_part(mlff_ctx *c) { return c->part + 0 * kMaxPart; }
+double *pq_part(mlff_ctx *c) { return c->part + 1 * kMaxPart; }
+double *rr_part(mlff_ctx *c) { return c->part + 2 * kMaxPart; }
+
+int alloc_panel(mlff_ctx *ctx, int64_t k) {
+  if (ctx->T != nullptr) {
+    (void)hipFree(ctx->T);
+    ctx->T = nullptr;
+  }
+  if (ctx->tpart != nullptr) {
+    (void)hipFree(ctx->tpart);
+    ctx->tpart = nullptr;
+  }
+  MLFF_HIP(ctx, hipMalloc(&ctx->T, sizeof(double) * round_up(k, 8) * ctx->blk));
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * ctx->blk, ctx->stream));
+  ctx->tsplit = choose_tsplit(k, ctx->blk);
+  MLFF_HIP(ctx, hipMalloc(&ctx->tpart, sizeof(double) * k * ctx->tsplit));
+  return MLFF_OK;
+}
+
+// _cho_factor_stable (iterative_solver.py:576-583): shift the diagonal by -1e-15
+// when the smallest eigenvalue is positive, +1e-15 otherwise, then Cholesky.  The
+// sign test is done by attempting the factorization: a successful Cholesky of
+// M - 1e-15 I certifies lo_eig > 0 up to rounding; otherwise M + 1e-15 I is used.
+int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
+  double *tmp = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&tmp, sizeof(double) * k * k, ctx->stream));
+  MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+  launch_add_diag(tmp, k, -1e-15, ctx->stream);
+  int rc = potrf_lower(ctx, tmp, k);
+  if (rc == MLFF_ERR_LINALG) {
+    MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+    launch_add_diag(tmp, k, 1e-15, ctx->stream);
+    rc = potrf_lower(ctx, tmp, k);
+  }
+  if (rc == MLFF_OK)
+    MLFF_HIP(ctx, hipMemcpyAsync(A, tmp, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+  MLFF_HIP(ctx, hipFreeAsync(tmp, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return rc;
+}
+
+// Woodbury panel from a wide factor W = L^T (k x blk) in place:
+//   G = lam I + W W^T; L2 = chol(G); W <- L2^-1 W   (iterative_cholesky.py:141-143)
+int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
+  double *G = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, ctx->stream));
+  MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
+  MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
+  launch_add_diag(G, k, ctx->lam, ctx->stream);
+  MLFF_TRY(potrf_lower(ctx, G, k));
+  MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));
+  MLFF_HIP(ctx, hipFreeAsync(G, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+// Nystrom panel (iterative_solver.py:112-283 for variant 0, :343-374 for variant 1,
+// :489-550 for the leverage scores which follow variant 0).  W: k x blk, zeroed.
+int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant, double lam,
+                  double *W) {
+  hipStream_t s = ctx->stream;
+  int64_t *didx = nullptr;
+  double *Smm = nullptr, *G = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&didx, sizeof(int64_t) * k, s));
+  MLFF_HIP(ctx, hipMallocAsync(&Smm, sizeof(double) * k * k, s));
+  MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(didx, idx_host, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
+  // K_nm^T (sign convention S = sigma_K K; sign flips cancel in B^T B)
+  launch_gather_cols(ctx->K, ctx->ld, ctx->nrows, didx, k, ctx->rows_per, ctx->blk, ctx->sigma_K,
+                     W, ctx->blk, s);
+  launch_gather_mm(W, ctx->blk, didx, k, ctx->row0, ctx->nrows, Smm, s);
+  MLFF_TRY(allreduce(ctx, Smm, (size_t)(k * k)));
+  int rc;
+  if (variant == 0) {
+    rc = cho_factor_stable(ctx, Smm, k);          // U^T U = -K_mm (+-1e-15)
+  } else {
+    launch_add_diag(Smm, k, 1e-16, s);            // cholesky(K_mm + 1e-16 I, lower=True)
+    rc = potrf_lower(ctx, Smm, k);
+  }
+  if (rc != MLFF_OK) return rc;
+  MLFF_TRY(trsm_lower_wide(ctx, Smm, k, W, ctx->blk, ctx->blk));   // C^T = U^-T K_nm^T
+  MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));           // C^T C
+  MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
+  launch_add_diag(G, k, lam, s);
+  if (variant == 0)
+    rc = cho_factor_stable(ctx, G, k);
+  else
+    rc = potrf_lower(ctx, G, k);
+  if (rc != MLFF_OK) return rc;
+  MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));     // B = V^-T C^T
+  MLFF_HIP(ctx, hipFreeAsync(didx, s));
+  MLFF_HIP(ctx, hipFreeAsync(Smm, s));
+  MLFF_HIP(ctx, hipFreeAsync(G, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  return MLFF_OK;
+}
+
+int check_idx(mlff_ctx *ctx, const int64_t *idx, int64_t k) {
+  if (idx == nullptr || k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "bad column index set");
+  for (int64_t j = 0; j < k; ++j) {
+    if (idx[j] < 0 || idx[j] >= ctx->N) return set_error(ctx, MLFF_ERR_ARG, "column index out of range");
+    if (j > 0 && idx[j] <= idx[j - 1])
+      return set_error(ctx, MLFF_ERR_ARG, "column indices must be sorted and unique (train.py:1197-1201)");
+  }
+  return MLFF_OK;
+}
+
+int require_operator(mlff_ctx *ctx) {
+  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_operator) return set_error(ctx, MLFF_ERR_STATE, "mlff_set_operator not called");
+  return MLFF_OK;
+}
+
+hipEvent_t timing_event(mlff_ctx *ctx) {
+  Timing &t = ctx->timing;
+  if (t.used >= t.ev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    t.ev.push_back(e);
+  }
+  return t.ev[t.used++];
+}
+
+struct GemvMark {
+  size_t ev0;
+  long long it;
+};
+
+// one PCG iteration (ITER = it), all launches status gated
+int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) {
+  hipStream_t s = ctx->stream;
+  const int *status = &ctx->st->status;
+  double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
+  const double *zsrc;
+  if (ctx->precon_kind != MLFF_PRECON_NONE) {
+    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
+    launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
+                    ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s);
+    zsrc = ctx->z;
+  } else {
+    launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s);
+    zsrc = ctx->r;
+  }
+  MLFF_TRY(allreduce(ctx, rho_part(ctx), kVecGrid));
+  launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
+  MLFF_TRY(allgather_blocks(ctx, ctx->p_full));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ctx->timing.on && marks != nullptr) {
+    e0 = timing_event(ctx);
+    if (e0) hipEventRecord(e0, s);
+  }
+  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->p_full, ctx->q, ctx->sigma_K, ctx->lam, p_loc,
+                   status, s);
+  if (e0 != nullptr) {
+    e1 = timing_event(ctx);
+    if (e1) {
+      hipEventRecord(e1, s);
+      marks->push_back({ctx->timing.used - 2, it});
+    }
+  }
+  launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
+  MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
+  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
+                   status, s);
+  MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
+  launch_stoptest(rr_part(ctx), ctx->st, ctx->trace, it, s);
+  return MLFF_OK;
+}
+
+// true-residual recheck of the python wrapper: r = b - A x, resid = ||r||
+int do_recheck(mlff_ctx *ctx) {
+  hipStream_t s = ctx->stream;
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * ctx->blk, ctx->x,
+                               sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
+  MLFF_TRY(allgather_blocks(ctx, ctx->xg));
+  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam, ctx->x,
+                   nullptr, s);
+  launch_residual(ctx->b, ctx->q, ctx->r, ctx->nrows, rr_part(ctx), s);
+  MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
+  launch_recheck_finish(rr_part(ctx), ctx->st, ctx->trace, s);
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
+}
+
+int poll_state(mlff_ctx *ctx) {
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->h_st, ctx->st, sizeof(DevState), hipMemcpyDeviceToHost,
+                               ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mlff_version(void) { return 100; }
+
+int mlff_device_count(int *n_out) {
+  if (n_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null pointer");
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *n_out = 0;
+    return hip_check(nullptr, e, "hipGetDeviceCount");
+  }
+  *n_out = n;
+  return MLFF_OK;
+}
+
+int mlff_comm_unique_id(unsigned char id_out[128]) {
+  if (id_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null pointer");
+  ncclUniqueId id;
+  MLFF_NCCL(nullptr, ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(id_out, &id, 128);
+  return MLFF_OK;
+}
+
+const char *mlff_last_error(mlff_ctx *ctx) {
+  if (ctx != nullptr) return ctx->err.c_str();
+  return g_last_error.c_str();
+}
+
+int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_id,
+                    int64_t n_global, mlff_ctx **ctx_out) {
+  if (ctx_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx_out");
+  *ctx_out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return set_error(nullptr, MLFF_ERR_ARG, "bad rank/world");
+  if (n_global < 1) return set_error(nullptr, MLFF_ERR_ARG, "N must be >= 1");
+  if (world > 1 && comm_id == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "comm_id required for world > 1");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
+    return set_error(nullptr, MLFF_ERR_HIP, "no HIP device available");
+  if (device < 0 || device >= ndev) return set_error(nullptr, MLFF_ERR_ARG, "bad device id");
+  mlff_ctx *ctx = new mlff_ctx();
+  ctx->device = device;
+  ctx->rank = rank;
+  ctx->world = world;
+  ctx->N = n_global;
+  ctx->rows_per = (n_global + world - 1) / world;
+  ctx->row0 = std::min<int64_t>((int64_t)rank * ctx->rows_per, n_global);
+  ctx->nrows = std::max<int64_t>(0, std::min<int64_t>(ctx->rows_per, n_global - ctx->row0));
+  ctx->blk = round_up(ctx->rows_per, kPad);
+  ctx->ld = (int64_t)world * ctx->blk;
+  auto fail = [&](int rc) {
+    mlff_ctx_destroy(ctx);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_HIP, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+    return fail(set_error(nullptr, MLFF_ERR_HIP, "hipStreamCreate failed"));
+  if (world > 1) {
+    ncclUniqueId id;
+    std::memcpy(&id, comm_id, 128);
+    const ncclResult_t e = ncclCommInitRank(&ctx->comm, world, id, rank);
+    if (e != ncclSuccess) {
+      ctx->comm = nullptr;
+      return fail(set_error(nullptr, MLFF_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e)));
+    }
+  }
+  double **vecs[] = {&ctx->x, &ctx->r, &ctx->z, &ctx->q, &ctx->b};
+  for (double **v : vecs) {
+    if (hipMalloc(v, sizeof(double) * ctx->blk) != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_NOMEM, "alloc"));
+    hipMemset(*v, 0, sizeof(double) * ctx->blk);
+  }
+  if (hipMalloc(&ctx->p_full, sizeof(double) * ctx->ld) != hipSuccess ||
+      hipMalloc(&ctx->xg, sizeof(double) * ctx->ld) != hipSuccess ||
+      hipMalloc(&ctx->part, sizeof(double) * 4 * kMaxPart) != hipSuccess ||
+      hipMalloc(&ctx->st, sizeof(DevState)) != hipSuccess ||
+      hipHostMalloc(&ctx->h_st, sizeof(DevState)) != hipSuccess ||
+      hipMalloc(&ctx->dwork, sizeof(double) * ctx->blk) != hipSuccess ||
+      hipMalloc(&ctx->pivflag, sizeof(int) * ctx->blk) != hipSuccess ||
+      hipMalloc(&ctx->perm, sizeof(int64_t) * n_global) != hipSuccess)
+    return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
+  hipMemset(ctx->p_full, 0, sizeof(double) * ctx->ld);
+  hipMemset(ctx->xg, 0, sizeof(double) * ctx->ld);
+  hipMemset(ctx->part, 0, sizeof(double) * 4 * kMaxPart);
+  hipMemset(ctx->st, 0, sizeof(DevState));
+  std::memset(ctx->h_st, 0, sizeof(DevState));
+  if (hipDeviceSynchronize() != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_HIP, "init sync failed"));
+  *ctx_out = ctx;
+  return MLFF_OK;
+}
+
+int mlff_ctx_destroy(mlff_ctx *ctx) {
+  if (ctx == nullptr) return MLFF_OK;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
+                  (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
+                  (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart,
+                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow})
+    dev_free(p);
+  if (ctx->h_st) hipHostFree(ctx->h_st);
+  for (hipEvent_t e : ctx->timing.ev) hipEventDestroy(e);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return MLFF_OK;
+}
+
+int mlff_shard_range(mlff_ctx *ctx, int64_t *row0_out, int64_t *nrows_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (row0_out) *row0_out = ctx->row0;
+  if (nrows_out) *nrows_out = ctx->nrows;
+  return MLFF_OK;
+}
+
+int mlff_matrix_ld(mlff_ctx *ctx, int64_t *ld_out) {
+  if (ctx == nullptr || ld_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  *ld_out = ctx->ld;
+  return MLFF_OK;
+}
+
+int mlff_synchronize(mlff_ctx *ctx) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_stream(mlff_ctx *ctx, void **stream_out) {
+  if (ctx == nullptr || stream_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  *stream_out = (void *)ctx->stream;
+  return MLFF_OK;
+}
+
+int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (K_local == nullptr && ctx->nrows > 0) return set_error(ctx, MLFF_ERR_ARG, "null K");
+  if (ld_host < ctx->N) return set_error(ctx, MLFF_ERR_ARG, "ld_host < N");
+  MLFF_TRY(ensure_matrix(ctx));
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->K, 0, sizeof(double) * ctx->blk * ctx->ld, ctx->stream));
+  for (int r = 0; r < ctx->world && ctx->nrows > 0; ++r) {
+    const int64_t g0 = (int64_t)r * ctx->rows_per;
+    if (g0 >= ctx->N) break;
+    const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
+    MLFF_HIP(ctx, hipMemcpy2DAsync(ctx->K + (int64_t)r * ctx->blk, sizeof(double) * ctx->ld,
+                                   K_local + g0, sizeof(double) * ld_host, sizeof(double) * cnt,
+                                   ctx->nrows, hipMemcpyHostToDevice, ctx->stream));
+  }
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->has_matrix = true;
+  return MLFF_OK;
+}
+
+int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int64_t ld_out) {
+  if (ctx == nullptr || out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (r0 < 0 || nr < 0 || r0 + nr > ctx->nrows || ld_out < ctx->N)
+    return set_error(ctx, MLFF_ERR_ARG, "row range / ld_out");
+  for (int r = 0; r < ctx->world; ++r) {
+    const int64_t g0 = (int64_t)r * ctx->rows_per;
+    if (g0 >= ctx->N) break;
+    const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
+    MLFF_HIP(ctx, hipMemcpy2DAsync(out + g0, sizeof(double) * ld_out,
+                                   ctx->K + r0 * ctx->ld + (int64_t)r * ctx->blk,
+                                   sizeof(double) * ctx->ld, sizeof(double) * cnt, nr,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+  }
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, double jitter) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (X == nullptr || d < 1 || d > 8 || !(length_scale > 0.0))
+    return set_error(ctx, MLFF_ERR_ARG, "gen_rbf: need X, 1 <= d <= 8, length_scale > 0");
+  MLFF_TRY(ensure_matrix(ctx));
+  std::vector<double> Xs((size_t)ctx->N * d);
+  for (size_t i = 0; i < Xs.size(); ++i) Xs[i] = X[i] / length_scale;  // sklearn: X / length_scale
+  double *dX = nullptr;
+  MLFF_HIP(ctx, hipMalloc(&dX, sizeof(double) * Xs.size()));
+  MLFF_HIP(ctx, hipMemcpy(dX, Xs.data(), sizeof(double) * Xs.size(), hipMemcpyHostToDevice));
+  if (ctx->blk > ctx->nrows)  // zero padding rows
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->K + ctx->nrows * ctx->ld, 0,
+                                 sizeof(double) * (ctx->blk - ctx->nrows) * ctx->ld, ctx->stream));
+  if (ctx->nrows > 0)
+    launch_gen_rbf(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->N, dX, d,
+                   jitter, ctx->stream);
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  hipFree(dX);
+  ctx->has_matrix = true;
+  return MLFF_OK;
+}
+
+int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
+                        int n_atoms, const int32_t *perms, int n_perms, double sig) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
+    return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: null input or sig <= 0");
+  MLFF_TRY(ensure_matrix(ctx));
+  MLFF_TRY(assemble_sgdml(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
+  ctx->has_matrix = true;
+  return MLFF_OK;
+}
+
+int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
+                           double *R_d_desc_out) {
+  if (R == nullptr || R_desc_out == nullptr || R_d_desc_out == nullptr || M < 1 || n_atoms < 2)
+    return set_error(nullptr, MLFF_ERR_ARG, "sgdml_descriptors: bad arguments");
+  const int rc = sgdml_descriptors(R, M, n_atoms, R_desc_out, R_d_desc_out);
+  if (rc != MLFF_OK) return set_error(nullptr, rc, "sgdml_descriptors: HIP failure");
+  return MLFF_OK;
+}
+
+int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!(lam > 0.0)) return set_error(ctx, MLFF_ERR_ARG, "lam must be > 0");
+  if (sigma_K != 1.0 && sigma_K != -1.0) return set_error(ctx, MLFF_ERR_ARG, "sigma_K must be +-1");
+  ctx->sigma_K = sigma_K;
+  ctx->lam = lam;
+  ctx->has_operator = true;
+  return MLFF_OK;
+}
+
+int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if (v_global == nullptr || (y_local == nullptr && ctx->nrows > 0)) return set_error(ctx, MLFF_ERR_ARG, "null vector");
+  MLFF_TRY(scatter_global(ctx, v_global, ctx->xg));
+  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam,
+                   ctx->xg + (int64_t)ctx->rank * ctx->blk, nullptr, ctx->stream);
+  MLFF_HIP(ctx, hipGetLastError());
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpyAsync(y_local, ctx->q, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  launch_diag_of(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->sigma_K,
+                 ctx->dwork, ctx->stream);
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpyAsync(diag_local, ctx->dwork, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_precon_none(mlff_ctx *ctx) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  ctx->precon_kind = MLFF_PRECON_NONE;
+  ctx->k = 0;
+  return MLFF_OK;
+}
+
+int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
+                        double *seconds_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if (k < 1 || k > ctx->N || k > 16384)
+    return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 16384)");
+  const auto t0 = std::chrono::steady_clock::now();
+  ctx->precon_kind = MLFF_PRECON_NONE;
+  MLFF_TRY(alloc_panel(ctx, k));
+  if (ctx->prow) hipFree(ctx->prow);
+  ctx->prow = nullptr;
+  MLFF_HIP(ctx, hipMalloc(&ctx->prow, sizeof(double) * (k + 1)));
+  MLFF_TRY(pivoted_cholesky(ctx, k, index_columns_out));
+  if (build_woodbury) {
+    MLFF_TRY(woodbury_inplace(ctx, ctx->T, k));
+    ctx->precon_kind = MLFF_PRECON_PIVCHOL;
+    ctx->k = k;
+    ctx->sigma_p = 1.0;
+  }
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (seconds_out)
+    *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return MLFF_OK;
+}
+
+int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant,
+                        double *seconds_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if (variant != 0 && variant != 1) return set_error(ctx, MLFF_ERR_ARG, "variant must be 0 or 1");
+  MLFF_TRY(check_idx(ctx, idx, k));
+  const auto t0 = std::chrono::steady_clock::now();
+  ctx->precon_kind = MLFF_PRECON_NONE;
+  MLFF_TRY(alloc_panel(ctx, k));
+  MLFF_TRY(nystrom_panel(ctx, idx, k, variant, ctx->lam, ctx->T));
+  ctx->precon_kind = variant == 0 ? MLFF_PRECON_NYSTROM : MLFF_PRECON_NYSTROM_SB;
+  ctx->k = k;
+  ctx->sigma_p = -1.0;  // _P_vec returns (B^T B v - v)/lam; _sb returns -(v - P^T P v)/lam
+  if (seconds_out)
+    *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return MLFF_OK;
+}
+
+int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if (k < 1 || k > ctx->N || (Lt_local == nullptr && ctx->nrows > 0))
+    return set_error(ctx, MLFF_ERR_ARG, "lowrank: bad factor");
+  ctx->precon_kind = MLFF_PRECON_NONE;
+  MLFF_TRY(alloc_panel(ctx, k));
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpy2DAsync(ctx->T, sizeof(double) * ctx->blk, Lt_local,
+                                   sizeof(double) * ctx->nrows, sizeof(double) * ctx->nrows, k,
+                                   hipMemcpyHostToDevice, ctx->stream));
+  MLFF_TRY(woodbury_inplace(ctx, ctx->T, k));
+  ctx->precon_kind = MLFF_PRECON_LOWRANK;
+  ctx->k = k;
+  ctx->sigma_p = 1.0;
+  return MLFF_OK;
+}
+
+int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (kind_out) *kind_out = ctx->precon_kind;
+  if (k_out) *k_out = ctx->k;
+  return MLFF_OK;
+}
+
+int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  hipStream_t s = ctx->stream;
+  double *rd = nullptr, *zd = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&rd, sizeof(double) * ctx->blk, s));
+  MLFF_HIP(ctx, hipMallocAsync(&zd, sizeof(double) * ctx->blk, s));
+  MLFF_HIP(ctx, hipMemsetAsync(rd, 0, sizeof(double) * ctx->blk, s));
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpyAsync(rd, r_local, sizeof(double) * ctx->nrows, hipMemcpyHostToDevice, s));
+  if (ctx->precon_kind == MLFF_PRECON_NONE) {
+    MLFF_HIP(ctx, hipMemcpyAsync(zd, rd, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
+  } else {
+    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, rd, ctx->tpart, nullptr, s);
+    MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
+    launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, rd, zd, ctx->nrows,
+                    ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s);
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
+  MLFF_HIP(ctx, hipFreeAsync(rd, s));
+  MLFF_HIP(ctx, hipFreeAsync(zd, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  return MLFF_OK;
+}
+
+int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (ctx->T == nullptr || ctx->k < 1) return set_error(ctx, MLFF_ERR_STATE, "no low-rank panel");
+  if (T_local == nullptr || ld_out < ctx->nrows) return set_error(ctx, MLFF_ERR_ARG, "bad output");
+  if (ctx->nrows > 0)
+    MLFF_HIP(ctx, hipMemcpy2DAsync(T_local, sizeof(double) * ld_out, ctx->T, sizeof(double) * ctx->blk,
+                                   sizeof(double) * ctx->nrows, ctx->k, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!(lam > 0.0) || scores_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "lev_scores: bad args");
+  MLFF_TRY(check_idx(ctx, idx, k));
+  hipStream_t s = ctx->stream;
+  double *W = nullptr;
+  MLFF_HIP(ctx, hipMalloc(&W, sizeof(double) * round_up(k, 8) * ctx->blk));
+  MLFF_HIP(ctx, hipMemsetAsync(W, 0, sizeof(double) * round_up(k, 8) * ctx->blk, s));
+  int rc = nystrom_panel(ctx, idx, k, 0, lam, W);
+  if (rc != MLFF_OK) {
+    hipFree(W);
+    return rc;
+  }
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
+  launch_colsumsq(W, k, ctx->nrows, ctx->blk, ctx->xg + (int64_t)ctx->rank * ctx->blk, s);
+  MLFF_TRY(allgather_blocks(ctx, ctx->xg));
+  for (int r = 0; r < ctx->world; ++r) {
+    const int64_t g0 = (int64_t)r * ctx->rows_per;
+    if (g0 >= ctx->N) break;
+    const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
+    MLFF_HIP(ctx, hipMemcpyAsync(scores_out + g0, ctx->xg + (int64_t)r * ctx->blk,
+                                 sizeof(double) * cnt, hipMemcpyDeviceToHost, s));
+  }
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  hipFree(W);
+  return MLFF_OK;
+}
+
+int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local, double tol,
+                   int64_t maxiter, int *early_exit_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if ((b_local == nullptr && ctx->nrows > 0) || maxiter < 1 || !(tol >= 0.0))
+    return set_error(ctx, MLFF_ERR_ARG, "pcg_start: need b, maxiter >= 1, tol >= 0");
+  hipStream_t s = ctx->stream;
+  if (ctx->trace_cap < maxiter + 1) {
+    if (ctx->trace) hipFree(ctx->trace);
+    ctx->trace = nullptr;
+    MLFF_HIP(ctx, hipMalloc(&ctx->trace, sizeof(double) * (maxiter + 1)));
+    ctx->trace_cap = maxiter + 1;
+  }
+  for (double *v : {ctx->b, ctx->x, ctx->r, ctx->z, ctx->q})
+    MLFF_HIP(ctx, hipMemsetAsync(v, 0, sizeof(double) * ctx->blk, s));
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->p_full, 0, sizeof(double) * ctx->ld, s));
+  if (ctx->nrows > 0) {
+    MLFF_HIP(ctx, hipMemcpyAsync(ctx->b, b_local, sizeof(double) * ctx->nrows, hipMemcpyHostToDevice, s));
+    if (x0_local)
+      MLFF_HIP(ctx, hipMemcpyAsync(ctx->x, x0_local, sizeof(double) * ctx->nrows, hipMemcpyHostToDevice, s));
+  }
+  double bb = 0.0, xx = 0.0;
+  MLFF_TRY(dot_sync(ctx, ctx->b, ctx->b, &bb));
+  MLFF_TRY(dot_sync(ctx, ctx->x, ctx->x, &xx));
+  const double bnorm = std::sqrt(bb);
+  double r0 = bnorm;
+  if (xx != 0.0) {
+    // r = b - A x0
+    MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * ctx->blk, ctx->x,
+                                 sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
+    MLFF_TRY(allgather_blocks(ctx, ctx->xg));
+    launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam, ctx->x,
+                     nullptr, s);
+    launch_residual(ctx->b, ctx->q, ctx->r, ctx->nrows, rr_part(ctx), s);
+    MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
+    launch_reduce_to(rr_part(ctx), kVecGrid, &ctx->st->pad0, s);
+    double rr = 0.0;
+    MLFF_HIP(ctx, hipMemcpyAsync(&rr, &ctx->st->pad0, sizeof(double), hipMemcpyDeviceToHost, s));
+    MLFF_HIP(ctx, hipStreamSynchronize(s));
+    r0 = std::sqrt(rr);
+  } else {
+    MLFF_HIP(ctx, hipMemcpyAsync(ctx->r, ctx->b, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
+  }
+  DevState h{};
+  h.maxiter = maxiter;
+  h.atol = (bnorm == 0.0) ? tol : tol * bnorm;
+  h.status = ST_RUNNING;
+  h.resid = r0;
+  int early = 0;
+  if (r0 <= tol) {          // _get_atol legacy: ||A x0 - b|| <= tol -> return x0
+    h.status = ST_CONVERGED;
+    early = 1;
+  } else if (r0 < h.atol) {  // CGREVCOM: ||r0|| < TOL -> converged before the first iteration
+    h.status = ST_CONVERGED;
+  }
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->st, &h, sizeof(DevState), hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->trace, &r0, sizeof(double), hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  *ctx->h_st = h;
+  ctx->tol = tol;
+  ctx->bnorm = bnorm;
+  ctx->pcg_done = 0;
+  ctx->pcg_active = true;
+  if (early_exit_out) *early_exit_out = early;
+  return MLFF_OK;
+}
+
+int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
+  if (n_iter < 0) return set_error(ctx, MLFF_ERR_ARG, "n_iter < 0");
+  if (chunk <= 0) chunk = 32;
+  hipStream_t s = ctx->stream;
+  const long long maxiter = ctx->h_st->maxiter;
+  const int64_t target = std::min<int64_t>(ctx->pcg_done + n_iter, maxiter);
+  std::vector<GemvMark> marks;
+  while (ctx->h_st->status == ST_RUNNING && ctx->pcg_done < target) {
+    const int64_t first = ctx->pcg_done + 1;
+    const int64_t last = std::min<int64_t>(first + chunk - 1, target);
+    ctx->timing.used = 0;
+    marks.clear();
+    hipEvent_t c0 = nullptr, c1 = nullptr;
+    if (ctx->timing.on) {
+      c0 = timing_event(ctx);
+      if (c0) hipEventRecord(c0, s);
+    }
+    for (int64_t it = first; it <= last; ++it) MLFF_TRY(launch_iteration(ctx, it, &marks));
+    if (ctx->timing.on) {
+      c1 = timing_event(ctx);
+      if (c1) hipEventRecord(c1, s);
+    }
+    MLFF_HIP(ctx, hipGetLastError());
+    MLFF_TRY(poll_state(ctx));
+    const int64_t done_now = ctx->h_st->iters;
+    if (ctx->timing.on && c0 && c1) {
+      for (const GemvMark &mk : marks) {
+        if (mk.it > done_now) continue;  // gated launches after convergence
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ctx->timing.ev[mk.ev0], ctx->timing.ev[mk.ev0 + 1]) == hipSuccess) {
+          ctx->timing.gemv_ms += ms;
+          ctx->timing.gemv_count += 1;
+        }
+      }
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, c0, c1) == hipSuccess) {
+        ctx->timing.iter_ms += ms;
+        ctx->timing.iter_count += done_now - ctx->pcg_done;
+      }
+    }
+    while (ctx->h_st->status == ST_RECHECK) {
+      MLFF_TRY(do_recheck(ctx));
+      MLFF_TRY(poll_state(ctx));
+    }
+    ctx->pcg_done = ctx->h_st->iters;
+  }
+  if (status_out) *status_out = ctx->h_st->status;
+  return MLFF_OK;
+}
+
+int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *resid_out,
+                    int *info_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
+  MLFF_TRY(poll_state(ctx));
+  const DevState &h = *ctx->h_st;
+  if (iters_out) *iters_out = h.iters;
+  if (status_out) *status_out = h.status;
+  if (resid_out) *resid_out = h.resid;
+  if (info_out) *info_out = (h.status == ST_CONVERGED) ? 0 : (int)h.iters;
+  return MLFF_OK;
+}
+
+int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (ctx->nrows > 0) {
+    if (x_local == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null x");
+    MLFF_HIP(ctx, hipMemcpyAsync(x_local, ctx->x, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (!ctx->pcg_active || ctx->trace == nullptr) return set_error(ctx, MLFF_ERR_STATE, "no solve");
+  if (trace_out == nullptr || n < 0) return set_error(ctx, MLFF_ERR_ARG, "bad output");
+  MLFF_TRY(poll_state(ctx));
+  const int64_t avail = ctx->h_st->iters + 1;
+  const int64_t cnt = std::min<int64_t>(n, avail);
+  if (cnt > 0)
+    MLFF_HIP(ctx, hipMemcpy(trace_out, ctx->trace, sizeof(double) * cnt, hipMemcpyDeviceToHost));
+  return MLFF_OK;
+}
+
+int mlff_timing_enable(mlff_ctx *ctx, int on) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  ctx->timing.on = on != 0;
+  if (ctx->timing.on && ctx->timing.ev.size() < kTimingPool) ctx->timing.ev.reserve(kTimingPool);
+  return MLFF_OK;
+}
+
+int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double *iter_ms,
+                     int64_t *iter_count) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (gemv_ms) *gemv_ms = ctx->timing.gemv_ms;
+  if (gemv_count) *gemv_count = ctx->timing.gemv_count;
+  if (iter_ms) *iter_ms = ctx->timing.iter_ms;
+  if (iter_count) *iter_count = ctx->timing.iter_count;
+  return MLFF_OK;
+}
+
+int mlff_timing_reset(mlff_ctx *ctx) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  ctx->timing.gemv_ms = 0.0;
+  ctx->timing.gemv_count = 0;
+  ctx->timing.iter_ms = 0.0;
+  ctx->timing.iter_count = 0;
+  return MLFF_OK;
+}
+
+}  // extern "C"

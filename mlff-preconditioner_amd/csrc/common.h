@@ -1,0 +1,199 @@
+// Shared definitions of the gfx950 PCG library: context layout, device scalar
+// block, launcher prototypes.  Everything here is private to libmlffpcg.so; the
+// public surface is include/mlffpcg.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/mlffpcg.h"
+
+namespace mlff {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;       // threads per workgroup for streaming kernels
+constexpr int kPad = 64;          // row / vector padding (doubles) = 512 B
+constexpr int kMaxPart = 1024;    // partial-sum slots per reduction
+constexpr int kVecGrid = 512;     // workgroups of the grid-stride vector kernels
+
+__host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// PCG status values kept on the device (status gating: every kernel of an
+// iteration returns immediately unless status == RUNNING).
+enum : int { ST_RUNNING = 0, ST_RECHECK = 1, ST_CONVERGED = 2, ST_MAXITER = 3 };
+
+// Device-resident scalars of the solver.  One instance per context.
+struct DevState {
+  double rho, rho1, alpha, pq, rr, resid, atol, pad0;
+  long long iters;     // completed CG iterations (scipy ITER)
+  long long maxiter;
+  int status;
+  int linalg_err;      // set by the Cholesky kernels on a non-positive pivot
+  int pivot_err;       // set by the pivoted-Cholesky finaliser (pivot <= 0)
+  int pad1;
+  long long m_pi;      // current pivot (global index) of the pivoted Cholesky
+  double sqrt_piv;     // its sqrt(pivot)
+  double best_val;     // argmax of this rank
+  long long best_pos;
+};
+
+struct Timing {
+  bool on = false;
+  std::vector<hipEvent_t> ev;  // pool, pairs (start, stop)
+  size_t used = 0;             // events used in the current chunk
+  double gemv_ms = 0.0;
+  int64_t gemv_count = 0;
+  double iter_ms = 0.0;
+  int64_t iter_count = 0;
+};
+
+}  // namespace mlff
+
+struct mlff_ctx {
+  int device = 0, rank = 0, world = 1;
+  int64_t N = 0;        // kernel size
+  int64_t rows_per = 0; // ceil(N / world)
+  int64_t row0 = 0, nrows = 0;
+  int64_t blk = 0;      // padded local length (multiple of 64) = column block per rank
+  int64_t ld = 0;       // world * blk: padded global length / K leading dimension
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+
+  // kernel matrix, blk rows x ld columns (padding rows/cols are zero)
+  double *K = nullptr;
+  bool has_matrix = false;
+  double sigma_K = 1.0, lam = 0.0;
+  bool has_operator = false;
+
+  // CG vectors.  local: blk entries; p_full / xg: ld entries (rank blocks)
+  double *x = nullptr, *r = nullptr, *z = nullptr, *q = nullptr, *b = nullptr;
+  double *p_full = nullptr, *xg = nullptr;
+  double *part = nullptr;  // partial sums: 3 * kMaxPart + tpart (k * S)
+  mlff::DevState *st = nullptr;
+  mlff::DevState *h_st = nullptr;  // pinned mirror
+  double *trace = nullptr;
+  int64_t trace_cap = 0;
+  bool pcg_active = false;
+  int64_t pcg_done = 0;   // iterations known complete on the host side
+  double tol = 0.0, bnorm = 0.0;
+
+  // preconditioner
+  int precon_kind = MLFF_PRECON_NONE;
+  int64_t k = 0;
+  double *T = nullptr;    // k x blk (row stride blk)
+  double sigma_p = 1.0;   // z = sigma_p * (r - T^T T r) / lam
+  int tsplit = 1;         // column splits of the T GEMV
+  double *tpart = nullptr;
+
+  // pivoted Cholesky scratch
+  int64_t *perm = nullptr;   // global permutation (replicated)
+  double *dwork = nullptr;   // residual diagonal (local)
+  int *pivflag = nullptr;    // local rows already pivoted
+  double *prow = nullptr;    // L[m_pi, :m]
+
+  mlff::Timing timing;
+  std::string err;
+};
+
+namespace mlff {
+
+// ---- error helpers (api.hip) ------------------------------------------------
+int set_error(mlff_ctx *ctx, int code, const std::string &msg);
+int hip_check(mlff_ctx *ctx, hipError_t e, const char *what);
+int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
+
+#define MLFF_HIP(ctx, call)                                   \
+  do {                                                        \
+    hipError_t e__ = (call);                                  \
+    if (e__ != hipSuccess) return mlff::hip_check(ctx, e__, #call); \
+  } while (0)
+#define MLFF_NCCL(ctx, call)                                  \
+  do {                                                        \
+    ncclResult_t e__ = (call);                                \
+    if (e__ != ncclSuccess) return mlff::nccl_check(ctx, e__, #call); \
+  } while (0)
+#define MLFF_TRY(x)             \
+  do {                          \
+    int rc__ = (x);             \
+    if (rc__ != MLFF_OK) return rc__; \
+  } while (0)
+
+// ---- vector / GEMV kernels (kernels_vec.hip) ---------------------------------
+// y = sigma * M v + lam * vloc  over `rows` rows of M (ld columns).
+void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v, double *y,
+                      double sigma, double lam, const double *vloc, const int *status,
+                      hipStream_t s);
+// partial T GEMV: tpart[sp * k + j] = sum_{c in split sp} T[j, c] * r[c]
+void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
+                       const double *r, double *tpart, const int *status, hipStream_t s);
+int choose_tsplit(int64_t k, int64_t ncols);
+// z = sigma_p/lam * (r - T^T t), t = sum_sp tpart; rho partials (r . z)
+void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,
+                     const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
+                     double *rho_part, const int *status, hipStream_t s);
+// rho partials of r . r (no preconditioner)
+void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
+                     const int *status, hipStream_t s);
+// p = z + (rho/rho1) p   (p = z at iteration 1); rho = sum(rho_part)
+void launch_update_p(const double *z, double *p, int64_t n, const double *rho_part,
+                     DevState *st, long long it, const int *status, hipStream_t s);
+// pq = sum(pq_part); alpha = rho/pq; x += alpha p; r -= alpha q; rr partials
+void launch_update_xr(double *x, double *r, const double *p, const double *q, int64_t n,
+                      const double *pq_part, double *rr_part, DevState *st, const int *status,
+                      hipStream_t s);
+// rr -> resid, trace, status (scipy stop test)
+void launch_stoptest(const double *rr_part, DevState *st, double *trace, long long it,
+                     hipStream_t s);
+// recheck: r = b - q, rr partials
+void launch_residual(const double *b, const double *q, double *r, int64_t n, double *rr_part,
+                     hipStream_t s);
+void launch_recheck_finish(const double *rr_part, DevState *st, double *trace, hipStream_t s);
+// sum of partials into a device double (1 workgroup)
+void launch_reduce_to(const double *part, int np, double *out, hipStream_t s);
+void launch_scale_copy(const double *a, double *y, int64_t n, double alpha, hipStream_t s);
+
+// ---- dense linear algebra (kernels_dense.hip) -------------------------------
+// C = alpha * op(A) op(B) + beta * C ; row-major; op(A): M x Kd, op(B): Kd x Nc
+void launch_gemm(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+                 const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                 double *C, int64_t ldc, hipStream_t s);
+// G = W W^T (k x k) over ncols columns of W (k x ncols, row stride ldw); split-K
+// with a deterministic slab reduction; work: >= splits * k * k doubles
+int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t ldw, double *G);
+// in-place lower Cholesky of the k x k matrix A (row-major, ld = k)
+int potrf_lower(mlff_ctx *ctx, double *A, int64_t k);
+// W <- L^-1 W, L k x k lower (ld = k), W k x ncols (row stride ldw)
+int trsm_lower_wide(mlff_ctx *ctx, const double *L, int64_t k, double *W, int64_t ncols,
+                    int64_t ldw);
+void launch_add_diag(double *A, int64_t k, double v, hipStream_t s);
+void launch_zero_upper(double *A, int64_t k, hipStream_t s);
+// column sums of squares: out[c] = sum_j W[j, c]^2
+void launch_colsumsq(const double *W, int64_t k, int64_t ncols, int64_t ldw, double *out,
+                     hipStream_t s);
+
+// ---- generators (kernels_gen.hip) -------------------------------------------
+void launch_gen_rbf(double *K, int64_t ld, int64_t nrows, int64_t row0, int64_t rows_per,
+                    int64_t blk, int64_t N, const double *Xs, int d, double jitter,
+                    hipStream_t s);
+void launch_diag_of(const double *K, int64_t ld, int64_t nrows, int64_t row0, int64_t rows_per,
+                    int64_t blk, double sigma, double *out, hipStream_t s);
+// gather columns idx (global) of the local rows: W[j, i] = sigma * K[i, pos(idx_j)]
+void launch_gather_cols(const double *K, int64_t ld, int64_t nrows, const int64_t *idx,
+                        int64_t k, int64_t rows_per, int64_t blk, double sigma, double *W,
+                        int64_t ldw, hipStream_t s);
+// Smm[j, j'] = W[j, idx_j' - row0] if idx_j' is local else 0
+void launch_gather_mm(const double *W, int64_t ldw, const int64_t *idx, int64_t k,
+                      int64_t row0, int64_t nrows, double *Smm, hipStream_t s);
+int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
+                   int n_atoms, const int32_t *perms, int n_perms, double sig);
+int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,
+                      double *R_d_desc);
+
+// ---- pivoted Cholesky (kernels_pivchol.hip) ---------------------------------
+int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out);
+
+}  // namespace mlff

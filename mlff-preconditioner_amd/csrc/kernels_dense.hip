@@ -1,0 +1,321 @@
+// Dense fp64 building blocks of the low-rank preconditioner builds (SYRK, POTRF,
+// TRSM on "wide" k x N panels).  They replace the numpy/LAPACK calls of
+//   iterative_cholesky.py:141-143   kernel = lam I + L^T L; L2 = cholesky; T = L2^-1 L^T
+//   iterative_solver.py:218-283     Nystrom: cho_factor / solve_triangular / K_nm^T K_nm
+//   iterative_solver.py:370-374     _sb variant
+//   iterative_solver.py:507-550     leverage scores
+// Panels are stored k x ncols row-major ("wide"), so every panel operation reads
+// contiguous 512-B row segments.
+#include "common.h"
+
+namespace mlff {
+
+// ---------------------------------------------------------------------------
+// Tiled fp64 GEMM, 64 x 64 output tile per 256-thread workgroup, 4 x 4 per
+// thread, BK = 16.  blockIdx.z = K split (slab = C + z * slab_stride).
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void k_gemm(int64_t M, int64_t N, int64_t K, double alpha,
+                                              const double *__restrict__ A, int64_t lda,
+                                              const double *__restrict__ B, int64_t ldb,
+                                              double beta, double *__restrict__ C, int64_t ldc,
+                                              int64_t kchunk, int64_t slab_stride) {
+  constexpr int BM = 64, BN = 64, BK = 16;
+  __shared__ double As[BK][BM + 1];
+  __shared__ double Bs[BK][BN + 1];
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const int64_t kb = (int64_t)blockIdx.z * kchunk;
+  int64_t ke = kb + kchunk;
+  if (ke > K) ke = K;
+  C += (int64_t)blockIdx.z * slab_stride;
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+
+  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const int e = tid + 256 * l;
+      int mm, kk;
+      if (TA) { kk = e >> 6; mm = e & 63; } else { mm = e >> 4; kk = e & 15; }
+      const int64_t gm = m0 + mm, gk = k0 + kk;
+      double a = 0.0;
+      if (gm < M && gk < ke) a = TA ? A[gk * lda + gm] : A[gm * lda + gk];
+      As[kk][mm] = a;
+      int nn, kb2;
+      if (TB) { nn = e >> 4; kb2 = e & 15; } else { kb2 = e >> 6; nn = e & 63; }
+      const int64_t gn = n0 + nn, gk2 = k0 + kb2;
+      double bv = 0.0;
+      if (gn < N && gk2 < ke) bv = TB ? B[gn * ldb + gk2] : B[gk2 * ldb + gn];
+      Bs[kb2][nn] = bv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; ++kk) {
+      double a[4], bb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[j] = Bs[kk][tx + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t gm = m0 + ty + 16 * i;
+    if (gm >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gn = n0 + tx + 16 * j;
+      if (gn >= N) continue;
+      double v = alpha * acc[i][j];
+      if (beta != 0.0) v = fma(beta, C[gm * ldc + gn], v);
+      C[gm * ldc + gn] = v;
+    }
+  }
+}
+
+static void gemm_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+                        const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                        double *C, int64_t ldc, int splits, int64_t slab_stride, hipStream_t s) {
+  if (M <= 0 || Nc <= 0) return;
+  int64_t kchunk = (Kd + splits - 1) / splits;
+  kchunk = round_up(kchunk < 1 ? 1 : kchunk, 16);
+  dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)splits);
+  if (!ta && !tb)
+    hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
+                       ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (!ta && tb)
+    hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
+                       ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (ta && !tb)
+    hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
+                       ldb, beta, C, ldc, kchunk, slab_stride);
+  else
+    hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
+                       ldb, beta, C, ldc, kchunk, slab_stride);
+}
+
+void launch_gemm(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+                 const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                 double *C, int64_t ldc, hipStream_t s) {
+  gemm_launch(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, 1, 0, s);
+}
+
+// deterministic slab sum: G[i] = sum_s slab[s][i]
+__global__ __launch_bounds__(256) void k_sum_slabs(const double *__restrict__ slabs, int splits,
+                                                   int64_t n, double *__restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    double a = 0.0;
+    for (int s = 0; s < splits; ++s) a += slabs[(int64_t)s * n + i];
+    out[i] = a;
+  }
+}
+
+int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t ldw, double *G) {
+  const int64_t tiles = ((k + 63) / 64) * ((k + 63) / 64);
+  int64_t splits = (1024 + tiles - 1) / tiles;
+  const int64_t max_splits = (ncols + 511) / 512;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  if (splits > 256) splits = 256;
+  if (splits == 1) {
+    gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, W, ldw, 0.0, G, k, 1, 0, ctx->stream);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  double *slabs = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&slabs, sizeof(double) * splits * k * k, ctx->stream));
+  gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, W, ldw, 0.0, slabs, k, (int)splits, k * k,
+              ctx->stream);
+  const int64_t n = k * k;
+  hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)),
+                     dim3(256), 0, ctx->stream, slabs, (int)splits, n, G);
+  MLFF_HIP(ctx, hipFreeAsync(slabs, ctx->stream));
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Unblocked Cholesky of the jb x jb diagonal block A[j0.., j0..] in LDS.
+__global__ __launch_bounds__(256) void k_potrf_diag(double *__restrict__ A, int64_t lda,
+                                                    int64_t j0, int jb, int *err) {
+  __shared__ double L[64][65];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < jb * jb; e += 256) {
+    const int i = e / jb, j = e % jb;
+    L[i][j] = A[(j0 + i) * lda + j0 + j];
+  }
+  __syncthreads();
+  for (int c = 0; c < jb; ++c) {
+    if (tid == 0) {
+      const double d = L[c][c];
+      if (!(d > 0.0)) atomicExch(err, 1);
+      L[c][c] = sqrt(d);
+    }
+    __syncthreads();
+    const double dc = L[c][c];
+    for (int i = c + 1 + tid; i < jb; i += 256) L[i][c] = L[i][c] / dc;
+    __syncthreads();
+    const int nt = jb - c - 1;
+    for (int e = tid; e < nt * nt; e += 256) {
+      const int i = c + 1 + e / nt, j = c + 1 + e % nt;
+      if (j <= i) L[i][j] = fma(-L[i][c], L[j][c], L[i][j]);
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < jb * jb; e += 256) {
+    const int i = e / jb, j = e % jb;
+    if (j <= i) A[(j0 + i) * lda + j0 + j] = L[i][j];
+  }
+}
+
+// Panel solve: rows i >= j0 + jb:  A[i, j0:j0+jb] <- A[i, j0:j0+jb] * L_dd^-T
+__global__ __launch_bounds__(64) void k_trsm_panel(double *__restrict__ A, int64_t lda,
+                                                   int64_t k, int64_t j0, int jb) {
+  __shared__ double L[64][65];
+  for (int e = threadIdx.x; e < jb * jb; e += 64) {
+    const int i = e / jb, j = e % jb;
+    L[i][j] = A[(j0 + i) * lda + j0 + j];
+  }
+  __syncthreads();
+  const int64_t i = j0 + jb + (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= k) return;
+  double x[64];
+  double *row = A + i * lda + j0;
+#pragma unroll
+  for (int c = 0; c < 64; ++c) x[c] = (c < jb) ? row[c] : 0.0;
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    if (c < jb) {
+      double v = x[c];
+#pragma unroll
+      for (int cc = 0; cc < c; ++cc) v = fma(-x[cc], L[c][cc], v);
+      x[c] = v / L[c][c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c)
+    if (c < jb) row[c] = x[c];
+}
+
+__global__ void k_zero_upper(double *A, int64_t k) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < k * k;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / k, j = e % k;
+    if (j > i) A[e] = 0.0;
+  }
+}
+
+void launch_zero_upper(double *A, int64_t k, hipStream_t s) {
+  const int64_t n = k * k;
+  hipLaunchKernelGGL(k_zero_upper, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
+                     dim3(256), 0, s, A, k);
+}
+
+__global__ void k_add_diag(double *A, int64_t k, double v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < k) A[i * k + i] += v;
+}
+
+void launch_add_diag(double *A, int64_t k, double v, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_diag, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, A, k, v);
+}
+
+int potrf_lower(mlff_ctx *ctx, double *A, int64_t k) {
+  int *err = &ctx->st->linalg_err;
+  MLFF_HIP(ctx, hipMemsetAsync(err, 0, sizeof(int), ctx->stream));
+  for (int64_t j0 = 0; j0 < k; j0 += 64) {
+    const int jb = (int)std::min<int64_t>(64, k - j0);
+    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, k, j0, jb, err);
+    const int64_t rest = k - j0 - jb;
+    if (rest > 0) {
+      hipLaunchKernelGGL(k_trsm_panel, dim3((unsigned)((rest + 63) / 64)), dim3(64), 0,
+                         ctx->stream, A, k, k, j0, jb);
+      const double *P = A + (j0 + jb) * k + j0;
+      gemm_launch(false, true, rest, rest, jb, -1.0, P, k, P, k, 1.0, A + (j0 + jb) * k + j0 + jb,
+                  k, 1, 0, ctx->stream);
+    }
+  }
+  launch_zero_upper(A, k, ctx->stream);
+  MLFF_HIP(ctx, hipGetLastError());
+  int h_err = 0;
+  MLFF_HIP(ctx, hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (h_err) return set_error(ctx, MLFF_ERR_LINALG, "Cholesky factorization failed: matrix is not positive definite");
+  return MLFF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// W[i0:i0+ib, :] <- L_ii^-1 W[i0:i0+ib, :], one thread per column.
+__global__ __launch_bounds__(256) void k_trsm_diag_wide(const double *__restrict__ Lm, int64_t k,
+                                                        int64_t i0, int ib,
+                                                        double *__restrict__ W, int64_t ldw,
+                                                        int64_t ncols) {
+  __shared__ double L[64][65];
+  for (int e = threadIdx.x; e < ib * ib; e += 256) {
+    const int i = e / ib, j = e % ib;
+    L[i][j] = Lm[(i0 + i) * k + i0 + j];
+  }
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= ncols) return;
+  double x[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) x[r] = (r < ib) ? W[(i0 + r) * ldw + c] : 0.0;
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    if (r < ib) {
+      double v = x[r];
+#pragma unroll
+      for (int rr = 0; rr < r; ++rr) v = fma(-L[r][rr], x[rr], v);
+      x[r] = v / L[r][r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 64; ++r)
+    if (r < ib) W[(i0 + r) * ldw + c] = x[r];
+}
+
+int trsm_lower_wide(mlff_ctx *ctx, const double *L, int64_t k, double *W, int64_t ncols,
+                    int64_t ldw) {
+  for (int64_t i0 = 0; i0 < k; i0 += 64) {
+    const int ib = (int)std::min<int64_t>(64, k - i0);
+    if (i0 > 0)
+      gemm_launch(false, false, ib, ncols, i0, -1.0, L + i0 * k, k, W, ldw, 1.0, W + i0 * ldw,
+                  ldw, 1, 0, ctx->stream);
+    hipLaunchKernelGGL(k_trsm_diag_wide, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0,
+                       ctx->stream, L, k, i0, ib, W, ldw, ncols);
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
+}
+
+__global__ __launch_bounds__(256) void k_colsumsq(const double *__restrict__ W, int64_t k,
+                                                  int64_t ncols, int64_t ldw,
+                                                  double *__restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= ncols) return;
+  double a = 0.0;
+  for (int64_t j = 0; j < k; ++j) {
+    const double v = W[j * ldw + c];
+    a = fma(v, v, a);
+  }
+  out[c] = a;
+}
+
+void launch_colsumsq(const double *W, int64_t k, int64_t ncols, int64_t ldw, double *out,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_colsumsq, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, s, W, k,
+                     ncols, ldw, out);
+}
+
+}  // namespace mlff

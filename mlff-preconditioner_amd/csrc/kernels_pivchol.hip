@@ -1,0 +1,227 @@
+// Greedy diagonal-pivoted partial Cholesky of S = sigma_K * K on the device.
+// Restates src/sGDML/sgdml/solvers/incomplete_cholesky.py:24-93:
+//   i_argmax = argmax(diag[index_columns][m:]) + m        (first max in permuted order, :53)
+//   swap index_columns[m], index_columns[i_argmax]          (:55)
+//   L[m_pi, m] = sqrt(diag[m_pi]); assert pivot > 0        (:61-63)
+//   L[i_pi, m] = (col[i_pi] - L[i_pi, :m] . L[m_pi, :m]) / L[m_pi, m]   (:66-75)
+//   diag[i_pi] -= L[i_pi, m]^2                              (:78)
+// where col = get_col(m_pi) = column m_pi of the operator (iterative_cholesky.py:152-156).
+// L is kept transposed (Lt: k x blk, rows = pivot steps, columns = original row
+// index), which is exactly the "wide" panel the Woodbury build consumes.
+// Multi-rank: the argmax is an allgather of per-rank (value, position) winners,
+// the pivot row L[m_pi, :m] an allreduce of a vector only its owner fills.
+#include "common.h"
+
+namespace mlff {
+
+struct ArgMax {
+  double v;
+  long long pos;
+};
+
+__device__ __forceinline__ bool better(double v, long long pos, double bv, long long bpos) {
+  // larger value wins; ties (and NaN-free equality) go to the smaller position
+  if (v > bv) return true;
+  if (v == bv && pos < bpos) return true;
+  return false;
+}
+
+// partial argmax over positions [m, N) of dwork[perm[pos] - row0] (local entries only)
+__global__ __launch_bounds__(256) void k_piv_argmax(const double *__restrict__ dwork,
+                                                    const int64_t *__restrict__ perm, int64_t N,
+                                                    int64_t m, int64_t row0, int64_t nrows,
+                                                    double *__restrict__ pv,
+                                                    long long *__restrict__ pp) {
+  __shared__ double sv[256];
+  __shared__ long long sp[256];
+  double bv = -INFINITY;
+  long long bp = (long long)N;
+  for (int64_t pos = m + (int64_t)blockIdx.x * 256 + threadIdx.x; pos < N;
+       pos += (int64_t)gridDim.x * 256) {
+    const int64_t g = perm[pos] - row0;
+    if (g >= 0 && g < nrows) {
+      const double v = dwork[g];
+      if (better(v, pos, bv, bp)) {
+        bv = v;
+        bp = pos;
+      }
+    }
+  }
+  sv[threadIdx.x] = bv;
+  sp[threadIdx.x] = bp;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      if (better(sv[threadIdx.x + o], sp[threadIdx.x + o], sv[threadIdx.x], sp[threadIdx.x])) {
+        sv[threadIdx.x] = sv[threadIdx.x + o];
+        sp[threadIdx.x] = sp[threadIdx.x + o];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    pv[blockIdx.x] = sv[0];
+    pp[blockIdx.x] = sp[0];
+  }
+}
+
+// reduce the per-workgroup winners of this rank into rank_win[0..1] (value, pos as double)
+__global__ __launch_bounds__(256) void k_piv_rank_winner(const double *__restrict__ pv,
+                                                         const long long *__restrict__ pp, int np,
+                                                         double *__restrict__ rank_win) {
+  __shared__ double sv[256];
+  __shared__ long long sp[256];
+  double bv = -INFINITY;
+  long long bp = LLONG_MAX;
+  for (int t = threadIdx.x; t < np; t += 256)
+    if (better(pv[t], pp[t], bv, bp)) {
+      bv = pv[t];
+      bp = pp[t];
+    }
+  sv[threadIdx.x] = bv;
+  sp[threadIdx.x] = bp;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      if (better(sv[threadIdx.x + o], sp[threadIdx.x + o], sv[threadIdx.x], sp[threadIdx.x])) {
+        sv[threadIdx.x] = sv[threadIdx.x + o];
+        sp[threadIdx.x] = sp[threadIdx.x + o];
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    rank_win[0] = sv[0];
+    rank_win[1] = (double)sp[0];  // exact for positions < 2^53
+  }
+}
+
+// global winner over ranks; swap; pivot; owner writes Lt[m, m_pi] and the pivot row
+__global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__ wins, int world,
+                                                      int64_t *__restrict__ perm, int64_t m,
+                                                      int64_t row0, int64_t nrows,
+                                                      double *__restrict__ Lt, int64_t ldl,
+                                                      int *__restrict__ pivflag,
+                                                      double *__restrict__ prow,
+                                                      DevState *st) {
+  __shared__ long long s_mpi;
+  __shared__ double s_sq;
+  if (threadIdx.x == 0) {
+    double bv = -INFINITY;
+    long long bp = LLONG_MAX;
+    for (int r = 0; r < world; ++r) {
+      const double v = wins[2 * r];
+      const long long p = (long long)wins[2 * r + 1];
+      if (better(v, p, bv, bp)) {
+        bv = v;
+        bp = p;
+      }
+    }
+    long long mpi = -1;
+    double sq = 0.0;
+    if (bp >= m && bp < (long long)0x7fffffffffffffffLL && bv == bv && bv > -INFINITY) {
+      const int64_t tmp = perm[m];
+      perm[m] = perm[bp];
+      perm[bp] = tmp;
+      mpi = perm[m];
+      if (!(bv > 0.0)) st->pivot_err = 1;
+      sq = sqrt(bv);
+    } else {
+      st->pivot_err = 1;
+    }
+    st->m_pi = mpi;
+    st->sqrt_piv = sq;
+    s_mpi = mpi;
+    s_sq = sq;
+  }
+  __syncthreads();
+  const long long mpi = s_mpi;
+  const int64_t g = mpi - row0;
+  const bool own = (mpi >= 0 && g >= 0 && g < nrows);
+  // pivot row L[m_pi, :m] = Lt[:m, m_pi] (zeros on non-owner ranks: summed by allreduce)
+  for (int64_t c = threadIdx.x; c < m; c += 256) prow[c] = own ? Lt[c * ldl + g] : 0.0;
+  if (threadIdx.x == 0 && own) {
+    Lt[m * ldl + g] = s_sq;
+    pivflag[g] = 1;
+  }
+}
+
+// new column of L for every not-yet-pivoted local row i:
+//   Lt[m, i] = (S[i, m_pi] - sum_{c<m} Lt[c, i] prow[c]) / sqrt_piv;  dwork[i] -= Lt[m,i]^2
+__global__ __launch_bounds__(256) void k_piv_column(const double *__restrict__ K, int64_t ld,
+                                                    double sigma, int64_t rows_per, int64_t blk,
+                                                    int64_t nrows, int64_t m,
+                                                    double *__restrict__ Lt, int64_t ldl,
+                                                    const double *__restrict__ prow,
+                                                    const int *__restrict__ pivflag,
+                                                    double *__restrict__ dwork,
+                                                    const DevState *__restrict__ st) {
+  extern __shared__ double ps[];
+  const long long mpi = st->m_pi;
+  if (mpi < 0) return;
+  const double sq = st->sqrt_piv;
+  for (int64_t c = threadIdx.x; c < m; c += 256) ps[c] = prow[c];
+  __syncthreads();
+  const int64_t pos = (mpi / rows_per) * blk + (mpi % rows_per);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrows;
+       i += (int64_t)gridDim.x * 256) {
+    if (pivflag[i]) continue;
+    const double col = sigma * K[i * ld + pos];
+    double s0 = 0.0;
+    for (int64_t c = 0; c < m; ++c) s0 = fma(Lt[c * ldl + i], ps[c], s0);
+    const double v = (col - s0) / sq;
+    Lt[m * ldl + i] = v;
+    dwork[i] -= v * v;
+  }
+}
+
+int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
+  hipStream_t s = ctx->stream;
+  const int64_t N = ctx->N, nrows = ctx->nrows, blk = ctx->blk;
+  const int np = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + 1023) / 1024));
+  double *pv = nullptr, *wins = nullptr;
+  long long *pp = nullptr;
+  MLFF_HIP(ctx, hipMallocAsync(&pv, sizeof(double) * np, s));
+  MLFF_HIP(ctx, hipMallocAsync(&pp, sizeof(long long) * np, s));
+  MLFF_HIP(ctx, hipMallocAsync(&wins, sizeof(double) * 2 * ctx->world, s));
+  // init: perm = arange(N), dwork = diag(S), pivflag = 0, Lt = 0
+  std::vector<int64_t> hperm(N);
+  for (int64_t i = 0; i < N; ++i) hperm[i] = i;
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->perm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
+  launch_diag_of(ctx->K, ctx->ld, nrows, ctx->row0, ctx->rows_per, blk, ctx->sigma_K, ctx->dwork, s);
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
+  MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
+  const unsigned gcol = (unsigned)std::min<int64_t>((nrows + 255) / 256, 1024);
+  for (int64_t m = 0; m < k; ++m) {
+    hipLaunchKernelGGL(k_piv_argmax, dim3(np), dim3(256), 0, s, ctx->dwork, ctx->perm, N, m,
+                       ctx->row0, nrows, pv, pp);
+    double *my = wins + 2 * ctx->rank;
+    hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
+    if (ctx->world > 1)
+      MLFF_NCCL(ctx, ncclAllGather(my, wins, 2, ncclDouble, ctx->comm, s));
+    hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world, ctx->perm, m,
+                       ctx->row0, nrows, ctx->T, blk, ctx->pivflag, ctx->prow, ctx->st);
+    if (ctx->world > 1 && m > 0)
+      MLFF_NCCL(ctx, ncclAllReduce(ctx->prow, ctx->prow, m, ncclDouble, ncclSum, ctx->comm, s));
+    hipLaunchKernelGGL(k_piv_column, dim3(gcol), dim3(256), sizeof(double) * (m + 1), s, ctx->K,
+                       ctx->ld, ctx->sigma_K, ctx->rows_per, blk, nrows, m, ctx->T, blk,
+                       ctx->prow, ctx->pivflag, ctx->dwork, ctx->st);
+    if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  int perr = 0;
+  MLFF_HIP(ctx, hipMemcpyAsync(&perr, &ctx->st->pivot_err, sizeof(int), hipMemcpyDeviceToHost, s));
+  if (index_columns_out != nullptr)
+    MLFF_HIP(ctx, hipMemcpyAsync(index_columns_out, ctx->perm, sizeof(int64_t) * N,
+                                 hipMemcpyDeviceToHost, s));
+  MLFF_HIP(ctx, hipFreeAsync(pv, s));
+  MLFF_HIP(ctx, hipFreeAsync(pp, s));
+  MLFF_HIP(ctx, hipFreeAsync(wins, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  if (perr)
+    return set_error(ctx, MLFF_ERR_NOT_PSD,
+                     "given matrix is not PSD (pivot <= 0 in pivoted Cholesky)");
+  return MLFF_OK;
+}
+
+}  // namespace mlff

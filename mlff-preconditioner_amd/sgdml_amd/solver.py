@@ -1,0 +1,280 @@
+"""KernelSolver: one GPU (one rank) of the MI355X PCG solver.
+
+Thin object wrapper over the C ABI (include/mlffpcg.h).  It owns a device
+context holding this rank's row block of the dense kernel matrix K, the operator
+A = sigma_K * K + lam * I, an optional low-rank preconditioner and the PCG state.
+
+    s = KernelSolver(n)                       # single GPU
+    s.gen_rbf(X, length_scale=0.2)            # or set_matrix / assemble_sgdml
+    s.set_operator(sigma_K=+1.0, lam=1e-6)
+    s.precon_nystrom(idx)                     # or precon_pivchol(k) / precon_none()
+    res = s.pcg(b, tol=1e-6, maxiter=5 * n)
+
+Multi-GPU: one process per GPU; every rank constructs KernelSolver(n, rank=r,
+world=W, comm_id=id) with the same RCCL id (sgdml_amd.distributed.make_comm_id)
+and passes its own row block (row_range()).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _native as nat
+
+
+@dataclass
+class PCGResult:
+    x: np.ndarray            # local solution block
+    info: int                # scipy convention: 0 converged, maxiter otherwise
+    iters: int               # CG iterations performed (scipy ITER)
+    resid: float             # last stop-test ||r|| (true residual after the recheck)
+    trace: np.ndarray        # ||r_0||, ||r_1||, ..., ||r_iters||
+    early_exit: bool = False  # legacy pre-check ||A x0 - b|| <= tol ended the solve
+    callbacks: int = 0       # number of scipy callback invocations this solve maps to
+    extra: dict = field(default_factory=dict)
+
+
+class KernelSolver:
+    def __init__(self, n: int, device: int | None = None, rank: int = 0, world: int = 1,
+                 comm_id: bytes | None = None):
+        self._lib = nat.load_library()
+        self.n = int(n)
+        self.rank, self.world = int(rank), int(world)
+        if device is None:
+            ndev = nat.device_count()
+            device = rank % max(ndev, 1)
+        self.device = int(device)
+        ctx = ctypes.c_void_p()
+        cid = None if comm_id is None else ctypes.c_char_p(bytes(comm_id))
+        nat.check(self._lib.mlff_ctx_create(self.device, self.rank, self.world, cid, self.n,
+                                            ctypes.byref(ctx)), None, "mlff_ctx_create")
+        self._ctx = ctx
+        r0, nr = ctypes.c_int64(), ctypes.c_int64()
+        self._call("mlff_shard_range", ctypes.byref(r0), ctypes.byref(nr))
+        self.row0, self.nrows = r0.value, nr.value
+
+    # ------------------------------------------------------------------ basics
+    def _call(self, name, *args):
+        rc = getattr(self._lib, name)(self._ctx, *args)
+        nat.check(rc, self._ctx, name)
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value is not None:
+            self._lib.mlff_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def row_range(self) -> tuple[int, int]:
+        return self.row0, self.row0 + self.nrows
+
+    def synchronize(self):
+        self._call("mlff_synchronize")
+
+    def stream_handle(self) -> int:
+        p = ctypes.c_void_p()
+        self._call("mlff_stream", ctypes.byref(p))
+        return p.value or 0
+
+    # ------------------------------------------------------------------ matrix
+    def set_matrix(self, K_local: np.ndarray):
+        """K_local: this rank's rows (nrows x N) of K."""
+        K_local = np.ascontiguousarray(K_local, dtype=np.float64)
+        if K_local.shape != (self.nrows, self.n):
+            raise ValueError(f"K_local must have shape {(self.nrows, self.n)}, got {K_local.shape}")
+        self._call("mlff_set_matrix_host", nat.dptr(K_local), self.n)
+
+    def get_matrix_rows(self, r0: int = 0, nr: int | None = None) -> np.ndarray:
+        nr = self.nrows - r0 if nr is None else nr
+        out = np.empty((nr, self.n))
+        self._call("mlff_get_matrix_rows", int(r0), int(nr), nat.dptr(out), self.n)
+        return out
+
+    def gen_rbf(self, X: np.ndarray, length_scale: float = 1.0, jitter: float = 0.0):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        if X.ndim != 2 or X.shape[0] != self.n:
+            raise ValueError("X must be N x d")
+        self._call("mlff_gen_rbf", nat.dptr(X), int(X.shape[1]), float(length_scale), float(jitter))
+
+    def assemble_sgdml(self, R_desc: np.ndarray, R_d_desc: np.ndarray, perms: np.ndarray,
+                       sig: float):
+        R_desc = np.ascontiguousarray(R_desc, dtype=np.float64)
+        R_d_desc = np.ascontiguousarray(R_d_desc, dtype=np.float64)
+        perms = np.ascontiguousarray(np.atleast_2d(perms), dtype=np.int32)
+        M, D = R_desc.shape
+        n_atoms = perms.shape[1]
+        if R_d_desc.shape != (M, D, 3) or D != n_atoms * (n_atoms - 1) // 2:
+            raise ValueError("R_desc / R_d_desc / perms shapes are inconsistent")
+        self._call("mlff_assemble_sgdml", nat.dptr(R_desc), nat.dptr(R_d_desc), int(M),
+                   int(n_atoms), nat.i32ptr(perms), int(perms.shape[0]), float(sig))
+
+    def set_operator(self, sigma_K: float, lam: float):
+        self._call("mlff_set_operator", float(sigma_K), float(lam))
+
+    def matvec(self, v: np.ndarray) -> np.ndarray:
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        if v.shape != (self.n,):
+            raise ValueError("v must have N entries")
+        y = np.empty(self.nrows)
+        self._call("mlff_matvec", nat.dptr(v), nat.dptr(y))
+        return y
+
+    def diag(self) -> np.ndarray:
+        d = np.empty(self.nrows)
+        self._call("mlff_get_diag", nat.dptr(d))
+        return d
+
+    # ------------------------------------------------------------ preconditioner
+    def precon_none(self):
+        self._call("mlff_precon_none")
+
+    def precon_pivchol(self, k: int, build_woodbury: bool = True):
+        """Pivoted Cholesky of S = sigma_K K to rank k (+ Woodbury).  Returns
+        (index_columns (N,), seconds)."""
+        idx = np.empty(self.n, dtype=np.int64)
+        sec = ctypes.c_double()
+        self._call("mlff_precon_pivchol", int(k), int(bool(build_woodbury)), nat.i64ptr(idx),
+                   ctypes.byref(sec))
+        return idx, sec.value
+
+    def precon_nystrom(self, idx: np.ndarray, variant: int = 0) -> float:
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        sec = ctypes.c_double()
+        self._call("mlff_precon_nystrom", nat.i64ptr(idx), int(idx.size), int(variant),
+                   ctypes.byref(sec))
+        return sec.value
+
+    def precon_lowrank(self, Lt_local: np.ndarray):
+        Lt_local = np.ascontiguousarray(Lt_local, dtype=np.float64)
+        k = Lt_local.shape[0]
+        if Lt_local.shape != (k, self.nrows):
+            raise ValueError("Lt_local must be k x nrows")
+        self._call("mlff_precon_lowrank", nat.dptr(Lt_local), int(k))
+
+    def precon_info(self) -> tuple[int, int]:
+        kind, k = ctypes.c_int(), ctypes.c_int64()
+        self._call("mlff_precon_info", ctypes.byref(kind), ctypes.byref(k))
+        return kind.value, k.value
+
+    def precon_apply(self, r_local: np.ndarray) -> np.ndarray:
+        r_local = np.ascontiguousarray(r_local, dtype=np.float64)
+        z = np.empty(self.nrows)
+        self._call("mlff_precon_apply", nat.dptr(r_local), nat.dptr(z))
+        return z
+
+    def precon_panel(self) -> np.ndarray:
+        _, k = self.precon_info()
+        T = np.empty((k, self.nrows))
+        self._call("mlff_precon_get_panel", nat.dptr(T), self.nrows)
+        return T
+
+    def lev_scores(self, idx: np.ndarray, lam: float) -> np.ndarray:
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        out = np.empty(self.n)
+        self._call("mlff_lev_scores", nat.i64ptr(idx), int(idx.size), float(lam), nat.dptr(out))
+        return out
+
+    # ---------------------------------------------------------------------- PCG
+    def pcg_start(self, b_local: np.ndarray, x0_local: np.ndarray | None = None,
+                  tol: float = 1e-5, maxiter: int | None = None) -> bool:
+        b_local = np.ascontiguousarray(b_local, dtype=np.float64)
+        if b_local.shape != (self.nrows,):
+            raise ValueError("b_local must have nrows entries")
+        x0p = None
+        if x0_local is not None:
+            x0_local = np.ascontiguousarray(x0_local, dtype=np.float64)
+            if x0_local.shape != (self.nrows,):
+                raise ValueError("x0_local must have nrows entries")
+            x0p = nat.dptr(x0_local)
+        maxiter = 10 * self.n if maxiter is None else int(maxiter)
+        early = ctypes.c_int()
+        self._call("mlff_pcg_start", nat.dptr(b_local), x0p, float(tol), maxiter,
+                   ctypes.byref(early))
+        self._maxiter = maxiter
+        return bool(early.value)
+
+    def pcg_run(self, n_iter: int, chunk: int = 0) -> int:
+        st = ctypes.c_int()
+        self._call("mlff_pcg_run", int(n_iter), int(chunk), ctypes.byref(st))
+        return st.value
+
+    def pcg_result(self) -> tuple[int, int, float, int]:
+        it, st, res, info = ctypes.c_int64(), ctypes.c_int(), ctypes.c_double(), ctypes.c_int()
+        self._call("mlff_pcg_result", ctypes.byref(it), ctypes.byref(st), ctypes.byref(res),
+                   ctypes.byref(info))
+        return it.value, st.value, res.value, info.value
+
+    def pcg_x(self) -> np.ndarray:
+        x = np.empty(self.nrows)
+        self._call("mlff_pcg_get_x", nat.dptr(x))
+        return x
+
+    def pcg_trace(self) -> np.ndarray:
+        it = self.pcg_result()[0]
+        t = np.empty(it + 1)
+        self._call("mlff_pcg_get_trace", nat.dptr(t), it + 1)
+        return t
+
+    def pcg(self, b_local: np.ndarray, x0_local: np.ndarray | None = None, tol: float = 1e-5,
+            maxiter: int | None = None, callback=None, cb_every: int = 0,
+            chunk: int = 0) -> PCGResult:
+        """Full solve with scipy-1.7.3 `cg(A, b, x0, tol, atol=None, maxiter, M)` semantics.
+
+        callback(x_local, iters, resid) is called every `cb_every` iterations (the
+        reference's 2-minute checkpoint / progress hook, iterative_solver.py:874-965)."""
+        early = self.pcg_start(b_local, x0_local, tol, maxiter)
+        status = self.pcg_result()[1]
+        step = int(cb_every) if cb_every and cb_every > 0 else self._maxiter
+        while status == nat.PCG_RUNNING:
+            status = self.pcg_run(step, chunk)
+            if callback is not None and status == nat.PCG_RUNNING:
+                it, _, res, _ = self.pcg_result()
+                callback(self.pcg_x(), it, res)
+        it, status, resid, info = self.pcg_result()
+        x = self.pcg_x()
+        trace = self.pcg_trace()
+        # scipy 1.7.3 calls callback(x) at the start of iterations 2..m and once at the
+        # end: m calls for m >= 1 iterations, one call when ||r0|| < atol, none on the
+        # legacy early exit.
+        callbacks = 0 if early else max(it, 1)
+        return PCGResult(x=x, info=info, iters=it, resid=resid, trace=trace,
+                         early_exit=early, callbacks=callbacks)
+
+    # ------------------------------------------------------------------- timing
+    def timing(self, on: bool = True):
+        self._call("mlff_timing_enable", int(bool(on)))
+
+    def timing_reset(self):
+        self._call("mlff_timing_reset")
+
+    def timing_read(self) -> dict:
+        gm, gc, im, ic = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
+        self._call("mlff_timing_read", ctypes.byref(gm), ctypes.byref(gc), ctypes.byref(im),
+                   ctypes.byref(ic))
+        return {"gemv_ms": gm.value, "gemv_count": gc.value, "iter_ms": im.value,
+                "iter_count": ic.value}
+
+
+def sgdml_descriptors(R: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Desc.from_R on the GPU (desc.py:292-358; no cutoff, no PBC).  R: M x n_atoms x 3."""
+    lib = nat.load_library()
+    R = np.ascontiguousarray(R, dtype=np.float64)
+    M, n = R.shape[0], R.shape[1]
+    D = n * (n - 1) // 2
+    Rd = np.empty((M, D))
+    Rdd = np.empty((M, D, 3))
+    nat.check(lib.mlff_sgdml_descriptors(nat.dptr(R), M, n, nat.dptr(Rd), nat.dptr(Rdd)), None,
+              "mlff_sgdml_descriptors")
+    return Rd, Rdd

@@ -1,0 +1,52 @@
+"""Shared parity criteria (calibrated on the golden fixtures).
+
+The sGDML systems are solved at lam = 1e-10 (cond(-K + lam I) ~ 1e9 already at
+N = 270).  Two regimes, both measured with the CPU oracle against the reference
+outputs and against itself under re-ordered summation (the noise floor):
+
+* stable:   identical iteration counts, |log10(r_k / r_k_ref)| <= 1e-4 pointwise,
+            ||dx|| / ||x|| <= 1e-6.
+* chaotic:  the residual curves agree to ~1e-12 for the first iterations and then
+            drift apart (a re-blocked NumPy mat-vec moves the count 144 -> 145
+            where the reference took 137 on sgdml_ethanol_n270/cholesky), while the
+            converged solutions still agree to ~1e-8.  Contract: both converged,
+            iteration count within 10 % (at least +-3), the first iterations
+            pointwise within 1e-6 in log10, every half-decade crossing of the
+            running-minimum residual within 10 % (+3) iterations of the
+            reference's, ||dx|| / ||x|| <= 1e-6.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def envelope(trace):
+    return np.minimum.accumulate(np.asarray(trace))
+
+
+def assert_pcg_parity(iters, trace, x, ref_iters, ref_trace, ref_x, mode="chaotic",
+                      head=8, x_tol=1e-6, iter_frac=0.10):
+    """trace / ref_trace: stop-test residuals of iterations 1..m (no r0 entry)."""
+    trace = np.asarray(trace)
+    ref_trace = np.asarray(ref_trace)
+    if mode == "stable":
+        assert iters == ref_iters, (iters, ref_iters)
+        m = min(len(trace), len(ref_trace))
+        d = np.abs(np.log10(trace[:m] / ref_trace[:m]))
+        assert d.max() <= 1e-4, d.max()
+    else:
+        slack = max(3, int(np.ceil(iter_frac * ref_iters)))
+        assert abs(iters - ref_iters) <= slack, (iters, ref_iters)
+        h = min(head, len(trace), len(ref_trace))
+        d = np.abs(np.log10(trace[:h] / ref_trace[:h]))
+        assert d.max() <= 1e-6, d
+        # decade crossings of the running minimum happen at nearly the same iteration
+        ea, eb = envelope(trace), envelope(ref_trace)
+        top, bot = np.log10(eb[0]), np.log10(max(eb[-1], ea[-1]))
+        for lvl in np.arange(np.floor(top) - 0.5, bot, -0.5):
+            ia = int(np.argmax(ea <= 10 ** lvl)) if np.any(ea <= 10 ** lvl) else len(ea)
+            ib = int(np.argmax(eb <= 10 ** lvl)) if np.any(eb <= 10 ** lvl) else len(eb)
+            assert abs(ia - ib) <= max(3, int(np.ceil(iter_frac * ib)) + 3), (lvl, ia, ib)
+    if x is not None and ref_x is not None:
+        rel = np.linalg.norm(np.asarray(x) - np.asarray(ref_x)) / np.linalg.norm(ref_x)
+        assert rel <= x_tol, rel

@@ -1,0 +1,73 @@
+"""The C-ABI library loads and exports every entry point include/mlffpcg.h
+declares; host-side argument validation works without a GPU.  CPU only."""
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+HEADER = REPO / "include" / "mlffpcg.h"
+
+
+def declared_symbols():
+    text = HEADER.read_text()
+    return sorted(set(re.findall(r"\b(mlff_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_matches_binding_table():
+    from sgdml_amd import _native
+
+    assert declared_symbols() == sorted(_native.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    from sgdml_amd import _native
+
+    lib = _native.load_library()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    assert lib.mlff_version() == 100
+
+
+def test_library_is_gfx950_code_object():
+    import subprocess
+
+    from sgdml_amd import _native
+
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-n", "--wide", str(_native.LIB_PATH)],
+                         capture_output=True, text=True)
+    blob = _native.LIB_PATH.read_bytes()
+    assert b"gfx950" in blob, "no gfx950 code object embedded"
+
+
+def test_errors_map_to_reference_exception_types():
+    from sgdml_amd import _native
+
+    lib = _native.load_library()
+    with pytest.raises(ValueError):
+        _native.check(_native.MLFF_ERR_ARG, None, "x")
+    with pytest.raises(AssertionError):
+        _native.check(_native.MLFF_ERR_NOT_PSD, None, "x")
+    with pytest.raises(np.linalg.LinAlgError):
+        _native.check(_native.MLFF_ERR_LINALG, None, "x")
+    with pytest.raises(RuntimeError):
+        _native.check(_native.MLFF_ERR_HIP, None, "x")
+    _native.check(_native.MLFF_OK)
+    assert isinstance(lib.mlff_last_error(None), bytes)
+
+
+def test_ctx_create_validates_arguments_before_touching_a_device():
+    import ctypes
+
+    from sgdml_amd import _native
+
+    lib = _native.load_library()
+    ctx = ctypes.c_void_p()
+    assert lib.mlff_ctx_create(0, 2, 2, None, 10, ctypes.byref(ctx)) == _native.MLFF_ERR_ARG
+    assert lib.mlff_ctx_create(0, 0, 1, None, 0, ctypes.byref(ctx)) == _native.MLFF_ERR_ARG
+    assert lib.mlff_ctx_create(0, 0, 2, None, 10, ctypes.byref(ctx)) == _native.MLFF_ERR_ARG
+    assert ctx.value is None
+    # null-context calls are rejected, not dereferenced
+    assert lib.mlff_pcg_run(None, 1, 1, None) == _native.MLFF_ERR_ARG
+    assert lib.mlff_matvec(None, None, None) == _native.MLFF_ERR_ARG
