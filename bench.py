@@ -1,0 +1,275 @@
+"""bench.py — PCG iterations/s on the north-star workload (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 65536] [--k 256]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[2]): synthetic SPD RBF
+kernel, N = 65536 points x ~ U[0,1)^3 (numpy default_rng seed 0), length scale
+0.2, A = K + 1e-6 I, b = sum(x^2), rank-256 Nystrom preconditioner on uniform
+random columns (`random_scores`, seed 0).  K is generated on the GPU (inputs
+resident in HBM before the timed region).  A step = one PCG iteration (the
+fp64 mat-vec over the whole N x N matrix + preconditioner apply + CG updates).
+With N GPUs the same problem is row-sharded (strong scaling); the mat-vec
+operand is all-gathered and the dot products all-reduced over RCCL.
+
+Prints one JSON line (rank 0) with the driver's keys plus
+  roofline:     bytes/launch of the K mat-vec (8 N_local N + 16 N_local) / its mean
+                HIP-event duration, against 8 TB/s; traffic from profiles/ (PMC) or null
+  cpu_baseline: the NumPy/SciPy oracle (oracle/, a port of the reference's CPU
+                path) timed on this host on a bounded number of PCG iterations
+                of the same matrix (rank 0, N = 1 only)
+  parity:       iterations to relres 1e-6 on GPU vs the CPU oracle on an N = 8192
+                instance of the same generator (rank 0, N = 1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path[:0] = [str(REPO), str(REPO / "mlff-preconditioner_amd")]
+
+import numpy as np  # noqa: E402
+
+METRIC = "CG iters/sec + GB/s on N×N fp64 kernel mat-vec; iters-to-1e-6 vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--k", type=int, default=256)
+    ap.add_argument("--lam", type=float, default=1e-6)
+    ap.add_argument("--ell", type=float, default=0.2)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-1e-6 legs")
+    ap.add_argument("--cpu-iters", type=int, default=12)
+    ap.add_argument("--solve-maxiter", type=int, default=20000)
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl")
+        pg = dist
+    return rank, world, local, pg
+
+
+def barrier(pg, solver):
+    solver.synchronize()
+    if pg is not None:
+        import torch
+
+        torch.cuda.synchronize()
+        pg.barrier()
+
+
+def max_over_ranks(pg, v: float) -> float:
+    if pg is None:
+        return v
+    import torch
+
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_solver(n, rank, world, local, pg):
+    import sgdml_amd
+
+    comm_id = None
+    if world > 1:
+        obj = [sgdml_amd.comm_unique_id() if rank == 0 else None]
+        pg.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    return sgdml_amd.KernelSolver(n, device=local, rank=rank, world=world, comm_id=comm_id)
+
+
+def pmc_traffic(workload: str, world: int):
+    p = REPO / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        e = d.get(f"{workload}/gpus{world}")
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def cpu_baseline(solver, X, b, idx, lam, ell, iters):
+    """Oracle PCG iterations (NumPy/SciPy port of the reference CPU path) on the same
+    matrix, copied from the device; timed per iteration after one warm-up iteration."""
+    import threadpoolctl
+
+    from oracle.pcg import cg_legacy
+    from oracle.precon import apply_panel, nystrom_panel
+
+    n = b.size
+    K = solver.get_matrix_rows()
+    B, sp = nystrom_panel(K[:, idx], idx, lam, 0)
+    info = threadpoolctl.threadpool_info()
+    threads = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+
+    def mv(v):
+        y = K @ v
+        y += lam * v
+        return y
+
+    cg_legacy(mv, b, tol=0.0, maxiter=1, psolve=lambda r: apply_panel(B, sp, lam, r))
+    t0 = time.perf_counter()
+    cg_legacy(mv, b, tol=0.0, maxiter=iters, psolve=lambda r: apply_panel(B, sp, lam, r))
+    el = time.perf_counter() - t0 - 0.0
+    # cg_legacy spends one extra mat-vec on the legacy ||A x0 - b|| check
+    t_mv = time.perf_counter()
+    mv(b)
+    t_mv = time.perf_counter() - t_mv
+    per_it = max(el - t_mv, 1e-9) / iters
+    del K
+    return {"value": 1.0 / per_it, "unit": "CG iters/s", "cores": int(threads), "kind": "port",
+            "sample": f"{iters} PCG iterations (oracle cg_legacy + Nystrom apply, NumPy/OpenBLAS) "
+                      f"on the same N={n} fp64 matrix copied from the GPU",
+            "ms_per_iter": per_it * 1e3,
+            "matvec_gbs": (8.0 * n * n) / (t_mv * 1e9)}
+
+
+def parity_small(n, k, lam, ell, tol=1e-6):
+    """Same generator at N = 8192: GPU vs CPU-oracle iterations to relres 1e-6."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    from oracle.pcg import cg_legacy
+    from oracle.precon import apply_panel, nystrom_panel
+    from oracle.rbf import rbf_kernel
+
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    with sgdml_amd.KernelSolver(n) as s:
+        s.gen_rbf(X, ell)
+        s.set_operator(1.0, lam)
+        s.precon_nystrom(idx)
+        r = s.pcg(b, tol=tol, maxiter=min(5 * n, 10000))
+    K = rbf_kernel(X, ell)
+    B, sp = nystrom_panel(K[:, idx], idx, lam, 0)
+    x, info, tr, it = cg_legacy(lambda v: K @ v + lam * v, b, tol=tol, maxiter=min(5 * n, 10000),
+                                psolve=lambda v: apply_panel(B, sp, lam, v))
+    return {"n": n, "k": k, "tol": tol, "gpu_iters": int(r.iters), "cpu_iters": int(it),
+            "gpu_info": int(r.info), "cpu_info": int(info),
+            "rel_dx": float(np.linalg.norm(r.x - x) / np.linalg.norm(x))}
+
+
+def main():
+    args = parse()
+    rank, world, local, pg = dist_setup(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    n, k, lam, ell = args.n, args.k, args.lam, args.ell
+    workload = f"rbf_n{n}_nystrom{k}"
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    solver = make_solver(n, rank, world, local, pg)
+    r0, r1 = solver.row_range()
+    t0 = time.perf_counter()
+    solver.gen_rbf(X, ell)
+    t_gen = time.perf_counter() - t0
+    solver.set_operator(1.0, lam)
+    t_pre = solver.precon_nystrom(idx, variant=0)
+    b_loc = np.ascontiguousarray(b[r0:r1])
+    # tol = 0: never converges, so exactly warmup + steps iterations run
+    solver.pcg_start(b_loc, tol=0.0, maxiter=args.warmup + args.steps + 1)
+    if args.warmup:
+        solver.pcg_run(args.warmup, args.warmup)
+    solver.timing(True)
+    solver.timing_reset()
+    barrier(pg, solver)
+    t0 = time.perf_counter()
+    solver.pcg_run(args.steps, args.steps)
+    barrier(pg, solver)
+    el = time.perf_counter() - t0
+    el = max_over_ranks(pg, el)
+    tm = solver.timing_read()
+    gemv_ms = tm["gemv_ms"] / max(tm["gemv_count"], 1)
+    iter_ms = tm["iter_ms"] / max(tm["iter_count"], 1)
+    nloc = r1 - r0
+    gemv_bytes = 8.0 * nloc * n + 16.0 * nloc
+    achieved = gemv_bytes / (gemv_ms * 1e-3) / 1e9
+    per_iter_bytes = 8.0 * nloc * n + 16.0 * k * nloc + 80.0 * nloc
+
+    solve = None
+    if not args.no_solve:
+        solver.timing_reset()
+        t1 = time.perf_counter()
+        res = solver.pcg(b_loc, tol=1e-6, maxiter=min(5 * n, args.solve_maxiter))
+        t_solve = max_over_ranks(pg, time.perf_counter() - t1)
+        solve = {"tol": 1e-6, "iters": int(res.iters), "info": int(res.info),
+                 "seconds": t_solve, "final_relres": float(res.resid / np.linalg.norm(b))}
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            try:
+                cpu = cpu_baseline(solver, X, b, idx, lam, ell, args.cpu_iters)
+            except Exception as e:  # a baseline failure must not hide the GPU number
+                cpu = {"value": None, "error": repr(e)}
+        par = None
+        if world == 1 and not args.no_solve:
+            par = parity_small(8192, k, lam, ell)
+        out = {
+            "metric": METRIC,
+            "value": args.steps / el,
+            "unit": "CG iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": workload, "n": n, "k": k, "lambda": lam, "length_scale": ell,
+                       "precon": "random_scores (Nystrom, iterative_solver.py:95-322)",
+                       "parallelism": f"row-shard x{world} (RCCL allgather/allreduce)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(workload, world),
+                         "kernel": "k_gemv<4,4,1> (K mat-vec)",
+                         "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms},
+            "matvec_gbs": achieved,
+            "iter_device_ms": iter_ms,
+            "iter_gbs_algorithmic": per_iter_bytes / (iter_ms * 1e-3) / 1e9,
+            "cpu_baseline": cpu,
+            "solve_to_1e-6": solve,
+            "parity_n8192": par,
+            "setup_s": {"gen_rbf": t_gen, "nystrom_build": t_pre},
+        }
+        print(json.dumps(out), flush=True)
+    solver.close()
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

