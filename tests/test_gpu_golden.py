@@ -36,11 +36,11 @@ def task_of(f):
 
 
 SEEDS = {"sgdml_ethanol_n270": 3, "sgdml_ethanol_n270_perms": 5, "sgdml_ethanol_n621": 7,
-         "sgdml_ethanol_n2997": 9}
+         "sgdml_ethanol_n2997": 9, "sgdml_ethanol_n270_nongroup": 5}
 
 
 @pytest.mark.parametrize("name", ["sgdml_ethanol_n270", "sgdml_ethanol_n621",
-                                  "sgdml_ethanol_n270_perms"])
+                                  "sgdml_ethanol_n270_perms", "sgdml_ethanol_n270_nongroup"])
 def test_assembly_operator_diag(sg, golden_dir, name):
     f = load(golden_dir, name)
     n = f["y"].size
@@ -52,10 +52,12 @@ def test_assembly_operator_diag(sg, golden_dir, name):
         d = s.diag()
     scale = np.abs(f["K"]).max()
     assert np.max(np.abs(K - f["K"])) <= 1e-13 * scale
-    # matrix-free reference operator K_op(v) = K v - lam v; ours is A v = -K v + lam v
-    assert np.linalg.norm(-Av - f["Kop_v"]) <= 1e-13 * np.linalg.norm(f["Kop_v"])
-    np.testing.assert_allclose(d, -np.diag(f["K"]), rtol=0, atol=0)
+    np.testing.assert_array_equal(d, -np.diag(K))
     np.testing.assert_allclose(d, f["diag_K"], rtol=1e-12)
+    if not name.endswith("nongroup"):
+        # matrix-free reference operator K_op(v) = K v - lam v; ours is A v = -K v + lam v
+        assert np.linalg.norm(-Av - f["Kop_v"]) <= 1e-13 * np.linalg.norm(f["Kop_v"])
+        np.testing.assert_array_equal(K, K.T)  # mirrored assembly is exactly symmetric
 
 
 def test_assembly_n2997_rows(sg, golden_dir):
@@ -138,16 +140,36 @@ def test_dropin_unpreconditioned_maxiter(sg, golden_dir):
     assert np.max(np.abs(np.log10(info["resid_trace"][1:9] / ref[:8]))) <= 1e-6
 
 
-def test_dropin_reference_failures(sg, golden_dir):
-    """Where the reference raises on a rank-deficient (symmetrised) kernel, so do we."""
+@pytest.mark.parametrize("precon", ["cholesky", "random_scores", "truncated_cholesky_custom"])
+def test_dropin_solve_perm_group(sg, golden_dir, precon):
     name = "sgdml_ethanol_n270_perms"
     f = load(golden_dir, name)
-    assert str(f["cholesky__error"]) == "AssertionError"
-    with pytest.raises(AssertionError):
-        run_dropin(f, name, "cholesky")
-    assert str(f["random_scores__error"]) == "LinAlgError"
-    with pytest.raises(np.linalg.LinAlgError):
-        run_dropin(f, name, "random_scores")
+    alphas, num_iters, resid, rmse, idxs, is_conv, info = run_dropin(f, name, precon)
+    assert is_conv
+    assert np.array_equal(idxs, f[f"{precon}__inducing_pts_idxs"])
+    assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+
+
+def test_error_semantics(sg):
+    """Non-PSD pivot -> AssertionError (incomplete_cholesky.py:62); singular K_mm in the
+    Nystrom build -> LinAlgError (scipy cho_factor)."""
+    n = 200
+    rng = np.random.default_rng(0)
+    A = rng.standard_normal((n, n))
+    indef = (A + A.T) / 2
+    with sg.KernelSolver(n) as s:
+        s.set_matrix(indef)
+        s.set_operator(1.0, 1e-6)
+        with pytest.raises(AssertionError):
+            s.precon_pivchol(50)
+    negdef = -np.eye(n) - 0.01 * np.ones((n, n))  # S_mm negative definite: no Cholesky
+    for variant in (0, 1):
+        with sg.KernelSolver(n) as s:
+            s.set_matrix(negdef)
+            s.set_operator(1.0, 1e-10)
+            with pytest.raises(np.linalg.LinAlgError):
+                s.precon_nystrom(np.arange(0, 200, 10), variant=variant)
 
 
 def test_dropin_unknown_preconditioner(sg, golden_dir):
