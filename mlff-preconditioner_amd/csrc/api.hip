@@ -18,7 +18,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 using namespace mlff;
 
@@ -41,6 +44,95 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what) {
   return set_error(ctx, MLFF_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(e));
 }
 
+// In-process transport: `world` contexts of one process (one host thread each,
+// any devices) joined by a comm_id "LOCAL:<key>".  Collectives are host-staged
+// and reduce in rank order.  Used to exercise the multi-rank code path on a
+// single GPU (RCCL refuses two ranks on one device); production multi-GPU runs
+// use RCCL.
+struct LocalGroup {
+  int world = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long long gen = 0;
+  std::vector<double> buf;  // world * count staging
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const long long g = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+static std::mutex g_groups_m;
+static std::map<std::string, std::weak_ptr<LocalGroup>> g_groups;
+
+std::shared_ptr<LocalGroup> join_local_group(const std::string &key, int world) {
+  std::lock_guard<std::mutex> lk(g_groups_m);
+  auto it = g_groups.find(key);
+  std::shared_ptr<LocalGroup> gp = (it != g_groups.end()) ? it->second.lock() : nullptr;
+  if (!gp) {
+    gp = std::make_shared<LocalGroup>();
+    gp->world = world;
+    g_groups[key] = gp;
+  }
+  return gp;
+}
+
+int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n) {
+  if (ctx->world <= 1 || n == 0) return MLFF_OK;
+  if (ctx->comm != nullptr) {
+    MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+    return MLFF_OK;
+  }
+  LocalGroup &g = *ctx->local;
+  std::vector<double> mine(n), sum(n, 0.0);
+  MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), buf, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  g.barrier();  // previous users of g.buf are done
+  if (ctx->rank == 0) g.buf.assign((size_t)g.world * n, 0.0);
+  g.barrier();
+  std::memcpy(g.buf.data() + (size_t)ctx->rank * n, mine.data(), sizeof(double) * n);
+  g.barrier();
+  for (int r = 0; r < g.world; ++r)
+    for (size_t i = 0; i < n; ++i) sum[i] += g.buf[(size_t)r * n + i];
+  g.barrier();
+  MLFF_HIP(ctx, hipMemcpyAsync(buf, sum.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
+int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count) {
+  if (ctx->world <= 1) {
+    if (send != recv)
+      MLFF_HIP(ctx, hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+    return MLFF_OK;
+  }
+  if (ctx->comm != nullptr) {
+    MLFF_NCCL(ctx, ncclAllGather(send, recv, count, ncclDouble, ctx->comm, ctx->stream));
+    return MLFF_OK;
+  }
+  LocalGroup &g = *ctx->local;
+  std::vector<double> mine(count);
+  MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  g.barrier();
+  if (ctx->rank == 0) g.buf.assign((size_t)g.world * count, 0.0);
+  g.barrier();
+  std::memcpy(g.buf.data() + (size_t)ctx->rank * count, mine.data(), sizeof(double) * count);
+  g.barrier();
+  std::vector<double> all(g.buf);
+  g.barrier();
+  MLFF_HIP(ctx, hipMemcpyAsync(recv, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
 }  // namespace mlff
 
 namespace {
@@ -60,17 +152,12 @@ int dev_free(void *p) {
 }
 
 // allreduce (sum) of n doubles in place, no-op on one rank
-int allreduce(mlff_ctx *ctx, double *buf, size_t n) {
-  if (ctx->world > 1 && n > 0)
-    MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-  return MLFF_OK;
-}
+int allreduce(mlff_ctx *ctx, double *buf, size_t n) { return comm_allreduce(ctx, buf, n); }
 
 // gather the rank blocks of an ld-long padded vector (in place)
 int allgather_blocks(mlff_ctx *ctx, double *full) {
   if (ctx->world > 1)
-    MLFF_NCCL(ctx, ncclAllGather(full + ctx->rank * ctx->blk, full, ctx->blk, ncclDouble,
-                                 ctx->comm, ctx->stream));
+    return comm_allgather(ctx, full + ctx->rank * ctx->blk, full, (size_t)ctx->blk);
   return MLFF_OK;
 }
 
@@ -352,7 +439,11 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (hipSetDevice(device) != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_HIP, "hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_error(nullptr, MLFF_ERR_HIP, "hipStreamCreate failed"));
-  if (world > 1) {
+  if (world > 1 && std::memcmp(comm_id, "LOCAL:", 6) == 0) {
+    const std::string key((const char *)comm_id, strnlen((const char *)comm_id, 128));
+    ctx->local = join_local_group(key, world);
+    if (ctx->local->world != world) return fail(set_error(nullptr, MLFF_ERR_ARG, "LOCAL group size mismatch"));
+  } else if (world > 1) {
     ncclUniqueId id;
     std::memcpy(&id, comm_id, 128);
     const ncclResult_t e = ncclCommInitRank(&ctx->comm, world, id, rank);
@@ -397,6 +488,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   if (ctx->h_st) hipHostFree(ctx->h_st);
   for (hipEvent_t e : ctx->timing.ev) hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
+  ctx->local.reset();
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return MLFF_OK;

@@ -7,6 +7,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -53,6 +54,10 @@ struct Timing {
 
 }  // namespace mlff
 
+namespace mlff {
+struct LocalGroup;  // in-process transport (api.hip), see comm_allreduce
+}
+
 struct mlff_ctx {
   int device = 0, rank = 0, world = 1;
   int64_t N = 0;        // kernel size
@@ -61,7 +66,8 @@ struct mlff_ctx {
   int64_t blk = 0;      // padded local length (multiple of 64) = column block per rank
   int64_t ld = 0;       // world * blk: padded global length / K leading dimension
   hipStream_t stream = nullptr;
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;                   // RCCL (one process per GPU)
+  std::shared_ptr<mlff::LocalGroup> local;     // or: ranks as threads of one process
 
   // kernel matrix, blk rows x ld columns (padding rows/cols are zero)
   double *K = nullptr;
@@ -121,6 +127,12 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
     int rc__ = (x);             \
     if (rc__ != MLFF_OK) return rc__; \
   } while (0)
+
+// ---- collectives (api.hip): RCCL, or the in-process transport ---------------
+// sum-allreduce of n doubles in place (no-op on one rank)
+int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n);
+// allgather: recv[r * count ...] = send of rank r; send may alias recv + rank * count
+int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count);
 
 // ---- vector / GEMV kernels (kernels_vec.hip) ---------------------------------
 // y = sigma * M v + lam * vloc  over `rows` rows of M (ld columns).

@@ -197,12 +197,10 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                        ctx->row0, nrows, pv, pp);
     double *my = wins + 2 * ctx->rank;
     hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
-    if (ctx->world > 1)
-      MLFF_NCCL(ctx, ncclAllGather(my, wins, 2, ncclDouble, ctx->comm, s));
+    if (ctx->world > 1) MLFF_TRY(comm_allgather(ctx, my, wins, 2));
     hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world, ctx->perm, m,
                        ctx->row0, nrows, ctx->T, blk, ctx->pivflag, ctx->prow, ctx->st);
-    if (ctx->world > 1 && m > 0)
-      MLFF_NCCL(ctx, ncclAllReduce(ctx->prow, ctx->prow, m, ncclDouble, ncclSum, ctx->comm, s));
+    if (ctx->world > 1 && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
     hipLaunchKernelGGL(k_piv_column, dim3(gcol), dim3(256), sizeof(double) * (m + 1), s, ctx->K,
                        ctx->ld, ctx->sigma_K, ctx->rows_per, blk, nrows, m, ctx->T, blk,
                        ctx->prow, ctx->pivflag, ctx->dwork, ctx->st);

@@ -1,0 +1,134 @@
+"""Multi-rank code path on one GPU.
+
+RCCL refuses two ranks on one device, so here W contexts of one process (one
+host thread each, all on cuda:0) are joined by the library's in-process
+transport (comm_id "LOCAL:<key>").  Everything rank-dependent runs exactly as on
+W GPUs — row sharding with padded blocks (uneven for W = 3), the elementwise
+all-reduce of partial sums, the all-gather of the search direction, the
+all-reduced low-rank apply, the distributed pivot search of the pivoted
+Cholesky — only the transport differs.  Results must match the W = 1 solve.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from tests.parity import assert_pcg_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def run_ranks(world, fn, timeout=300):
+    results = [None] * world
+    errors = [None] * world
+    key = f"LOCAL:test-{np.random.default_rng().integers(1 << 62)}".encode().ljust(128, b"\0")
+
+    def body(r):
+        try:
+            results[r] = fn(r, world, key)
+        except BaseException as e:  # noqa: BLE001
+            errors[r] = e
+
+    threads = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout)
+        assert not t.is_alive(), "rank thread hung"
+    for e in errors:
+        if e is not None:
+            raise e
+    return results
+
+
+def problem(n=1003, seed=3):
+    from sgdml_amd import synthetic
+
+    return synthetic.rbf_points(n, 3, seed)
+
+
+def solve_case(rank, world, key, n, precon, lam=1e-1, k=150, tol=1e-8):
+    import sgdml_amd
+
+    X, b = problem(n)
+    idx = np.sort(np.random.default_rng(5).choice(n, k, replace=False))
+    s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world,
+                               comm_id=key if world > 1 else None)
+    try:
+        s.gen_rbf(X, 0.2)
+        s.set_operator(1.0, lam)
+        piv = None
+        if precon == "pivchol":
+            piv, _ = s.precon_pivchol(k)
+        elif precon == "nystrom":
+            s.precon_nystrom(idx, variant=0)
+        else:
+            s.precon_none()
+        r0, r1 = s.row_range()
+        z = s.precon_apply(np.ascontiguousarray(b[r0:r1]))
+        y = s.matvec(b)
+        res = s.pcg(np.ascontiguousarray(b[r0:r1]), tol=tol, maxiter=5 * n, chunk=5)
+        lev = s.lev_scores(idx, 1e-8)
+        return {"r": (r0, r1), "x": res.x, "iters": res.iters, "trace": res.trace, "piv": piv,
+                "z": z, "y": y, "lev": lev, "info": res.info}
+    finally:
+        s.close()
+
+
+def gather(outs, key):
+    return np.concatenate([o[key] for o in outs])
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("precon", ["none", "nystrom", "pivchol"])
+def test_sharded_solve_matches_single_rank(world, precon):
+    n = 1003
+    ref = run_ranks(1, lambda r, w, key: solve_case(r, w, key, n, precon))[0]
+    outs = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    spans = [o["r"] for o in outs]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for a, b in zip(spans, spans[1:]):
+        assert a[1] == b[0]
+    # every rank runs the same number of iterations with the same residual curve
+    for o in outs[1:]:
+        assert o["iters"] == outs[0]["iters"]
+        np.testing.assert_array_equal(o["trace"], outs[0]["trace"])
+        np.testing.assert_array_equal(o["lev"], outs[0]["lev"])
+        if precon == "pivchol":
+            np.testing.assert_array_equal(o["piv"], outs[0]["piv"])
+    if precon == "pivchol":
+        np.testing.assert_array_equal(outs[0]["piv"][:150], ref["piv"][:150])
+    np.testing.assert_allclose(gather(outs, "y"), ref["y"], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(gather(outs, "z"), ref["z"], rtol=1e-9,
+                               atol=1e-9 * np.abs(ref["z"]).max())
+    np.testing.assert_allclose(outs[0]["lev"], ref["lev"], rtol=1e-8, atol=1e-12)
+    assert outs[0]["info"] == ref["info"] == 0
+    assert_pcg_parity(outs[0]["iters"], outs[0]["trace"][1:], gather(outs, "x"), ref["iters"],
+                      ref["trace"][1:], ref["x"], mode="chaotic", x_tol=1e-7)
+
+
+@pytest.mark.timeout(300)
+def test_sharded_sgdml_assembly_rows():
+    import sgdml_amd
+    from oracle.sgdml import descriptors
+    from sgdml_amd import synthetic
+
+    d = synthetic.ethanol_like(9, seed=8)
+    Rd, Rdd = descriptors(d["R"])
+    P = np.array([np.arange(9), [0, 1, 2, 4, 5, 3, 6, 7, 8], [0, 1, 2, 5, 3, 4, 6, 7, 8]])
+    n = 9 * 27
+
+    def body(rank, world, key):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world,
+                                   comm_id=key if world > 1 else None)
+        try:
+            s.assemble_sgdml(Rd, Rdd, P, 10.0)
+            return s.get_matrix_rows()
+        finally:
+            s.close()
+
+    ref = run_ranks(1, body)[0]
+    for world in (2, 4):
+        rows = np.concatenate(run_ranks(world, body))
+        np.testing.assert_array_equal(rows, ref)
