@@ -33,6 +33,8 @@
  *                                                                       mlff_pcg_result
  *   _lev_scores (numeric part)
  *       src/sGDML/sgdml/solvers/iterative_solver.py:447-552          -> mlff_lev_scores
+ *   _init_precon_operator_eigvals / _rank_k_leverage_scores (svd of K)
+ *       src/sGDML/sgdml/solvers/iterative_solver.py:1110-1329        -> mlff_precon_eig
  *
  * Conventions
  *  - All matrices are fp64.  Host buffers are C-contiguous, owned by the
@@ -70,6 +72,7 @@ extern "C" {
 #define MLFF_PRECON_NYSTROM 2  /* Nystrom, _init_precon_operator (iterative_solver.py:95-322) */
 #define MLFF_PRECON_NYSTROM_SB 3 /* _init_precon_operator_sb (iterative_solver.py:326-381) */
 #define MLFF_PRECON_LOWRANK 4  /* Woodbury on a caller-supplied factor (iterative_solver.py:1313-1329) */
+#define MLFF_PRECON_EIG 5      /* truncated eigen-decomposition + Woodbury (iterative_solver.py:1177-1329) */
 
 /* pcg status (mlff_pcg_result) */
 #define MLFF_PCG_RUNNING 0
@@ -142,6 +145,16 @@ int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int varian
 /* Woodbury on a caller-supplied factor L (N x k, given as Lt_local: k x nrows):
  * T = chol(lam I + L^T L)^-1 L^T, apply z = (r - T^T T r)/lam. */
 int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k);
+/* Truncated eigen-decomposition of S = sigma_K * K (single rank): the k largest
+ * |eigenvalues| s and eigenvectors U (= scipy svd(K) of the reference).
+ * mask_mode 0: K as is ('eigvec_precon'); 1: all entries zeroed
+ * ('eigvec_precon_block_diagonal', iterative_solver.py:1255-1261); 2: only same-atom
+ * 3x3 blocks and the max-|K| entries kept ('eigvec_precon_atomic_interactions',
+ * :1238-1254; dim_i = 3 * n_atoms).  build_woodbury = 1 installs the preconditioner
+ * L = U sqrt(s)[:, :k] + Woodbury (svd_preconditioner :1313-1329).
+ * evals_out (k) and rowlev_out (N, ||U[i, :k]||, :1172-1173) are optional. */
+int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
+                    double *evals_out, double *rowlev_out);
 int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out);
 /* z_local = M r_local (collective over ranks for the low-rank part) */
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local);

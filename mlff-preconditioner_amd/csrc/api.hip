@@ -702,6 +702,26 @@ int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
   return MLFF_OK;
 }
 
+int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
+                    double *evals_out, double *rowlev_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  if (ctx->world != 1) return set_error(ctx, MLFF_ERR_ARG, "eigen preconditioner needs a single rank");
+  if (k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "eig: need 1 <= k <= N");
+  if (mask_mode < 0 || mask_mode > 2 || (mask_mode == 2 && (dim_i < 3 || dim_i % 3 != 0)))
+    return set_error(ctx, MLFF_ERR_ARG, "eig: bad mask_mode / dim_i");
+  ctx->precon_kind = MLFF_PRECON_NONE;
+  MLFF_TRY(alloc_panel(ctx, k));
+  MLFF_TRY(eig_lowrank(ctx, k, mask_mode, dim_i, ctx->T, evals_out, rowlev_out));
+  if (build_woodbury) {
+    MLFF_TRY(woodbury_inplace(ctx, ctx->T, k));
+    ctx->precon_kind = MLFF_PRECON_EIG;
+    ctx->k = k;
+    ctx->sigma_p = 1.0;
+  }
+  return MLFF_OK;
+}
+
 int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
   if (kind_out) *kind_out = ctx->precon_kind;

@@ -205,6 +205,10 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
 int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,
                       double *R_d_desc);
 
+// ---- eigen preconditioner (kernels_eig.hip) ----------------------------------
+int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *Lt_out,
+                double *evals_out, double *rowlev_out);
+
 // ---- pivoted Cholesky (kernels_pivchol.hip) ---------------------------------
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out);
 

@@ -29,7 +29,7 @@ MLFF_ERR_STATE = -5
 MLFF_ERR_COMM = -6
 MLFF_ERR_NOMEM = -7
 
-PRECON_NONE, PRECON_PIVCHOL, PRECON_NYSTROM, PRECON_NYSTROM_SB, PRECON_LOWRANK = range(5)
+PRECON_NONE, PRECON_PIVCHOL, PRECON_NYSTROM, PRECON_NYSTROM_SB, PRECON_LOWRANK, PRECON_EIG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER = 0, 2, 3
 
 # every symbol declared in include/mlffpcg.h with its ctypes signature
@@ -65,6 +65,7 @@ SIGNATURES = {
     "mlff_precon_pivchol": (_int, [_c_ctx, _i64, _int, _p_i64, _p_dbl]),
     "mlff_precon_nystrom": (_int, [_c_ctx, _p_i64, _i64, _int, _p_dbl]),
     "mlff_precon_lowrank": (_int, [_c_ctx, _p_dbl, _i64]),
+    "mlff_precon_eig": (_int, [_c_ctx, _i64, _int, _i64, _int, _p_dbl, _p_dbl]),
     "mlff_precon_info": (_int, [_c_ctx, _p_int, _p_i64]),
     "mlff_precon_apply": (_int, [_c_ctx, _p_dbl, _p_dbl]),
     "mlff_precon_get_panel": (_int, [_c_ctx, _p_dbl, _i64]),

@@ -163,6 +163,16 @@ class KernelSolver:
             raise ValueError("Lt_local must be k x nrows")
         self._call("mlff_precon_lowrank", nat.dptr(Lt_local), int(k))
 
+    def precon_eig(self, k: int, mask_mode: int = 0, dim_i: int = 0, build_woodbury: bool = True,
+                   want_evals: bool = False, want_rowlev: bool = False):
+        """Top-k eigen-decomposition of S = sigma_K K (see mlff_precon_eig).  Returns
+        (evals or None, ||U[i, :k]|| or None)."""
+        ev = np.empty(int(k)) if want_evals else None
+        rl = np.empty(self.n) if want_rowlev else None
+        self._call("mlff_precon_eig", int(k), int(mask_mode), int(dim_i), int(bool(build_woodbury)),
+                   nat.dptr(ev), nat.dptr(rl))
+        return ev, rl
+
     def precon_info(self) -> tuple[int, int]:
         kind, k = ctypes.c_int(), ctypes.c_int64()
         self._call("mlff_precon_info", ctypes.byref(kind), ctypes.byref(k))

@@ -68,10 +68,11 @@ class Iterative(object):
         lev_scores = solver.lev_scores(lev_approx_idxs.astype(np.int64), lam)
         return lev_scores, np.argsort(lev_scores)
 
-    def _eigvec_factor(self, solver, k, masked):
-        raise NotImplementedError(
-            "eigvec_precon / rank_k_lev_scores need the on-device eigen-decomposition "
-            "(SURVEY.md 8(f) rank 3); not built in this round")
+    def _eigvec_factor(self, solver, k, name, dim_i):
+        """_init_precon_operator_eigvals (iterative_solver.py:1177-1329) on the device."""
+        mask = {"eigvec_precon": 0, "eigvec_precon_block_diagonal": 1,
+                "eigvec_precon_atomic_interactions": 2}[name]
+        solver.precon_eig(k, mask_mode=mask, dim_i=dim_i, build_woodbury=True)
 
     # --------------------------------------------------------------- solve
     def solve(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std, save_progr_callback=None,
@@ -146,7 +147,7 @@ class Iterative(object):
             inducing_pts_idxs = np.arange(int(break_percentage * n))
         elif str_preconditioner in EIGVEC_KEYS:
             k = int(np.max([int(break_percentage * n), 1]))
-            self._eigvec_factor(solver, k, str_preconditioner)
+            self._eigvec_factor(solver, k, str_preconditioner, dim_i)
             inducing_pts_idxs = np.arange(k)
         elif str_preconditioner == "none":
             solver.precon_none()
@@ -190,7 +191,10 @@ class Iterative(object):
         return alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info
 
     def _rank_k_leverage_scores(self, solver, break_percentage, n):
-        self._eigvec_factor(solver, max(int(break_percentage * n), 1), "rank_k_lev_scores")
+        """_rank_k_leverage_scores (iterative_solver.py:1110-1175): ||U[:, :k] row||."""
+        k = int(np.max([int(break_percentage * n), 1]))
+        _, rowlev = solver.precon_eig(k, mask_mode=0, build_woodbury=False, want_rowlev=True)
+        return rowlev
 
 
 class _Checkpointer:

@@ -201,3 +201,29 @@ def test_sgdml_assembly(sg, perms):
         K = s.get_matrix_rows()
     scale = np.max(np.abs(K_ref))
     assert np.max(np.abs(K - K_ref)) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("mask", [0, 1])
+def test_eig_preconditioner_apply(sg, mask):
+    """svd_preconditioner (iterative_solver.py:1313-1329): L = U sqrt(s)[:, :k] + Woodbury."""
+    from oracle.precon import apply_panel, svd_panel
+    from oracle.rbf import rbf_kernel
+
+    n, k, lam = 700, 60, 1e-4
+    X, _ = _rbf(n)
+    K = rbf_kernel(X, 0.2)
+    r = np.random.default_rng(8).standard_normal(n)
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, length_scale=0.2)
+        s.set_operator(1.0, lam)
+        ev, lev = s.precon_eig(k, mask_mode=mask, want_evals=True, want_rowlev=True)
+        z = s.precon_apply(r)
+    if mask == 1:  # block_diagonal zeroes the whole kernel: P = I / lam
+        np.testing.assert_allclose(z, r / lam, rtol=1e-14)
+        return
+    T, sp = svd_panel(K, k, lam)
+    zref = apply_panel(T, sp, lam, r)
+    assert np.linalg.norm(z - zref) <= 1e-8 * np.linalg.norm(zref)
+    U, sv, _ = np.linalg.svd(K)
+    np.testing.assert_allclose(ev, sv[:k], rtol=1e-10, atol=1e-12 * sv[0])
+    np.testing.assert_allclose(lev, np.linalg.norm(U[:, :k], axis=1), rtol=1e-7, atol=1e-10)
