@@ -14,8 +14,11 @@ With N GPUs the same problem is row-sharded (strong scaling); the mat-vec
 operand is all-gathered and the dot products all-reduced over RCCL.
 
 Prints one JSON line (rank 0) with the driver's keys plus
-  roofline:     bytes/launch of the K mat-vec (8 N_local N + 16 N_local) / its mean
-                HIP-event duration, against 8 TB/s; traffic from profiles/ (PMC) or null
+  roofline:     algorithmic bytes/launch of the K mat-vec / its mean HIP-event
+                duration, against 8 TB/s; traffic from profiles/ (PMC) or null.  With
+                the symmetric tiled storage (default) the bytes are the stored lower
+                block triangle (8 * tiles * 512^2 + 16 N_local, ~4 N^2);
+                matvec_gbs_dense_equivalent restates the rate against 8 N^2
   cpu_baseline: the NumPy/SciPy oracle (oracle/, a port of the reference's CPU
                 path) timed on this host on a bounded number of PCG iterations
                 of the same matrix (rank 0, N = 1 only)
@@ -52,7 +55,14 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-1e-6 legs")
     ap.add_argument("--cpu-iters", type=int, default=12)
+    ap.add_argument("--workload", choices=["rbf", "nanotube", "ethanol"], default="rbf",
+                    help="rbf: configs[2] (default); nanotube: configs[1] (sGDML N=15540, "
+                         "pivoted Cholesky k=2701 built on the GPU); ethanol: configs[0] geometry")
+    ap.add_argument("--m", type=int, default=0, help="training points (sGDML workloads)")
     ap.add_argument("--solve-maxiter", type=int, default=20000)
+    ap.add_argument("--storage", choices=["auto", "sym", "dense"], default="auto",
+                    help="operator storage: symmetric 512x512 tiles of the lower block "
+                         "triangle (auto/sym, ~4 N^2 bytes) or dense rows (8 N^2 bytes)")
     return ap.parse_args()
 
 
@@ -102,13 +112,13 @@ def make_solver(n, rank, world, local, pg):
     return sgdml_amd.KernelSolver(n, device=local, rank=rank, world=world, comm_id=comm_id)
 
 
-def pmc_traffic(workload: str, world: int):
+def pmc_traffic(workload: str, storage: str, world: int):
     p = REPO / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
     try:
         d = json.loads(p.read_text())
-        e = d.get(f"{workload}/gpus{world}")
+        e = d.get(f"{workload}/{storage}/gpus{world}")
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except Exception:
         return None
@@ -175,6 +185,38 @@ def parity_small(n, k, lam, ell, tol=1e-6):
             "rel_dx": float(np.linalg.norm(r.x - x) / np.linalg.norm(x))}
 
 
+def sgdml_workload(args, rank, world, local, pg):
+    """configs[0]/[1]: synthetic ethanol / nanotube sGDML kernel assembled on the GPU."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+    from sgdml_amd.rule_of_thumb import get_params, rule_of_thumb
+
+    if args.workload == "nanotube":
+        M = args.m or 14
+        ds = synthetic.nanotube_like(M, seed=0)
+        name = "nanotube"
+    else:
+        M = args.m or 111
+        ds = synthetic.ethanol_like(M, seed=0)
+        name = "ethanol"
+    n_atoms = ds["R"].shape[1]
+    n = 3 * n_atoms * M
+    m, kmin, _ = get_params(name)
+    k = int(rule_of_thumb(n=n, k_min=kmin, m=m))
+    y, _ = synthetic.labels(ds["F"])
+    t0 = time.perf_counter()
+    Rd, Rdd = sgdml_amd.sgdml_descriptors(ds["R"])
+    solver = make_solver(n, rank, world, local, pg)
+    solver.assemble_sgdml(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
+    solver.set_operator(-1.0, 1e-10)
+    solver.synchronize()
+    t_asm = time.perf_counter() - t0
+    _, t_chol = solver.precon_pivchol(k)
+    return solver, n, k, y, {"assemble_s": t_asm, "pivchol_build_s": t_chol,
+                             "workload": f"sgdml_{name}_n{n}_pivchol{k}", "M": M,
+                             "n_atoms": n_atoms}
+
+
 def main():
     args = parse()
     rank, world, local, pg = dist_setup(args)
@@ -184,16 +226,27 @@ def main():
     from sgdml_amd import synthetic
 
     n, k, lam, ell = args.n, args.k, args.lam, args.ell
-    workload = f"rbf_n{n}_nystrom{k}"
-    X, b = synthetic.rbf_points(n, 3, 0)
-    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
-    solver = make_solver(n, rank, world, local, pg)
-    r0, r1 = solver.row_range()
+    sg_info = None
+    if args.workload == "rbf":
+        workload = f"rbf_n{n}_nystrom{k}"
+        X, b = synthetic.rbf_points(n, 3, 0)
+        idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+        solver = make_solver(n, rank, world, local, pg)
+        t0 = time.perf_counter()
+        solver.gen_rbf(X, ell)
+        t_gen = time.perf_counter() - t0
+        solver.set_operator(1.0, lam)
+        t_pre = solver.precon_nystrom(idx, variant=0)
+    else:
+        solver, n, k, b, sg_info = sgdml_workload(args, rank, world, local, pg)
+        workload, lam = sg_info["workload"], 1e-10
+        t_gen, t_pre = sg_info["assemble_s"], sg_info["pivchol_build_s"]
+        args.no_cpu = True
+    solver.set_storage(args.storage)
     t0 = time.perf_counter()
-    solver.gen_rbf(X, ell)
-    t_gen = time.perf_counter() - t0
-    solver.set_operator(1.0, lam)
-    t_pre = solver.precon_nystrom(idx, variant=0)
+    storage, op_bytes = solver.storage_info()  # builds the symmetric tiles (setup)
+    t_pack = time.perf_counter() - t0
+    r0, r1 = solver.row_range()
     b_loc = np.ascontiguousarray(b[r0:r1])
     # tol = 0: never converges, so exactly warmup + steps iterations run
     solver.pcg_start(b_loc, tol=0.0, maxiter=args.warmup + args.steps + 1)
@@ -211,15 +264,17 @@ def main():
     gemv_ms = tm["gemv_ms"] / max(tm["gemv_count"], 1)
     iter_ms = tm["iter_ms"] / max(tm["iter_count"], 1)
     nloc = r1 - r0
-    gemv_bytes = 8.0 * nloc * n + 16.0 * nloc
+    gemv_bytes = op_bytes  # algorithmic bytes of this rank's operator launch
     achieved = gemv_bytes / (gemv_ms * 1e-3) / 1e9
-    per_iter_bytes = 8.0 * nloc * n + 16.0 * k * nloc + 80.0 * nloc
+    dense_equiv = (8.0 * nloc * n + 16.0 * nloc) / (gemv_ms * 1e-3) / 1e9
+    per_iter_bytes = op_bytes + 16.0 * k * nloc + 80.0 * nloc
 
     solve = None
     if not args.no_solve:
         solver.timing_reset()
         t1 = time.perf_counter()
-        res = solver.pcg(b_loc, tol=1e-6, maxiter=min(5 * n, args.solve_maxiter))
+        res = solver.pcg(b_loc, tol=1e-6 if sg_info is None else 1e-6,
+                         maxiter=min(5 * n, args.solve_maxiter))
         t_solve = max_over_ranks(pg, time.perf_counter() - t1)
         solve = {"tol": 1e-6, "iters": int(res.iters), "info": int(res.info),
                  "seconds": t_solve, "final_relres": float(res.resid / np.linalg.norm(b))}
@@ -233,7 +288,7 @@ def main():
             except Exception as e:  # a baseline failure must not hide the GPU number
                 cpu = {"value": None, "error": repr(e)}
         par = None
-        if world == 1 and not args.no_solve:
+        if world == 1 and not args.no_solve and args.workload == "rbf":
             par = parity_small(8192, k, lam, ell)
         out = {
             "metric": METRIC,
@@ -248,21 +303,31 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": workload, "n": n, "k": k, "lambda": lam, "length_scale": ell,
-                       "precon": "random_scores (Nystrom, iterative_solver.py:95-322)",
-                       "parallelism": f"row-shard x{world} (RCCL allgather/allreduce)"},
+            "config": {"workload": workload, "n": n, "k": k, "lambda": lam,
+                       "length_scale": ell if sg_info is None else 10.0,
+                       "precon": "random_scores (Nystrom, iterative_solver.py:95-322)"
+                       if sg_info is None else
+                       "cholesky (pivoted Cholesky + Woodbury, iterative_cholesky.py:115-150)",
+                       "storage": storage,
+                       "parallelism": f"row-shard x{world} (RCCL allgather/allreduce"
+                       + ("/reduce-scatter)" if storage == "sym" else ")")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(workload, world),
-                         "kernel": "k_gemv<4,4,1> (K mat-vec)",
+                         "traffic": pmc_traffic(workload, storage, world),
+                         "kernel": "k_symv_tiles + k_sym_reduce (K mat-vec, lower-triangle tiles)"
+                         if storage == "sym" else "k_gemv<4,4,1> (K mat-vec)",
                          "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms},
             "matvec_gbs": achieved,
+            # with half storage also report against the dense 8 N^2 bytes
+            "matvec_gbs_dense_equivalent": dense_equiv,
             "iter_device_ms": iter_ms,
             "iter_gbs_algorithmic": per_iter_bytes / (iter_ms * 1e-3) / 1e9,
             "cpu_baseline": cpu,
             "solve_to_1e-6": solve,
             "parity_n8192": par,
-            "setup_s": {"gen_rbf": t_gen, "nystrom_build": t_pre},
+            "setup_s": dict({"gen_rbf": t_gen, "nystrom_build": t_pre} if sg_info is None else
+                            {"descriptors_and_assembly": t_gen, "pivoted_cholesky_build": t_pre},
+                            storage_pack=t_pack),
         }
         print(json.dumps(out), flush=True)
     solver.close()

@@ -74,6 +74,11 @@ extern "C" {
 #define MLFF_PRECON_LOWRANK 4  /* Woodbury on a caller-supplied factor (iterative_solver.py:1313-1329) */
 #define MLFF_PRECON_EIG 5      /* truncated eigen-decomposition + Woodbury (iterative_solver.py:1177-1329) */
 
+/* operator storage (mlff_set_storage / mlff_storage_info) */
+#define MLFF_STORAGE_DENSE 0   /* dense row block, row GEMV: 8 N^2 bytes per mat-vec */
+#define MLFF_STORAGE_SYMTILE 1 /* lower block triangle in 512 x 512 tiles: ~4 N^2 bytes */
+#define MLFF_STORAGE_AUTO 2    /* SYMTILE when K is symmetric and memory allows (default) */
+
 /* pcg status (mlff_pcg_result) */
 #define MLFF_PCG_RUNNING 0
 #define MLFF_PCG_CONVERGED 2
@@ -124,8 +129,21 @@ int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_de
  * semidefinite, the solved system is (-K + lam I) x = y, iterative_solver.py:995);
  * RBF: sigma_K = +1. */
 int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam);
-/* y_local = A v_global (one collective-free local GEMV; v_global has N entries) */
+/* y_local = A v_global (v_global has N entries).  Collective over the ranks
+ * when the symmetric tiled storage is in use (a reduce-scatter of the partial
+ * products), so every rank calls it. */
 int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local);
+/* Storage of K used by the operator (K_op, iterative_solver.py:383-445; same
+ * operator, different bytes).  AUTO (default): symmetric tiles when K was
+ * generated/assembled by this library (symmetric by construction) or, on one
+ * rank, a host matrix passes an exact symmetry check; dense otherwise or when
+ * the tile copy does not fit.  SYMTILE on a non-symmetric host matrix fails
+ * with MLFF_ERR_ARG.  The tiles are a second copy next to the dense rows (the
+ * preconditioner builds read the dense rows). */
+int mlff_set_storage(mlff_ctx *ctx, int mode);
+/* resolves the storage (building the tiles if needed) and reports the mode in
+ * use and the algorithmic HBM bytes of one operator application on this rank */
+int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out);
 /* diag(sigma_K * K) (local) */
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local);
 

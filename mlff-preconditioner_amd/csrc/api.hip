@@ -133,6 +133,34 @@ int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count
   return MLFF_OK;
 }
 
+int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t count) {
+  if (ctx->world <= 1) {
+    if (send != recv)
+      MLFF_HIP(ctx, hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+    return MLFF_OK;
+  }
+  if (ctx->comm != nullptr) {
+    MLFF_NCCL(ctx, ncclReduceScatter(send, recv, count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+    return MLFF_OK;
+  }
+  LocalGroup &g = *ctx->local;
+  const size_t n = count * (size_t)g.world;
+  std::vector<double> mine(n), out(count, 0.0);
+  MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), send, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  g.barrier();
+  if (ctx->rank == 0) g.buf.assign((size_t)g.world * n, 0.0);
+  g.barrier();
+  std::memcpy(g.buf.data() + (size_t)ctx->rank * n, mine.data(), sizeof(double) * n);
+  g.barrier();
+  for (int r = 0; r < g.world; ++r)
+    for (size_t i = 0; i < count; ++i) out[i] += g.buf[(size_t)r * n + (size_t)ctx->rank * count + i];
+  g.barrier();
+  MLFF_HIP(ctx, hipMemcpyAsync(recv, out.data(), sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+}
+
 }  // namespace mlff
 
 namespace {
@@ -300,6 +328,78 @@ int require_operator(mlff_ctx *ctx) {
   return MLFF_OK;
 }
 
+// Decide the operator storage (mlff_set_storage) and build the symmetric tiles
+// if they are to be used and not current.
+int resolve_storage(mlff_ctx *ctx) {
+  if (ctx->storage == MLFF_STORAGE_DENSE) {
+    ctx->use_sym = false;
+    return MLFF_OK;
+  }
+  if (ctx->sym.ready) {
+    ctx->use_sym = true;
+    return MLFF_OK;
+  }
+  const bool explicit_sym = ctx->storage == MLFF_STORAGE_SYMTILE;
+  if (ctx->world > 1 && !ctx->K_symmetric && !explicit_sym) {
+    ctx->use_sym = false;  // a sharded host matrix cannot be checked locally
+    return MLFF_OK;
+  }
+  const bool check = !ctx->K_symmetric && ctx->world == 1;
+  bool symmetric = true;
+  int rc = sym_build(ctx, check, &symmetric);
+  if (ctx->world > 1) {
+    // every rank must take the same path (the tiled operator has a collective)
+    const double fail_here = (rc != MLFF_OK || !symmetric) ? 1.0 : 0.0;
+    double *flag = ctx->part + 3 * kMaxPart;
+    MLFF_HIP(ctx, hipMemcpyAsync(flag, &fail_here, sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    MLFF_TRY(comm_allreduce(ctx, flag, 1));
+    double fails = 0.0;
+    MLFF_HIP(ctx, hipMemcpyAsync(&fails, flag, sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (fails > 0.0 && rc == MLFF_OK) symmetric = false;
+  }
+  if (rc != MLFF_OK || !symmetric) {
+    sym_free(ctx->sym);
+    (void)hipGetLastError();
+    ctx->use_sym = false;
+    if (explicit_sym) {
+      if (rc != MLFF_OK) return rc;
+      return set_error(ctx, MLFF_ERR_ARG, "MLFF_STORAGE_SYMTILE: K is not symmetric");
+    }
+    ctx->err.clear();
+    return MLFF_OK;  // AUTO: dense row GEMV
+  }
+  ctx->use_sym = true;
+  return MLFF_OK;
+}
+
+// y_loc = sigma_K K v_full + lam v_loc over this rank's rows (status gated)
+int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const double *v_loc,
+                    const int *status) {
+  hipStream_t s = ctx->stream;
+  if (!ctx->use_sym) {
+    launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, v_full, y_loc, ctx->sigma_K, ctx->lam, v_loc,
+                     status, s);
+    return MLFF_OK;
+  }
+  SymPack &sp = ctx->sym;
+  launch_symv(sp, v_full, sp.P, status, s);
+  if (ctx->world == 1) {
+    launch_sym_reduce(sp, 0, 1, ctx->nrows, y_loc, true, ctx->sigma_K, ctx->lam, v_loc, status, s);
+    return MLFF_OK;
+  }
+  launch_sym_reduce(sp, ctx->rank, ctx->world, ctx->ld, sp.yg, false, 0.0, 0.0, nullptr, status, s);
+  MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, y_loc, (size_t)ctx->blk));
+  launch_axpby_loc(y_loc, ctx->nrows, ctx->sigma_K, ctx->lam, v_loc, status, s);
+  return MLFF_OK;
+}
+
+double operator_bytes(const mlff_ctx *ctx) {
+  if (ctx->use_sym)
+    return 8.0 * (double)ctx->sym.ntiles * kSymTile * kSymTile + 16.0 * (double)ctx->nrows;
+  return 8.0 * (double)ctx->nrows * (double)ctx->N + 16.0 * (double)ctx->nrows;
+}
+
 hipEvent_t timing_event(mlff_ctx *ctx) {
   Timing &t = ctx->timing;
   if (t.used >= t.ev.size()) {
@@ -339,8 +439,7 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) 
     e0 = timing_event(ctx);
     if (e0) hipEventRecord(e0, s);
   }
-  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->p_full, ctx->q, ctx->sigma_K, ctx->lam, p_loc,
-                   status, s);
+  MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
   if (e0 != nullptr) {
     e1 = timing_event(ctx);
     if (e1) {
@@ -363,8 +462,7 @@ int do_recheck(mlff_ctx *ctx) {
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * ctx->blk, ctx->x,
                                sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
   MLFF_TRY(allgather_blocks(ctx, ctx->xg));
-  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam, ctx->x,
-                   nullptr, s);
+  MLFF_TRY(launch_operator(ctx, ctx->xg, ctx->q, ctx->x, nullptr));
   launch_residual(ctx->b, ctx->q, ctx->r, ctx->nrows, rr_part(ctx), s);
   MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
   launch_recheck_finish(rr_part(ctx), ctx->st, ctx->trace, s);
@@ -430,7 +528,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   ctx->rows_per = (n_global + world - 1) / world;
   ctx->row0 = std::min<int64_t>((int64_t)rank * ctx->rows_per, n_global);
   ctx->nrows = std::max<int64_t>(0, std::min<int64_t>(ctx->rows_per, n_global - ctx->row0));
-  ctx->blk = round_up(ctx->rows_per, kPad);
+  // world > 1: rank blocks hold whole tiles of the symmetric operator
+  ctx->blk = round_up(ctx->rows_per, world > 1 ? kSymTile : kPad);
   ctx->ld = (int64_t)world * ctx->blk;
   auto fail = [&](int rc) {
     mlff_ctx_destroy(ctx);
@@ -457,8 +556,10 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
     if (hipMalloc(v, sizeof(double) * ctx->blk) != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_NOMEM, "alloc"));
     hipMemset(*v, 0, sizeof(double) * ctx->blk);
   }
-  if (hipMalloc(&ctx->p_full, sizeof(double) * ctx->ld) != hipSuccess ||
-      hipMalloc(&ctx->xg, sizeof(double) * ctx->ld) != hipSuccess ||
+  // full-length operands are padded to whole tiles (entries >= ld stay zero)
+  const int64_t ldp = round_up(ctx->ld, kSymTile);
+  if (hipMalloc(&ctx->p_full, sizeof(double) * ldp) != hipSuccess ||
+      hipMalloc(&ctx->xg, sizeof(double) * ldp) != hipSuccess ||
       hipMalloc(&ctx->part, sizeof(double) * 4 * kMaxPart) != hipSuccess ||
       hipMalloc(&ctx->st, sizeof(DevState)) != hipSuccess ||
       hipHostMalloc(&ctx->h_st, sizeof(DevState)) != hipSuccess ||
@@ -466,8 +567,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
       hipMalloc(&ctx->pivflag, sizeof(int) * ctx->blk) != hipSuccess ||
       hipMalloc(&ctx->perm, sizeof(int64_t) * n_global) != hipSuccess)
     return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
-  hipMemset(ctx->p_full, 0, sizeof(double) * ctx->ld);
-  hipMemset(ctx->xg, 0, sizeof(double) * ctx->ld);
+  hipMemset(ctx->p_full, 0, sizeof(double) * ldp);
+  hipMemset(ctx->xg, 0, sizeof(double) * ldp);
   hipMemset(ctx->part, 0, sizeof(double) * 4 * kMaxPart);
   hipMemset(ctx->st, 0, sizeof(DevState));
   std::memset(ctx->h_st, 0, sizeof(DevState));
@@ -485,6 +586,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart,
                   (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow})
     dev_free(p);
+  sym_free(ctx->sym);
   if (ctx->h_st) hipHostFree(ctx->h_st);
   for (hipEvent_t e : ctx->timing.ev) hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -535,6 +637,8 @@ int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) 
   }
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->has_matrix = true;
+  ctx->K_symmetric = false;
+  ctx->sym.ready = false;
   return MLFF_OK;
 }
 
@@ -576,6 +680,8 @@ int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, dou
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   hipFree(dX);
   ctx->has_matrix = true;
+  ctx->K_symmetric = true;
+  ctx->sym.ready = false;
   return MLFF_OK;
 }
 
@@ -587,6 +693,8 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_TRY(ensure_matrix(ctx));
   MLFF_TRY(assemble_sgdml(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
   ctx->has_matrix = true;
+  ctx->K_symmetric = true;  // the assembly mirrors the lower block triangle
+  ctx->sym.ready = false;
   return MLFF_OK;
 }
 
@@ -609,13 +717,34 @@ int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
   return MLFF_OK;
 }
 
+int mlff_set_storage(mlff_ctx *ctx, int mode) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (mode != MLFF_STORAGE_DENSE && mode != MLFF_STORAGE_SYMTILE && mode != MLFF_STORAGE_AUTO)
+    return set_error(ctx, MLFF_ERR_ARG, "bad storage mode");
+  if (mode != ctx->storage) {
+    ctx->storage = mode;
+    ctx->use_sym = false;
+    if (mode == MLFF_STORAGE_DENSE) sym_free(ctx->sym);
+  }
+  return MLFF_OK;
+}
+
+int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_TRY(require_operator(ctx));
+  MLFF_TRY(resolve_storage(ctx));
+  if (mode_out) *mode_out = ctx->use_sym ? MLFF_STORAGE_SYMTILE : MLFF_STORAGE_DENSE;
+  if (bytes_per_matvec_out) *bytes_per_matvec_out = operator_bytes(ctx);
+  return MLFF_OK;
+}
+
 int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
   MLFF_TRY(require_operator(ctx));
   if (v_global == nullptr || (y_local == nullptr && ctx->nrows > 0)) return set_error(ctx, MLFF_ERR_ARG, "null vector");
+  MLFF_TRY(resolve_storage(ctx));
   MLFF_TRY(scatter_global(ctx, v_global, ctx->xg));
-  launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam,
-                   ctx->xg + (int64_t)ctx->rank * ctx->blk, nullptr, ctx->stream);
+  MLFF_TRY(launch_operator(ctx, ctx->xg, ctx->q, ctx->xg + (int64_t)ctx->rank * ctx->blk, nullptr));
   MLFF_HIP(ctx, hipGetLastError());
   if (ctx->nrows > 0)
     MLFF_HIP(ctx, hipMemcpyAsync(y_local, ctx->q, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
@@ -802,6 +931,7 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
   MLFF_TRY(require_operator(ctx));
   if ((b_local == nullptr && ctx->nrows > 0) || maxiter < 1 || !(tol >= 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "pcg_start: need b, maxiter >= 1, tol >= 0");
+  MLFF_TRY(resolve_storage(ctx));
   hipStream_t s = ctx->stream;
   if (ctx->trace_cap < maxiter + 1) {
     if (ctx->trace) hipFree(ctx->trace);
@@ -827,8 +957,7 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
     MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * ctx->blk, ctx->x,
                                  sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
     MLFF_TRY(allgather_blocks(ctx, ctx->xg));
-    launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->xg, ctx->q, ctx->sigma_K, ctx->lam, ctx->x,
-                     nullptr, s);
+    MLFF_TRY(launch_operator(ctx, ctx->xg, ctx->q, ctx->x, nullptr));
     launch_residual(ctx->b, ctx->q, ctx->r, ctx->nrows, rr_part(ctx), s);
     MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
     launch_reduce_to(rr_part(ctx), kVecGrid, &ctx->st->pad0, s);

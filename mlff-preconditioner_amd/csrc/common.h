@@ -20,6 +20,7 @@ constexpr int kBlock = 256;       // threads per workgroup for streaming kernels
 constexpr int kPad = 64;          // row / vector padding (doubles) = 512 B
 constexpr int kMaxPart = 1024;    // partial-sum slots per reduction
 constexpr int kVecGrid = 512;     // workgroups of the grid-stride vector kernels
+constexpr int kSymTile = 512;     // tile edge of the symmetric tiled operator
 
 __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
@@ -40,6 +41,19 @@ struct DevState {
   double sqrt_piv;     // its sqrt(pivot)
   double best_val;     // argmax of this rank
   long long best_pos;
+};
+
+// Lower-block-triangle tiles of K owned by this rank (kernels_sym.hip).
+struct SymPack {
+  bool ready = false;
+  double *tiles = nullptr;   // ntiles x B x B
+  int2 *list = nullptr;      // (I, J) of each stored tile, I >= J
+  int64_t ntiles = 0;
+  int64_t Np = 0;            // padded global length (multiple of B)
+  int64_t nb = 0;            // Np / B
+  int64_t tiles_per_rank = 0;
+  double *P = nullptr;       // slot buffer nb x Np
+  double *yg = nullptr;      // this rank's partial y over [0, Np) (world > 1)
 };
 
 struct Timing {
@@ -74,6 +88,10 @@ struct mlff_ctx {
   bool has_matrix = false;
   double sigma_K = 1.0, lam = 0.0;
   bool has_operator = false;
+  bool K_symmetric = false;  // known symmetric by construction (generated / assembled)
+  int storage = MLFF_STORAGE_AUTO;  // requested operator storage
+  bool use_sym = false;             // resolved: symmetric tiles in use
+  mlff::SymPack sym;
 
   // CG vectors.  local: blk entries; p_full / xg: ld entries (rank blocks)
   double *x = nullptr, *r = nullptr, *z = nullptr, *q = nullptr, *b = nullptr;
@@ -204,6 +222,24 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
                    int n_atoms, const int32_t *perms, int n_perms, double sig);
 int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,
                       double *R_d_desc);
+
+// ---- symmetric tiled operator (kernels_sym.hip) -----------------------------
+// build the tiles this rank owns from the dense rows; check_symmetry compares
+// every tile with its mirror (one rank only)
+int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out);
+void sym_free(SymPack &sp);
+// P <- slot partials of K v_full over the stored tiles
+void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
+                 hipStream_t s);
+// y[i] = sum of this rank's slots of row i (i < n_out); epilogue (world 1 only):
+// y = sigma * y + lam * vloc
+void launch_sym_reduce(const SymPack &sp, int rank, int world, int64_t n_out, double *y,
+                       bool epilogue, double sigma, double lam, const double *vloc,
+                       const int *status, hipStream_t s);
+void launch_axpby_loc(double *y, int64_t n, double sigma, double lam, const double *vloc,
+                      const int *status, hipStream_t s);
+// reduce-scatter (sum) of ld doubles into blk doubles per rank
+int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t count);
 
 // ---- eigen preconditioner (kernels_eig.hip) ----------------------------------
 int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *Lt_out,

@@ -31,6 +31,7 @@ MLFF_ERR_NOMEM = -7
 
 PRECON_NONE, PRECON_PIVCHOL, PRECON_NYSTROM, PRECON_NYSTROM_SB, PRECON_LOWRANK, PRECON_EIG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER = 0, 2, 3
+STORAGE_DENSE, STORAGE_SYMTILE, STORAGE_AUTO = 0, 1, 2
 
 # every symbol declared in include/mlffpcg.h with its ctypes signature
 _c_ctx = ctypes.c_void_p
@@ -61,6 +62,8 @@ SIGNATURES = {
     "mlff_set_operator": (_int, [_c_ctx, _dbl, _dbl]),
     "mlff_matvec": (_int, [_c_ctx, _p_dbl, _p_dbl]),
     "mlff_get_diag": (_int, [_c_ctx, _p_dbl]),
+    "mlff_set_storage": (_int, [_c_ctx, _int]),
+    "mlff_storage_info": (_int, [_c_ctx, _p_int, _p_dbl]),
     "mlff_precon_none": (_int, [_c_ctx]),
     "mlff_precon_pivchol": (_int, [_c_ctx, _i64, _int, _p_i64, _p_dbl]),
     "mlff_precon_nystrom": (_int, [_c_ctx, _p_i64, _i64, _int, _p_dbl]),

@@ -123,6 +123,20 @@ class KernelSolver:
     def set_operator(self, sigma_K: float, lam: float):
         self._call("mlff_set_operator", float(sigma_K), float(lam))
 
+    def set_storage(self, mode: str):
+        """Operator storage: 'dense' (row GEMV), 'sym' (lower block triangle in
+        512 x 512 tiles, half the bytes), 'auto' (default: sym when K is symmetric)."""
+        code = {"dense": nat.STORAGE_DENSE, "sym": nat.STORAGE_SYMTILE,
+                "auto": nat.STORAGE_AUTO}[mode]
+        self._call("mlff_set_storage", code)
+
+    def storage_info(self) -> tuple[str, float]:
+        """(storage in use, algorithmic HBM bytes of one operator application on this rank)."""
+        mode = ctypes.c_int()
+        nbytes = ctypes.c_double()
+        self._call("mlff_storage_info", ctypes.byref(mode), ctypes.byref(nbytes))
+        return ("sym" if mode.value == nat.STORAGE_SYMTILE else "dense"), nbytes.value
+
     def matvec(self, v: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(v, dtype=np.float64)
         if v.shape != (self.n,):

@@ -47,7 +47,7 @@ def problem(n=1003, seed=3):
     return synthetic.rbf_points(n, 3, seed)
 
 
-def solve_case(rank, world, key, n, precon, lam=1e-1, k=150, tol=1e-8):
+def solve_case(rank, world, key, n, precon, lam=1e-1, k=150, tol=1e-8, storage="auto"):
     import sgdml_amd
 
     X, b = problem(n)
@@ -57,6 +57,9 @@ def solve_case(rank, world, key, n, precon, lam=1e-1, k=150, tol=1e-8):
     try:
         s.gen_rbf(X, 0.2)
         s.set_operator(1.0, lam)
+        s.set_storage(storage)
+        mode, _ = s.storage_info()
+        assert mode == ("dense" if storage == "dense" else "sym")
         piv = None
         if precon == "pivchol":
             piv, _ = s.precon_pivchol(k)
@@ -80,12 +83,15 @@ def gather(outs, key):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("precon", ["none", "nystrom", "pivchol"])
-def test_sharded_solve_matches_single_rank(world, precon):
+@pytest.mark.parametrize("world,precon,storage", [
+    (2, "none", "auto"), (3, "none", "auto"), (2, "nystrom", "auto"), (3, "nystrom", "auto"),
+    (2, "pivchol", "auto"), (3, "pivchol", "auto"), (2, "none", "dense"),
+    (3, "pivchol", "dense")])
+def test_sharded_solve_matches_single_rank(world, precon, storage):
+    """auto = symmetric tiles (reduce-scatter of the partial products), dense = row GEMV."""
     n = 1003
-    ref = run_ranks(1, lambda r, w, key: solve_case(r, w, key, n, precon))[0]
-    outs = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    ref = run_ranks(1, lambda r, w, key: solve_case(r, w, key, n, precon, storage=storage))[0]
+    outs = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon, storage=storage))
     spans = [o["r"] for o in outs]
     assert spans[0][0] == 0 and spans[-1][1] == n
     for a, b in zip(spans, spans[1:]):
