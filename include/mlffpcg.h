@@ -77,7 +77,8 @@ extern "C" {
 /* operator storage (mlff_set_storage / mlff_storage_info) */
 #define MLFF_STORAGE_DENSE 0   /* dense row block, row GEMV: 8 N^2 bytes per mat-vec */
 #define MLFF_STORAGE_SYMTILE 1 /* lower block triangle in 512 x 512 tiles: ~4 N^2 bytes */
-#define MLFF_STORAGE_AUTO 2    /* SYMTILE when K is symmetric and memory allows (default) */
+#define MLFF_STORAGE_AUTO 2    /* cheapest available: MATFREE, SYMTILE or DENSE (default) */
+#define MLFF_STORAGE_MATFREE 3 /* matrix-free sGDML operator (the reference's K_op), no N^2 bytes */
 
 /* pcg status (mlff_pcg_result) */
 #define MLFF_PCG_RUNNING 0
@@ -122,6 +123,15 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
                         int64_t M, int n_atoms, const int32_t *perms, int n_perms, double sig);
 /* sGDML descriptors on the GPU (desc.py:203-358, no cutoff / no PBC):
  * R: M x n_atoms x 3  ->  R_desc: M x D (1/r_ij), R_d_desc: M x D x 3          */
+/* Matrix-free sGDML operator (K_op / _K_vec, iterative_solver.py:383-445, i.e.
+ * GDMLPredict force prediction with alphas = x, predict.py:72-234) from the same
+ * inputs as mlff_assemble_sgdml, without forming K: O(M n_perms D) memory.
+ * Mat-vecs and PCG iterations run on it; the preconditioner builds that read K
+ * (pivoted Cholesky, Nystrom, eigen, leverage scores) need mlff_assemble_sgdml,
+ * which also sets this operator up.  For a permutation group it equals the
+ * assembled K; for other permutation sets it is the reference's K_op. */
+int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
+                        int n_atoms, const int32_t *perms, int n_perms, double sig);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out);
 
@@ -134,8 +144,9 @@ int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam);
  * products), so every rank calls it. */
 int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local);
 /* Storage of K used by the operator (K_op, iterative_solver.py:383-445; same
- * operator, different bytes).  AUTO (default): symmetric tiles when K was
- * generated/assembled by this library (symmetric by construction) or, on one
+ * operator, different bytes).  AUTO (default): the matrix-free sGDML operator
+ * when it exists and moves fewer bytes than the tiles; else symmetric tiles when K
+ * was generated/assembled by this library (symmetric by construction) or, on one
  * rank, a host matrix passes an exact symmetry check; dense otherwise or when
  * the tile copy does not fit.  SYMTILE on a non-symmetric host matrix fails
  * with MLFF_ERR_ARG.  The tiles are a second copy next to the dense rows (the

@@ -322,15 +322,50 @@ int check_idx(mlff_ctx *ctx, const int64_t *idx, int64_t k) {
   return MLFF_OK;
 }
 
+// the operator needs K (dense rows) or the matrix-free sGDML data
 int require_operator(mlff_ctx *ctx) {
-  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_matrix && !ctx->mf.ready)
+    return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix / operator set");
   if (!ctx->has_operator) return set_error(ctx, MLFF_ERR_STATE, "mlff_set_operator not called");
+  return MLFF_OK;
+}
+
+// preconditioner builds read columns of the dense K
+int require_matrix(mlff_ctx *ctx) {
+  MLFF_TRY(require_operator(ctx));
+  if (!ctx->has_matrix)
+    return set_error(ctx, MLFF_ERR_STATE,
+                     "this build reads the dense kernel matrix (assemble it first); the "
+                     "matrix-free operator only serves mat-vecs");
   return MLFF_OK;
 }
 
 // Decide the operator storage (mlff_set_storage) and build the symmetric tiles
 // if they are to be used and not current.
 int resolve_storage(mlff_ctx *ctx) {
+  ctx->use_mf = false;
+  if (ctx->storage == MLFF_STORAGE_MATFREE) {
+    if (!ctx->mf.ready)
+      return set_error(ctx, MLFF_ERR_STATE, "MLFF_STORAGE_MATFREE needs mlff_sgdml_operator / mlff_assemble_sgdml");
+    ctx->use_sym = false;
+    ctx->use_mf = true;
+    return MLFF_OK;
+  }
+  if (!ctx->has_matrix) {  // only the matrix-free operator exists
+    ctx->use_sym = false;
+    ctx->use_mf = true;
+    return MLFF_OK;
+  }
+  if (ctx->storage == MLFF_STORAGE_AUTO && ctx->mf.ready) {
+    // the matrix-free operator moves O(M n_perms D) instead of O(N^2) bytes;
+    // take it when it is the cheaper one
+    const double tiles = 4.0 * (double)round_up(ctx->ld, kSymTile) * (double)round_up(ctx->ld, kSymTile) / ctx->world;
+    if (mf_bytes(ctx) < 0.5 * tiles) {
+      ctx->use_sym = false;
+      ctx->use_mf = true;
+      return MLFF_OK;
+    }
+  }
   if (ctx->storage == MLFF_STORAGE_DENSE) {
     ctx->use_sym = false;
     return MLFF_OK;
@@ -377,6 +412,10 @@ int resolve_storage(mlff_ctx *ctx) {
 int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const double *v_loc,
                     const int *status) {
   hipStream_t s = ctx->stream;
+  if (ctx->use_mf) {
+    launch_mf_operator(ctx, v_full, y_loc, v_loc, status);
+    return MLFF_OK;
+  }
   if (!ctx->use_sym) {
     launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, v_full, y_loc, ctx->sigma_K, ctx->lam, v_loc,
                      status, s);
@@ -395,6 +434,7 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
 }
 
 double operator_bytes(const mlff_ctx *ctx) {
+  if (ctx->use_mf) return mf_bytes(ctx);
   if (ctx->use_sym)
     return 8.0 * (double)ctx->sym.ntiles * kSymTile * kSymTile + 16.0 * (double)ctx->nrows;
   return 8.0 * (double)ctx->nrows * (double)ctx->N + 16.0 * (double)ctx->nrows;
@@ -587,6 +627,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
                   (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow})
     dev_free(p);
   sym_free(ctx->sym);
+  mf_free(ctx->mf);
   if (ctx->h_st) hipHostFree(ctx->h_st);
   for (hipEvent_t e : ctx->timing.ev) hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -639,6 +680,7 @@ int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) 
   ctx->has_matrix = true;
   ctx->K_symmetric = false;
   ctx->sym.ready = false;
+  mf_free(ctx->mf);
   return MLFF_OK;
 }
 
@@ -682,6 +724,7 @@ int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, dou
   ctx->has_matrix = true;
   ctx->K_symmetric = true;
   ctx->sym.ready = false;
+  mf_free(ctx->mf);
   return MLFF_OK;
 }
 
@@ -692,8 +735,22 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
     return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: null input or sig <= 0");
   MLFF_TRY(ensure_matrix(ctx));
   MLFF_TRY(assemble_sgdml(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
+  // the matrix-free form of the same operator (chosen by MLFF_STORAGE_AUTO when cheaper)
+  MLFF_TRY(mf_setup(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
   ctx->has_matrix = true;
   ctx->K_symmetric = true;  // the assembly mirrors the lower block triangle
+  ctx->sym.ready = false;
+  return MLFF_OK;
+}
+
+int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
+                        int n_atoms, const int32_t *perms, int n_perms, double sig) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
+    return set_error(ctx, MLFF_ERR_ARG, "sgdml_operator: null input or sig <= 0");
+  MLFF_TRY(mf_setup(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
+  ctx->use_mf = false;
+  ctx->has_matrix = false;  // a dense K set earlier is not this operator
   ctx->sym.ready = false;
   return MLFF_OK;
 }
@@ -719,12 +776,14 @@ int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
 
 int mlff_set_storage(mlff_ctx *ctx, int mode) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  if (mode != MLFF_STORAGE_DENSE && mode != MLFF_STORAGE_SYMTILE && mode != MLFF_STORAGE_AUTO)
+  if (mode != MLFF_STORAGE_DENSE && mode != MLFF_STORAGE_SYMTILE && mode != MLFF_STORAGE_AUTO &&
+      mode != MLFF_STORAGE_MATFREE)
     return set_error(ctx, MLFF_ERR_ARG, "bad storage mode");
   if (mode != ctx->storage) {
     ctx->storage = mode;
     ctx->use_sym = false;
-    if (mode == MLFF_STORAGE_DENSE) sym_free(ctx->sym);
+    ctx->use_mf = false;
+    if (mode == MLFF_STORAGE_DENSE || mode == MLFF_STORAGE_MATFREE) sym_free(ctx->sym);
   }
   return MLFF_OK;
 }
@@ -733,7 +792,9 @@ int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
   MLFF_TRY(require_operator(ctx));
   MLFF_TRY(resolve_storage(ctx));
-  if (mode_out) *mode_out = ctx->use_sym ? MLFF_STORAGE_SYMTILE : MLFF_STORAGE_DENSE;
+  if (mode_out)
+    *mode_out = ctx->use_mf ? MLFF_STORAGE_MATFREE
+                            : (ctx->use_sym ? MLFF_STORAGE_SYMTILE : MLFF_STORAGE_DENSE);
   if (bytes_per_matvec_out) *bytes_per_matvec_out = operator_bytes(ctx);
   return MLFF_OK;
 }
@@ -773,7 +834,7 @@ int mlff_precon_none(mlff_ctx *ctx) {
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  MLFF_TRY(require_operator(ctx));
+  MLFF_TRY(require_matrix(ctx));
   if (k < 1 || k > ctx->N || k > 16384)
     return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 16384)");
   const auto t0 = std::chrono::steady_clock::now();
@@ -798,7 +859,7 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
 int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant,
                         double *seconds_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  MLFF_TRY(require_operator(ctx));
+  MLFF_TRY(require_matrix(ctx));
   if (variant != 0 && variant != 1) return set_error(ctx, MLFF_ERR_ARG, "variant must be 0 or 1");
   MLFF_TRY(check_idx(ctx, idx, k));
   const auto t0 = std::chrono::steady_clock::now();
@@ -834,7 +895,7 @@ int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
 int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
                     double *evals_out, double *rowlev_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  MLFF_TRY(require_operator(ctx));
+  MLFF_TRY(require_matrix(ctx));
   if (ctx->world != 1) return set_error(ctx, MLFF_ERR_ARG, "eigen preconditioner needs a single rank");
   if (k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "eig: need 1 <= k <= N");
   if (mask_mode < 0 || mask_mode > 2 || (mask_mode == 2 && (dim_i < 3 || dim_i % 3 != 0)))

@@ -56,6 +56,20 @@ struct SymPack {
   double *yg = nullptr;      // this rank's partial y over [0, Np) (world > 1)
 };
 
+// Matrix-free sGDML operator data (kernels_mf.hip).
+struct MfData {
+  bool ready = false;
+  int64_t M = 0, D = 0;
+  int n = 0, n_perms = 0;
+  double sig = 0.0;
+  int64_t i0 = 0, ni = 0;            // training points touched by this rank's rows
+  double *Rd = nullptr, *Rdd = nullptr;   // M x D, M x D x 3
+  double *Rt = nullptr, *Zt = nullptr;    // (M n_perms) x D
+  int32_t *Pt = nullptr, *ps = nullptr, *pt = nullptr;
+  double *m5 = nullptr, *w = nullptr;     // ni x (M n_perms), x independent
+  double *c = nullptr, *F = nullptr;      // ni x (M n_perms), ni x D scratch
+};
+
 struct Timing {
   bool on = false;
   std::vector<hipEvent_t> ev;  // pool, pairs (start, stop)
@@ -91,7 +105,9 @@ struct mlff_ctx {
   bool K_symmetric = false;  // known symmetric by construction (generated / assembled)
   int storage = MLFF_STORAGE_AUTO;  // requested operator storage
   bool use_sym = false;             // resolved: symmetric tiles in use
+  bool use_mf = false;              // resolved: matrix-free sGDML operator in use
   mlff::SymPack sym;
+  mlff::MfData mf;                  // matrix-free sGDML operator (optional)
 
   // CG vectors.  local: blk entries; p_full / xg: ld entries (rank blocks)
   double *x = nullptr, *r = nullptr, *z = nullptr, *q = nullptr, *b = nullptr;
@@ -240,6 +256,16 @@ void launch_axpby_loc(double *y, int64_t n, double sigma, double lam, const doub
                       const int *status, hipStream_t s);
 // reduce-scatter (sum) of ld doubles into blk doubles per rank
 int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t count);
+
+// ---- matrix-free sGDML operator (kernels_mf.hip) ---------------------------
+int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
+             const int32_t *perms, int n_perms, double sig);
+void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
+                        const double *x_loc, const int *status);
+double mf_bytes(const mlff_ctx *ctx);
+void mf_free(MfData &mf);
+int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,
+                     std::vector<int32_t> &Pt, std::vector<int32_t> &piinv);
 
 // ---- eigen preconditioner (kernels_eig.hip) ----------------------------------
 int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *Lt_out,

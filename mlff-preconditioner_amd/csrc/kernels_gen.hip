@@ -350,23 +350,19 @@ __global__ __launch_bounds__(256) void k_sgdml_block(double *__restrict__ K, int
   }
 }
 
-int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
-                   int n_atoms, const int32_t *perms, int n_perms, double sig) {
-  const int n = n_atoms;
+// descriptor permutations P_p[pair(a,b)] = pair(pi a, pi b) (Desc.perm, desc.py:360-389)
+// and inverse atom maps; validates that every row of perms is a permutation
+int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,
+                     std::vector<int32_t> &Pt, std::vector<int32_t> &piinv) {
   const int64_t D = (int64_t)n * (n - 1) / 2;
-  const int64_t n3 = 3 * n;
-  if (n < 2 || M < 1 || n_perms < 1) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: bad sizes");
-  if (n3 * M != ctx->N)
-    return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: N != 3 * n_atoms * M");
-  if (n_perms > 1024) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: too many permutations");
-  // descriptor permutations P_p[pair(a,b)] = pair(pi a, pi b), inverse atom maps
-  std::vector<int32_t> Pt((size_t)n_perms * D), piinv((size_t)n_perms * n);
+  Pt.assign((size_t)n_perms * D, 0);
+  piinv.assign((size_t)n_perms * n, 0);
   for (int p = 0; p < n_perms; ++p) {
     const int32_t *pp = perms + (size_t)p * n;
     std::vector<int> seen(n, 0);
     for (int a = 0; a < n; ++a) {
       if (pp[a] < 0 || pp[a] >= n || seen[pp[a]])
-        return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: perms row is not a permutation");
+        return set_error(ctx, MLFF_ERR_ARG, "sgdml: perms row is not a permutation");
       seen[pp[a]] = 1;
       piinv[(size_t)p * n + pp[a]] = a;
     }
@@ -377,6 +373,20 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
         Pt[(size_t)p * D + (int64_t)a * (a - 1) / 2 + b] = (int32_t)e;
       }
   }
+  return MLFF_OK;
+}
+
+int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
+                   int n_atoms, const int32_t *perms, int n_perms, double sig) {
+  const int n = n_atoms;
+  const int64_t D = (int64_t)n * (n - 1) / 2;
+  const int64_t n3 = 3 * n;
+  if (n < 2 || M < 1 || n_perms < 1) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: bad sizes");
+  if (n3 * M != ctx->N)
+    return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: N != 3 * n_atoms * M");
+  if (n_perms > 1024) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: too many permutations");
+  std::vector<int32_t> Pt, piinv;
+  MLFF_TRY(desc_perm_tables(ctx, perms, n, n_perms, Pt, piinv));
   // training points whose rows intersect this rank
   const int64_t i0 = ctx->row0 / n3;
   const int64_t i1 = (ctx->row0 + ctx->nrows + n3 - 1) / n3;  // exclusive

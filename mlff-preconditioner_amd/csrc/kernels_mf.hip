@@ -1,0 +1,308 @@
+// Matrix-free sGDML kernel operator: y = sigma * K x + lam * x without forming K.
+//
+// This is the operator the reference's CG actually applies: K_op / _K_vec
+// (src/sGDML/sgdml/solvers/iterative_solver.py:383-445) runs a GDMLPredict force
+// prediction at every training point with alphas = x (predict.py:72-234,
+// set_alphas :400-445).  Per training point i (query) and training point j,
+// permutation p (descriptor map P_p, desc.py:360-389):
+//   z_j      = J_j x_j                       compact Jacobian (desc.py:464-508)
+//   Zt[jp]   = z_j[P_p],  Rt[jp] = Rd_j[P_p]
+//   diff     = Rd_i - Rt[jp],  norm = sqrt5 |diff|
+//   m        = exp(-norm / sig) 5 / (3 sig^4),  w = (sig^2 + sig norm) m
+//   F_i      = sum_jp 5 m (diff . Zt[jp]) diff - w Zt[jp]
+//   y_i      = J_i^T F_i
+// For a permutation group this is the assembled K (train.py:81-236); for other
+// permutation sets it is the reference's K_op rather than its mirrored assembly.
+//
+// Work per mat-vec is O(M^2 n_perms D) flops over O(M n_perms D) data (the
+// descriptor tables stay L2/MALL resident) instead of streaming 8 N^2 bytes of a
+// dense K (N = 3 n M, D = n (n - 1) / 2): for the nanotube (M = 14, n = 370)
+// ~60 MB of traffic instead of 1.9 GB.  The x-independent quantities (Rt, 5m, w)
+// are computed once at setup.
+//
+// Kernels of one application (all status gated, fixed-order reductions):
+//   k_mf_z     Zt[jp, d]            (M n_perms D)
+//   k_mf_pair  c[i, jp] = 5m (diff . Zt[jp])   workgroup per (jp, 16 points)
+//   k_mf_h     F[i, d]                          thread per (d, 16 points)
+//   k_mf_jt    y rows of this rank = J_i^T F_i, epilogue sigma y + lam x
+#include "common.h"
+
+namespace mlff {
+
+namespace {
+
+constexpr int kIC = 16;  // training points per workgroup in the pair / F kernels
+
+__device__ __forceinline__ int64_t xpos(int64_t g, int64_t rows_per, int64_t blk) {
+  return (g / rows_per) * blk + g % rows_per;
+}
+
+__global__ __launch_bounds__(256) void k_mf_rt(const double *__restrict__ Rd,
+                                               const int32_t *__restrict__ Pt, int64_t M,
+                                               int n_perms, int64_t D, double *__restrict__ Rt) {
+  const int64_t jp = blockIdx.y;
+  const int64_t j = jp / n_perms, p = jp % n_perms;
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)
+    Rt[jp * D + d] = Rd[j * D + Pt[p * D + d]];
+}
+
+// Zt[jp, d] = sum_c Rdd_j[e, c] (x_j[t_e, c] - x_j[s_e, c]),  e = P_p[d], pair e = (s_e > t_e)
+__global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
+                                              const int32_t *__restrict__ Pt,
+                                              const int32_t *__restrict__ ps,
+                                              const int32_t *__restrict__ pt, int64_t M,
+                                              int n, int n_perms, int64_t D,
+                                              const double *__restrict__ x, int64_t rows_per,
+                                              int64_t blk, double *__restrict__ Zt,
+                                              const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  const int64_t jp = blockIdx.y;
+  const int64_t j = jp / n_perms, p = jp % n_perms;
+  const int64_t g0 = j * 3 * n;
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
+    const int64_t e = Pt[p * D + d];
+    const int s = ps[e], t = pt[e];
+    const double *r = Rdd + (j * D + e) * 3;
+    double z = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double xt = x[xpos(g0 + 3 * t + c, rows_per, blk)];
+      const double xs = x[xpos(g0 + 3 * s + c, rows_per, blk)];
+      z = fma(r[c], xt - xs, z);
+    }
+    Zt[jp * D + d] = z;
+  }
+}
+
+// out[il, jp] for the points il in [ic0, ic0 + kIC) of this workgroup:
+//   MODE 0: m5 / w from |Rd_i - Rt[jp]|      (setup)
+//   MODE 1: c = m5 * ((Rd_i - Rt[jp]) . Zt[jp])
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
+                                                 const double *__restrict__ Rt,
+                                                 const double *__restrict__ Zt, int64_t D,
+                                                 int64_t i0, int64_t ni, int64_t MP, double sig,
+                                                 const double *__restrict__ m5,
+                                                 double *__restrict__ out0,
+                                                 double *__restrict__ out1,
+                                                 const int *__restrict__ status) {
+  if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[4][kIC];
+  const int64_t jp = blockIdx.x;
+  const int64_t ic0 = (int64_t)blockIdx.y * kIC;
+  const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
+  double acc[kIC];
+#pragma unroll
+  for (int k = 0; k < kIC; ++k) acc[k] = 0.0;
+  const double *rt = Rt + jp * D;
+  const double *zt = Zt + jp * D;
+  for (int64_t d = threadIdx.x; d < D; d += 256) {
+    const double r = rt[d];
+    const double v = MODE == 1 ? zt[d] : 0.0;
+#pragma unroll
+    for (int k = 0; k < kIC; ++k) {
+      if (k < nk) {
+        const double df = Rd[(i0 + ic0 + k) * D + d] - r;
+        acc[k] = fma(df, MODE == 0 ? df : v, acc[k]);
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kIC; ++k) {
+    double v = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if (lane == 0) sh[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < nk) {
+    const int k = threadIdx.x;
+    const double s = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+    const int64_t o = (ic0 + k) * MP + jp;
+    if (MODE == 0) {
+      const double norm = sqrt(5.0) * sqrt(s);
+      const double m = exp(-norm / sig) * 5.0 / (3.0 * sig * sig * sig * sig);
+      out0[o] = 5.0 * m;
+      out1[o] = (sig * sig + sig * norm) * m;
+    } else {
+      out0[o] = m5[o] * s;
+    }
+  }
+}
+
+// F[il, d] = sum_jp c[il, jp] (Rd_i[d] - Rt[jp, d]) - w[il, jp] Zt[jp, d]   (fixed jp order)
+__global__ __launch_bounds__(256) void k_mf_h(const double *__restrict__ Rd,
+                                              const double *__restrict__ Rt,
+                                              const double *__restrict__ Zt, int64_t D,
+                                              int64_t i0, int64_t ni, int64_t MP,
+                                              const double *__restrict__ cf,
+                                              const double *__restrict__ wf,
+                                              double *__restrict__ F,
+                                              const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sc[kIC][256];
+  __shared__ double sw[kIC][256];
+  const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t ic0 = (int64_t)blockIdx.y * kIC;
+  const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
+  const bool act = d < D;
+  double rdi[kIC], h[kIC];
+#pragma unroll
+  for (int k = 0; k < kIC; ++k) {
+    rdi[k] = (act && k < nk) ? Rd[(i0 + ic0 + k) * D + d] : 0.0;
+    h[k] = 0.0;
+  }
+  for (int64_t j0 = 0; j0 < MP; j0 += 256) {
+    const int cnt = (int)((MP - j0) < 256 ? (MP - j0) : 256);
+    __syncthreads();
+    for (int k = 0; k < nk; ++k) {
+      if (threadIdx.x < cnt) {
+        sc[k][threadIdx.x] = cf[(ic0 + k) * MP + j0 + threadIdx.x];
+        sw[k][threadIdx.x] = wf[(ic0 + k) * MP + j0 + threadIdx.x];
+      }
+    }
+    __syncthreads();
+    if (act) {
+      for (int jj = 0; jj < cnt; ++jj) {
+        const double r = Rt[(j0 + jj) * D + d];
+        const double z = Zt[(j0 + jj) * D + d];
+#pragma unroll
+        for (int k = 0; k < kIC; ++k)
+          if (k < nk) h[k] = fma(sc[k][jj], rdi[k] - r, fma(-sw[k][jj], z, h[k]));
+      }
+    }
+  }
+  if (act)
+#pragma unroll
+    for (int k = 0; k < kIC; ++k)
+      if (k < nk) F[(ic0 + k) * D + d] = h[k];
+}
+
+__device__ __forceinline__ int64_t pair_of(int a, int b) {
+  return a > b ? (int64_t)a * (a - 1) / 2 + b : (int64_t)b * (b - 1) / 2 + a;
+}
+
+// rows of this rank: g = i 3n + 3a + c,  y = sum_{b != a} sgn J * Rdd_i[pair(a,b), c] F_i[pair(a,b)]
+// (J[pair, (t, c)] = +Rdd, J[pair, (s, c)] = -Rdd with s > t, desc.py:444-462)
+__global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
+                                               const double *__restrict__ F, int64_t D, int n,
+                                               int64_t i0, int64_t row0, int64_t nrows,
+                                               double sigma, double lam,
+                                               const double *__restrict__ xloc,
+                                               double *__restrict__ y,
+                                               const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  const int64_t g = row0 + r;
+  const int64_t n3 = 3 * (int64_t)n;
+  const int64_t i = g / n3;
+  const int a = (int)((g % n3) / 3), c = (int)(g % 3);
+  const double *Fi = F + (i - i0) * D;
+  const double *Ri = Rdd + i * D * 3;
+  double acc = 0.0;
+  for (int b = 0; b < n; ++b) {
+    if (b == a) continue;
+    const int64_t e = pair_of(a, b);
+    const double v = Ri[e * 3 + c] * Fi[e];
+    acc += a > b ? -v : v;
+  }
+  double yv = sigma * acc;
+  if (xloc != nullptr) yv += lam * xloc[r];
+  y[r] = yv;
+}
+
+}  // namespace
+
+int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
+             const int32_t *perms, int n_perms, double sig) {
+  MfData &mf = ctx->mf;
+  mf_free(mf);
+  const int n = n_atoms;
+  const int64_t D = (int64_t)n * (n - 1) / 2, n3 = 3 * (int64_t)n;
+  if (n < 2 || M < 1 || n_perms < 1) return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: bad sizes");
+  if (n3 * M != ctx->N) return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: N != 3 * n_atoms * M");
+  std::vector<int32_t> Pt, piinv;
+  MLFF_TRY(desc_perm_tables(ctx, perms, n, n_perms, Pt, piinv));
+  std::vector<int32_t> ps(D), pt(D);
+  for (int a = 1; a < n; ++a)
+    for (int b = 0; b < a; ++b) {
+      ps[(int64_t)a * (a - 1) / 2 + b] = a;
+      pt[(int64_t)a * (a - 1) / 2 + b] = b;
+    }
+  mf.M = M;
+  mf.n = n;
+  mf.D = D;
+  mf.n_perms = n_perms;
+  mf.sig = sig;
+  mf.i0 = ctx->row0 / n3;
+  mf.ni = ctx->nrows > 0 ? (ctx->row0 + ctx->nrows + n3 - 1) / n3 - mf.i0 : 0;
+  const int64_t MP = M * n_perms;
+  const int64_t nic = std::max<int64_t>(mf.ni, 1);
+  hipStream_t s = ctx->stream;
+  MLFF_HIP(ctx, hipMalloc(&mf.Rd, sizeof(double) * M * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.Rdd, sizeof(double) * M * D * 3));
+  MLFF_HIP(ctx, hipMalloc(&mf.Rt, sizeof(double) * MP * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.Zt, sizeof(double) * MP * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.Pt, sizeof(int32_t) * n_perms * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.ps, sizeof(int32_t) * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.pt, sizeof(int32_t) * D));
+  MLFF_HIP(ctx, hipMalloc(&mf.m5, sizeof(double) * nic * MP));
+  MLFF_HIP(ctx, hipMalloc(&mf.w, sizeof(double) * nic * MP));
+  MLFF_HIP(ctx, hipMalloc(&mf.c, sizeof(double) * nic * MP));
+  MLFF_HIP(ctx, hipMalloc(&mf.F, sizeof(double) * nic * D));
+  MLFF_HIP(ctx, hipMemcpyAsync(mf.Rd, R_desc, sizeof(double) * M * D, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(mf.Rdd, R_d_desc, sizeof(double) * M * D * 3, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(mf.Pt, Pt.data(), sizeof(int32_t) * n_perms * D, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(mf.ps, ps.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(mf.pt, pt.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
+  const unsigned gx = (unsigned)std::min<int64_t>((D + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_mf_rt, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rd, mf.Pt, M, n_perms, D,
+                     mf.Rt);
+  if (mf.ni > 0)
+    hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)MP, (unsigned)((mf.ni + kIC - 1) / kIC)),
+                       dim3(256), 0, s, mf.Rd, mf.Rt, (const double *)nullptr, D, mf.i0, mf.ni, MP,
+                       sig, (const double *)nullptr, mf.m5, mf.w, (const int *)nullptr);
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  mf.ready = true;
+  return MLFF_OK;
+}
+
+void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
+                        const double *x_loc, const int *status) {
+  const MfData &mf = ctx->mf;
+  hipStream_t s = ctx->stream;
+  const int64_t MP = mf.M * mf.n_perms;
+  const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
+                     mf.M, mf.n, mf.n_perms, mf.D, x_full, ctx->rows_per, ctx->blk, mf.Zt, status);
+  if (mf.ni == 0) return;
+  const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
+  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)MP, gi), dim3(256), 0, s, mf.Rd, mf.Rt, mf.Zt,
+                     mf.D, mf.i0, mf.ni, MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
+  hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 255) / 256), gi), dim3(256), 0, s, mf.Rd,
+                     mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s, mf.Rdd,
+                     mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows, ctx->sigma_K, ctx->lam, x_loc,
+                     y_loc, status);
+}
+
+double mf_bytes(const mlff_ctx *ctx) {
+  const MfData &mf = ctx->mf;
+  const double MP = (double)(mf.M * mf.n_perms), D = (double)mf.D;
+  const double chunks = (double)((mf.ni + kIC - 1) / kIC);
+  // Zt written once; Rt, Zt read by every point chunk in two kernels; Rd, Rdd, F
+  return 8.0 * (MP * D * (1.0 + 4.0 * chunks) + (double)mf.ni * D * 6.0 + 16.0 * ctx->nrows);
+}
+
+void mf_free(MfData &mf) {
+  for (void *p : {(void *)mf.Rd, (void *)mf.Rdd, (void *)mf.Rt, (void *)mf.Zt, (void *)mf.Pt,
+                  (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
+                  (void *)mf.F})
+    if (p) (void)hipFree(p);
+  mf = MfData();
+}
+
+}  // namespace mlff

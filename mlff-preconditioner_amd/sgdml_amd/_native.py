@@ -31,7 +31,7 @@ MLFF_ERR_NOMEM = -7
 
 PRECON_NONE, PRECON_PIVCHOL, PRECON_NYSTROM, PRECON_NYSTROM_SB, PRECON_LOWRANK, PRECON_EIG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER = 0, 2, 3
-STORAGE_DENSE, STORAGE_SYMTILE, STORAGE_AUTO = 0, 1, 2
+STORAGE_DENSE, STORAGE_SYMTILE, STORAGE_AUTO, STORAGE_MATFREE = 0, 1, 2, 3
 
 # every symbol declared in include/mlffpcg.h with its ctypes signature
 _c_ctx = ctypes.c_void_p
@@ -58,6 +58,7 @@ SIGNATURES = {
     "mlff_get_matrix_rows": (_int, [_c_ctx, _i64, _i64, _p_dbl, _i64]),
     "mlff_gen_rbf": (_int, [_c_ctx, _p_dbl, _int, _dbl, _dbl]),
     "mlff_assemble_sgdml": (_int, [_c_ctx, _p_dbl, _p_dbl, _i64, _int, _p_i32, _int, _dbl]),
+    "mlff_sgdml_operator": (_int, [_c_ctx, _p_dbl, _p_dbl, _i64, _int, _p_i32, _int, _dbl]),
     "mlff_sgdml_descriptors": (_int, [_p_dbl, _i64, _int, _p_dbl, _p_dbl]),
     "mlff_set_operator": (_int, [_c_ctx, _dbl, _dbl]),
     "mlff_matvec": (_int, [_c_ctx, _p_dbl, _p_dbl]),

@@ -108,6 +108,19 @@ class KernelSolver:
             raise ValueError("X must be N x d")
         self._call("mlff_gen_rbf", nat.dptr(X), int(X.shape[1]), float(length_scale), float(jitter))
 
+    def sgdml_operator(self, R_desc: np.ndarray, R_d_desc: np.ndarray, perms: np.ndarray,
+                       sig: float):
+        """Matrix-free sGDML operator (the reference's K_op) without assembling K."""
+        R_desc = np.ascontiguousarray(R_desc, dtype=np.float64)
+        R_d_desc = np.ascontiguousarray(R_d_desc, dtype=np.float64)
+        perms = np.ascontiguousarray(np.atleast_2d(perms), dtype=np.int32)
+        M, D = R_desc.shape
+        n_atoms = perms.shape[1]
+        if R_d_desc.shape != (M, D, 3) or D != n_atoms * (n_atoms - 1) // 2:
+            raise ValueError("R_desc / R_d_desc / perms shapes do not match")
+        self._call("mlff_sgdml_operator", nat.dptr(R_desc), nat.dptr(R_d_desc), M, n_atoms,
+                   nat.i32ptr(perms), perms.shape[0], float(sig))
+
     def assemble_sgdml(self, R_desc: np.ndarray, R_d_desc: np.ndarray, perms: np.ndarray,
                        sig: float):
         R_desc = np.ascontiguousarray(R_desc, dtype=np.float64)
@@ -125,9 +138,10 @@ class KernelSolver:
 
     def set_storage(self, mode: str):
         """Operator storage: 'dense' (row GEMV), 'sym' (lower block triangle in
-        512 x 512 tiles, half the bytes), 'auto' (default: sym when K is symmetric)."""
+        512 x 512 tiles, half the bytes), 'matfree' (sGDML operator evaluated from
+        the descriptors, no N^2 bytes), 'auto' (default: the cheapest available)."""
         code = {"dense": nat.STORAGE_DENSE, "sym": nat.STORAGE_SYMTILE,
-                "auto": nat.STORAGE_AUTO}[mode]
+                "auto": nat.STORAGE_AUTO, "matfree": nat.STORAGE_MATFREE}[mode]
         self._call("mlff_set_storage", code)
 
     def storage_info(self) -> tuple[str, float]:
@@ -135,7 +149,9 @@ class KernelSolver:
         mode = ctypes.c_int()
         nbytes = ctypes.c_double()
         self._call("mlff_storage_info", ctypes.byref(mode), ctypes.byref(nbytes))
-        return ("sym" if mode.value == nat.STORAGE_SYMTILE else "dense"), nbytes.value
+        name = {nat.STORAGE_SYMTILE: "sym", nat.STORAGE_MATFREE: "matfree"}.get(mode.value,
+                                                                                "dense")
+        return name, nbytes.value
 
     def matvec(self, v: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(v, dtype=np.float64)

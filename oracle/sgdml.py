@@ -77,3 +77,43 @@ def assemble_kernel(R_desc, R_d_desc, tril_perms_lin_, sig):
             K[i * dim_i:(i + 1) * dim_i, j * dim_i:(j + 1) * dim_i] = blk
             K[j * dim_i:(j + 1) * dim_i, i * dim_i:(i + 1) * dim_i] = blk.T
     return K
+
+
+def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
+    """K x without forming K, as the reference's CG operator evaluates it: the
+    force prediction of GDMLPredict with alphas = x (predict.py:72-234, set_alphas
+    :400-445, Desc.d_desc_dot_vec / vec_dot_d_desc desc.py:464-508) for every
+    training point i as the query:
+        z_j      = J_j x_j                              (D)
+        diff_ijp = Rd_i - Rd_j[P_p]                     (D), norm = sqrt5 |diff|
+        F_i      = sum_jp 5 m (diff . z_j[P_p]) diff - w z_j[P_p]
+        y_i      = J_i^T F_i
+    with m = exp(-norm/sig) 5/(3 sig^4), w = (sig^2 + sig norm) m.  For a
+    permutation group this equals the assembled K @ x; for other permutation sets
+    it is the reference's K_op (not its mirrored assembly)."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    perms = np.atleast_2d(perms)
+    P = np.array([desc_perm(p) for p in perms])  # n_perms x D descriptor maps
+    s_at, t_at = np.tril_indices(n, k=-1)          # pair d = (s, t), s > t
+    X = np.asarray(x, dtype=np.float64).reshape(M, n, 3)
+    z = np.einsum("mdc,mdc->md", R_d_desc, X[:, t_at, :] - X[:, s_at, :])
+    Rt = R_desc[:, P]                               # M x n_perms x D: Rd_j[P_p d]
+    Zt = z[:, P]
+    sqrt5 = np.sqrt(5.0)
+    y = np.empty((M, n, 3))
+    for i in range(M):
+        diff = R_desc[i][None, None, :] - Rt        # M x n_perms x D
+        norm = sqrt5 * np.linalg.norm(diff, axis=2)
+        m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+        w = (sig ** 2 + sig * norm) * m
+        a = np.einsum("jpd,jpd->jp", diff, Zt)
+        F = np.einsum("jp,jpd->d", 5.0 * m * a, diff) - np.einsum("jp,jpd->d", w, Zt)
+        # y_i = J_i^T F: atom t gets +Rdd F, atom s gets -Rdd F
+        contrib = R_d_desc[i] * F[:, None]
+        yi = np.zeros((n, 3))
+        np.add.at(yi, t_at, contrib)
+        np.add.at(yi, s_at, -contrib)
+        y[i] = yi
+    return y.reshape(-1)

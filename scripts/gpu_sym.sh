@@ -13,9 +13,9 @@ step() {  # step <timeout> <name> <cmd...>; stops the script on a crash / timeou
   if [ $rc -ge 2 ]; then echo "stopping after $name (rc=$rc)" >> $L; exit $rc; fi
   return 0
 }
-step 300 symtests python -m pytest tests/test_gpu_symtile.py -q -x -p no:cacheprovider -rf
+step 400 newtests python -m pytest tests/test_gpu_symtile.py tests/test_gpu_matfree.py -q -p no:cacheprovider -rf
 step 300 bench_sym python bench.py --steps 30 --warmup 3 --no-cpu --no-solve
 step 300 bench_dense python bench.py --steps 30 --warmup 3 --no-cpu --no-solve --storage dense
-step 1200 gputests python -m pytest tests/ -q -m gpu -p no:cacheprovider -rf -x
 step 600 nanotube python bench.py --workload nanotube --steps 20 --warmup 2
+step 1200 gputests python -m pytest tests/ -q -m gpu -p no:cacheprovider -rf
 echo done >> $L

@@ -19,3 +19,10 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+def load_golden(golden_dir, name):
+    """Committed reference fixture (data only: allow_pickle=False)."""
+    import numpy as np
+
+    return np.load(Path(golden_dir) / f"{name}.npz", allow_pickle=False)

@@ -1,0 +1,124 @@
+"""Matrix-free sGDML operator (csrc/kernels_mf.hip) against the reference's K_op.
+
+The reference's CG operator is matrix-free (iterative_solver.py:383-445 -> GDMLPredict,
+predict.py:72-234); the golden fixtures hold its output `Kop_v` = K_op(v) = K v - lam v.
+Tolerance: 1e-13 relative (fp64, different summation order).  For the non-group
+permutation fixture the reference's K_op differs from its mirrored assembly; the
+matrix-free operator follows K_op.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from tests.conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = ["sgdml_ethanol_n270", "sgdml_ethanol_n621", "sgdml_ethanol_n270_perms",
+            "sgdml_ethanol_n270_nongroup"]
+
+
+@pytest.fixture(scope="module")
+def sg():
+    import sgdml_amd
+
+    if sgdml_amd.device_count() < 1:
+        pytest.fail("no GPU visible to libmlffpcg.so")
+    return sgdml_amd
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_matfree_matches_reference_kop(sg, golden_dir, name):
+    f = load_golden(golden_dir, name)
+    n, lam = f["y"].size, float(f["lam"])
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+        s.set_operator(-1.0, lam)
+        assert s.storage_info()[0] == "matfree"
+        y = s.matvec(f["v"])
+        with pytest.raises(RuntimeError):  # builds need the assembled K
+            s.precon_pivchol(10)
+    ref = -f["Kop_v"]  # (-K + lam I) v
+    assert np.linalg.norm(y - ref) <= 1e-13 * np.linalg.norm(ref)
+
+
+@pytest.mark.parametrize("name", ["sgdml_ethanol_n621", "sgdml_ethanol_n270_perms"])
+def test_matfree_auto_after_assembly(sg, golden_dir, name):
+    f = load_golden(golden_dir, name)
+    n, lam = f["y"].size, float(f["lam"])
+    with sg.KernelSolver(n) as s:
+        s.assemble_sgdml(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+        s.set_operator(-1.0, lam)
+        assert s.storage_info()[0] == "matfree"  # O(M D) bytes beat the N^2 tiles
+        y_mf = s.matvec(f["v"])
+        s.set_storage("dense")
+        y_d = s.matvec(f["v"])
+    np.testing.assert_allclose(y_mf, y_d, rtol=0, atol=1e-13 * np.abs(y_d).max())
+
+
+def test_matfree_pcg_none_matches_dense(sg, golden_dir):
+    from tests.parity import assert_pcg_parity
+
+    f = load_golden(golden_dir, "sgdml_ethanol_n270")
+    n, lam = f["y"].size, float(f["lam"])
+    res = {}
+    for mode in ("matfree", "dense"):
+        with sg.KernelSolver(n) as s:
+            s.assemble_sgdml(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+            s.set_operator(-1.0, lam)
+            s.set_storage(mode)
+            s.precon_pivchol(74)
+            res[mode] = s.pcg(f["y"], tol=1e-6, maxiter=5 * n)
+    a, b = res["matfree"], res["dense"]
+    assert a.info == b.info == 0
+    assert_pcg_parity(a.iters, a.trace[1:], a.x, b.iters, b.trace[1:], b.x, mode="chaotic")
+
+
+def test_matfree_nanotube_vs_assembled(sg):
+    """370-atom nanotube-like geometry (BASELINE configs[1] shape, fewer points)."""
+    from sgdml_amd import synthetic
+
+    ds = synthetic.nanotube_like(4, seed=1)
+    Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+    n = 3 * 370 * 4
+    v = np.random.default_rng(2).standard_normal(n)
+    with sg.KernelSolver(n) as s:
+        s.assemble_sgdml(Rd, Rdd, np.arange(370)[None, :], 10.0)
+        s.set_operator(-1.0, 1e-10)
+        assert s.storage_info()[0] == "matfree"
+        y_mf = s.matvec(v)
+        s.set_storage("sym")
+        y_sym = s.matvec(v)
+    np.testing.assert_allclose(y_mf, y_sym, rtol=0, atol=1e-12 * np.abs(y_sym).max())
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_matfree_sharded(sg, golden_dir, world):
+    """Rows split inside a training point's 27-row block (N = 270, W = 4)."""
+    f = load_golden(golden_dir, "sgdml_ethanol_n270_perms")
+    n, lam = f["y"].size, float(f["lam"])
+    key = f"LOCAL:mf-{world}-{np.random.default_rng().integers(1 << 60)}".encode().ljust(128, b"\0")
+    outs, errs = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            with sg.KernelSolver(n, device=0, rank=r, world=world, comm_id=key) as s:
+                s.sgdml_operator(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+                s.set_operator(-1.0, lam)
+                outs[r] = s.matvec(f["v"])
+        except BaseException as e:  # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+        assert not t.is_alive()
+    for e in errs:
+        if e is not None:
+            raise e
+    y = np.concatenate(outs)
+    ref = -f["Kop_v"]
+    assert np.linalg.norm(y - ref) <= 1e-13 * np.linalg.norm(ref)
