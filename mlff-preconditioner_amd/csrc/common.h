@@ -68,6 +68,9 @@ struct MfData {
   int32_t *Pt = nullptr, *ps = nullptr, *pt = nullptr;
   double *m5 = nullptr, *w = nullptr;     // ni x (M n_perms), x independent
   double *c = nullptr, *F = nullptr;      // ni x (M n_perms), ni x D scratch
+  double *part = nullptr;                 // nz x ni x (M n_perms) pair partial sums
+  int nz = 1;                             // descriptor slices of the pair sums
+  int64_t dslice = 0;
 };
 
 struct Timing {

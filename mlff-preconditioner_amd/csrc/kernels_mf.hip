@@ -74,29 +74,31 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
   }
 }
 
-// out[il, jp] for the points il in [ic0, ic0 + kIC) of this workgroup:
-//   MODE 0: m5 / w from |Rd_i - Rt[jp]|      (setup)
-//   MODE 1: c = m5 * ((Rd_i - Rt[jp]) . Zt[jp])
+// Partial pair sums over the descriptor slice z of this workgroup, for the
+// points il in [ic0, ic0 + kIC):
+//   MODE 0: |Rd_i - Rt[jp]|^2                (setup)
+//   MODE 1: (Rd_i - Rt[jp]) . Zt[jp]
+// part[(z * ni + il) * MP + jp]; k_mf_pair_fin sums the slices in order.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
                                                  const double *__restrict__ Rt,
                                                  const double *__restrict__ Zt, int64_t D,
-                                                 int64_t i0, int64_t ni, int64_t MP, double sig,
-                                                 const double *__restrict__ m5,
-                                                 double *__restrict__ out0,
-                                                 double *__restrict__ out1,
+                                                 int64_t dslice, int64_t i0, int64_t ni,
+                                                 int64_t MP, double *__restrict__ part,
                                                  const int *__restrict__ status) {
   if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[4][kIC];
   const int64_t jp = blockIdx.x;
   const int64_t ic0 = (int64_t)blockIdx.y * kIC;
   const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
+  const int64_t d0 = (int64_t)blockIdx.z * dslice;
+  const int64_t d1 = (d0 + dslice) < D ? (d0 + dslice) : D;
   double acc[kIC];
 #pragma unroll
   for (int k = 0; k < kIC; ++k) acc[k] = 0.0;
   const double *rt = Rt + jp * D;
   const double *zt = Zt + jp * D;
-  for (int64_t d = threadIdx.x; d < D; d += 256) {
+  for (int64_t d = d0 + threadIdx.x; d < d1; d += 256) {
     const double r = rt[d];
     const double v = MODE == 1 ? zt[d] : 0.0;
 #pragma unroll
@@ -118,16 +120,31 @@ __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
   __syncthreads();
   if (threadIdx.x < nk) {
     const int k = threadIdx.x;
-    const double s = (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
-    const int64_t o = (ic0 + k) * MP + jp;
-    if (MODE == 0) {
-      const double norm = sqrt(5.0) * sqrt(s);
-      const double m = exp(-norm / sig) * 5.0 / (3.0 * sig * sig * sig * sig);
-      out0[o] = 5.0 * m;
-      out1[o] = (sig * sig + sig * norm) * m;
-    } else {
-      out0[o] = m5[o] * s;
-    }
+    part[((int64_t)blockIdx.z * ni + ic0 + k) * MP + jp] =
+        (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
+  }
+}
+
+// MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ part, int nz,
+                                                     int64_t nout, double sig,
+                                                     const double *__restrict__ m5,
+                                                     double *__restrict__ out0,
+                                                     double *__restrict__ out1,
+                                                     const int *__restrict__ status) {
+  if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
+  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (o >= nout) return;
+  double s = 0.0;
+  for (int z = 0; z < nz; ++z) s += part[(int64_t)z * nout + o];
+  if (MODE == 0) {
+    const double norm = sqrt(5.0) * sqrt(s);
+    const double m = exp(-norm / sig) * 5.0 / (3.0 * sig * sig * sig * sig);
+    out0[o] = 5.0 * m;
+    out1[o] = (sig * sig + sig * norm) * m;
+  } else {
+    out0[o] = m5[o] * s;
   }
 }
 
@@ -184,33 +201,48 @@ __device__ __forceinline__ int64_t pair_of(int a, int b) {
 }
 
 // rows of this rank: g = i 3n + 3a + c,  y = sum_{b != a} sgn J * Rdd_i[pair(a,b), c] F_i[pair(a,b)]
-// (J[pair, (t, c)] = +Rdd, J[pair, (s, c)] = -Rdd with s > t, desc.py:444-462)
-__global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
-                                               const double *__restrict__ F, int64_t D, int n,
-                                               int64_t i0, int64_t row0, int64_t nrows,
-                                               double sigma, double lam,
-                                               const double *__restrict__ xloc,
-                                               double *__restrict__ y,
-                                               const int *__restrict__ status) {
+// (J[pair, (t, c)] = +Rdd, J[pair, (s, c)] = -Rdd with s > t, desc.py:444-462).
+// One wave per (point, atom): lanes stride over the partner atoms b, 3 wave sums.
+__global__ __launch_bounds__(64) void k_mf_jt(const double *__restrict__ Rdd,
+                                              const double *__restrict__ F, int64_t D, int n,
+                                              int64_t i0, int64_t row0, int64_t nrows,
+                                              double sigma, double lam,
+                                              const double *__restrict__ xloc,
+                                              double *__restrict__ y,
+                                              const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= nrows) return;
-  const int64_t g = row0 + r;
+  const int a = blockIdx.x;
+  const int64_t i = i0 + blockIdx.y;
   const int64_t n3 = 3 * (int64_t)n;
-  const int64_t i = g / n3;
-  const int a = (int)((g % n3) / 3), c = (int)(g % 3);
-  const double *Fi = F + (i - i0) * D;
+  const int64_t g0 = i * n3 + 3 * a;  // global row of component 0
+  if (g0 + 2 < row0 || g0 >= row0 + nrows) return;
+  const double *Fi = F + (int64_t)blockIdx.y * D;
   const double *Ri = Rdd + i * D * 3;
-  double acc = 0.0;
-  for (int b = 0; b < n; ++b) {
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < n; b += 64) {
     if (b == a) continue;
     const int64_t e = pair_of(a, b);
-    const double v = Ri[e * 3 + c] * Fi[e];
-    acc += a > b ? -v : v;
+    const double f = a > b ? -Fi[e] : Fi[e];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) acc[c] = fma(Ri[e * 3 + c], f, acc[c]);
   }
-  double yv = sigma * acc;
-  if (xloc != nullptr) yv += lam * xloc[r];
-  y[r] = yv;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    double v = acc[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    acc[c] = v;
+  }
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int64_t r = g0 + c - row0;
+      if (r < 0 || r >= nrows) continue;
+      double yv = sigma * acc[c];
+      if (xloc != nullptr) yv += lam * xloc[r];
+      y[r] = yv;
+    }
+  }
 }
 
 }  // namespace
@@ -260,10 +292,21 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   const unsigned gx = (unsigned)std::min<int64_t>((D + 255) / 256, 1024);
   hipLaunchKernelGGL(k_mf_rt, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rd, mf.Pt, M, n_perms, D,
                      mf.Rt);
-  if (mf.ni > 0)
-    hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)MP, (unsigned)((mf.ni + kIC - 1) / kIC)),
-                       dim3(256), 0, s, mf.Rd, mf.Rt, (const double *)nullptr, D, mf.i0, mf.ni, MP,
-                       sig, (const double *)nullptr, mf.m5, mf.w, (const int *)nullptr);
+  // descriptor slices of the pair sums: enough workgroups to cover the chip
+  const int64_t gi = (mf.ni + kIC - 1) / kIC;
+  int64_t nz = (1024 + MP * gi - 1) / std::max<int64_t>(MP * gi, 1);
+  nz = std::max<int64_t>(1, std::min<int64_t>(nz, (D + 1023) / 1024));
+  mf.nz = (int)nz;
+  mf.dslice = round_up((D + nz - 1) / nz, 256);
+  MLFF_HIP(ctx, hipMalloc(&mf.part, sizeof(double) * nz * nic * MP));
+  if (mf.ni > 0) {
+    hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)MP, (unsigned)gi, (unsigned)nz), dim3(256), 0,
+                       s, mf.Rd, mf.Rt, (const double *)nullptr, D, mf.dslice, mf.i0, mf.ni, MP,
+                       mf.part, (const int *)nullptr);
+    hipLaunchKernelGGL(k_mf_pair_fin<0>, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0,
+                       s, mf.part, mf.nz, mf.ni * MP, sig, (const double *)nullptr, mf.m5, mf.w,
+                       (const int *)nullptr);
+  }
   MLFF_HIP(ctx, hipGetLastError());
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   mf.ready = true;
@@ -280,11 +323,13 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                      mf.M, mf.n, mf.n_perms, mf.D, x_full, ctx->rows_per, ctx->blk, mf.Zt, status);
   if (mf.ni == 0) return;
   const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
-  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)MP, gi), dim3(256), 0, s, mf.Rd, mf.Rt, mf.Zt,
-                     mf.D, mf.i0, mf.ni, MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
+  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)MP, gi, (unsigned)mf.nz), dim3(256), 0, s, mf.Rd,
+                     mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part, status);
+  hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0, s,
+                     mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
   hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 255) / 256), gi), dim3(256), 0, s, mf.Rd,
                      mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
-  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s, mf.Rdd,
+  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)mf.n, (unsigned)mf.ni), dim3(64), 0, s, mf.Rdd,
                      mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows, ctx->sigma_K, ctx->lam, x_loc,
                      y_loc, status);
 }
@@ -300,7 +345,7 @@ double mf_bytes(const mlff_ctx *ctx) {
 void mf_free(MfData &mf) {
   for (void *p : {(void *)mf.Rd, (void *)mf.Rdd, (void *)mf.Rt, (void *)mf.Zt, (void *)mf.Pt,
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
-                  (void *)mf.F})
+                  (void *)mf.F, (void *)mf.part})
     if (p) (void)hipFree(p);
   mf = MfData();
 }

@@ -57,7 +57,11 @@ def test_assembly_operator_diag(sg, golden_dir, name):
     if not name.endswith("nongroup"):
         # matrix-free reference operator K_op(v) = K v - lam v; ours is A v = -K v + lam v
         assert np.linalg.norm(-Av - f["Kop_v"]) <= 1e-13 * np.linalg.norm(f["Kop_v"])
-        np.testing.assert_array_equal(K, K.T)  # mirrored assembly is exactly symmetric
+        if name.endswith("_perms"):
+            # diagonal blocks are stored transposed (train.py:172-210): symmetric to rounding
+            np.testing.assert_allclose(K, K.T, rtol=0, atol=1e-15 * scale)
+        else:
+            np.testing.assert_array_equal(K, K.T)  # mirrored assembly is exactly symmetric
 
 
 def test_assembly_n2997_rows(sg, golden_dir):
