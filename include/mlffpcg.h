@@ -126,10 +126,13 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
 /* Matrix-free sGDML operator (K_op / _K_vec, iterative_solver.py:383-445, i.e.
  * GDMLPredict force prediction with alphas = x, predict.py:72-234) from the same
  * inputs as mlff_assemble_sgdml, without forming K: O(M n_perms D) memory.
- * Mat-vecs and PCG iterations run on it; the preconditioner builds that read K
- * (pivoted Cholesky, Nystrom, eigen, leverage scores) need mlff_assemble_sgdml,
- * which also sets this operator up.  For a permutation group it equals the
- * assembled K; for other permutation sets it is the reference's K_op. */
+ * Mat-vecs, PCG iterations and the column-based builds run on it: pivoted
+ * Cholesky, Nystrom and leverage scores fetch columns as K_op e_i (the
+ * reference's get_col, iterative_cholesky.py:152-156) and the diagonal from the
+ * diagonal blocks (_assemble_kernel_mat_diag, :241-380); only the eigen
+ * preconditioner (all of K) needs mlff_assemble_sgdml, which also sets this
+ * operator up.  For a permutation group it equals the assembled K; for other
+ * permutation sets it is the reference's K_op. */
 int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,

@@ -231,6 +231,12 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * ctx->blk, ctx->stream));
   ctx->tsplit = choose_tsplit(k, ctx->blk);
   MLFF_HIP(ctx, hipMalloc(&ctx->tpart, sizeof(double) * k * ctx->tsplit));
+  if (ctx->zpart != nullptr) {
+    (void)hipFree(ctx->zpart);
+    ctx->zpart = nullptr;
+  }
+  ctx->zsplit = choose_ksplit(k, ctx->blk);
+  MLFF_HIP(ctx, hipMalloc(&ctx->zpart, sizeof(double) * ctx->zsplit * ctx->blk));
   return MLFF_OK;
 }
 
@@ -271,6 +277,39 @@ int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
   return MLFF_OK;
 }
 
+__global__ void k_unit_idx(double *__restrict__ x, const int64_t *__restrict__ idx, int64_t j,
+                           int64_t rows_per, int64_t blk, double val) {
+  if (threadIdx.x == 0) {
+    const int64_t g = idx[j];
+    x[(g / rows_per) * blk + g % rows_per] = val;
+  }
+}
+
+// W[j, i] = (sigma_K K)[row0 + i, idx_j] for the local rows: a gather from the
+// dense rows, or one matrix-free operator application per column (the
+// reference's own column access, K_op.matvec(e_i), iterative_cholesky.py:152-156)
+int fetch_cols(mlff_ctx *ctx, const int64_t *didx, int64_t k, double *W, int64_t ldw) {
+  hipStream_t s = ctx->stream;
+  if (ctx->has_matrix) {
+    launch_gather_cols(ctx->K, ctx->ld, ctx->nrows, didx, k, ctx->rows_per, ctx->blk, ctx->sigma_K,
+                       W, ldw, s);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  if (!ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix / operator set");
+  MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
+  for (int64_t j = 0; j < k; ++j) {
+    hipLaunchKernelGGL(k_unit_idx, dim3(1), dim3(64), 0, s, ctx->xg, didx, j, ctx->rows_per,
+                       ctx->blk, 1.0);
+    launch_mf_operator(ctx, ctx->xg, W + j * ldw, nullptr, nullptr, ctx->sigma_K, 0.0);
+    hipLaunchKernelGGL(k_unit_idx, dim3(1), dim3(64), 0, s, ctx->xg, didx, j, ctx->rows_per,
+                       ctx->blk, 0.0);
+    if ((j & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
+}
+
 // Nystrom panel (iterative_solver.py:112-283 for variant 0, :343-374 for variant 1,
 // :489-550 for the leverage scores which follow variant 0).  W: k x blk, zeroed.
 int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant, double lam,
@@ -283,8 +322,7 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
   MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, s));
   MLFF_HIP(ctx, hipMemcpyAsync(didx, idx_host, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
   // K_nm^T (sign convention S = sigma_K K; sign flips cancel in B^T B)
-  launch_gather_cols(ctx->K, ctx->ld, ctx->nrows, didx, k, ctx->rows_per, ctx->blk, ctx->sigma_K,
-                     W, ctx->blk, s);
+  MLFF_TRY(fetch_cols(ctx, didx, k, W, ctx->blk));
   launch_gather_mm(W, ctx->blk, didx, k, ctx->row0, ctx->nrows, Smm, s);
   MLFF_TRY(allreduce(ctx, Smm, (size_t)(k * k)));
   int rc;
@@ -335,8 +373,7 @@ int require_matrix(mlff_ctx *ctx) {
   MLFF_TRY(require_operator(ctx));
   if (!ctx->has_matrix)
     return set_error(ctx, MLFF_ERR_STATE,
-                     "this build reads the dense kernel matrix (assemble it first); the "
-                     "matrix-free operator only serves mat-vecs");
+                     "this build needs the dense kernel matrix (assemble it first)");
   return MLFF_OK;
 }
 
@@ -413,7 +450,7 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
                     const int *status) {
   hipStream_t s = ctx->stream;
   if (ctx->use_mf) {
-    launch_mf_operator(ctx, v_full, y_loc, v_loc, status);
+    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam);
     return MLFF_OK;
   }
   if (!ctx->use_sym) {
@@ -432,6 +469,21 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
   launch_axpby_loc(y_loc, ctx->nrows, ctx->sigma_K, ctx->lam, v_loc, status, s);
   return MLFF_OK;
 }
+
+}  // namespace
+
+int mlff::operator_diag(mlff_ctx *ctx, double *out) {
+  if (ctx->has_matrix) {
+    launch_diag_of(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->sigma_K,
+                   out, ctx->stream);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  if (!ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix / operator set");
+  return mf_diag(ctx, out);
+}
+
+namespace {
 
 double operator_bytes(const mlff_ctx *ctx) {
   if (ctx->use_mf) return mf_bytes(ctx);
@@ -465,7 +517,7 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) 
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
     MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
-                    ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s);
+                    ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
     zsrc = ctx->z;
   } else {
     launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s);
@@ -624,7 +676,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
                   (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart,
-                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow})
+                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart})
     dev_free(p);
   sym_free(ctx->sym);
   mf_free(ctx->mf);
@@ -815,9 +867,8 @@ int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
 
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
-  launch_diag_of(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->sigma_K,
-                 ctx->dwork, ctx->stream);
+  if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  MLFF_TRY(operator_diag(ctx, ctx->dwork));
   if (ctx->nrows > 0)
     MLFF_HIP(ctx, hipMemcpyAsync(diag_local, ctx->dwork, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -834,7 +885,7 @@ int mlff_precon_none(mlff_ctx *ctx) {
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  MLFF_TRY(require_matrix(ctx));
+  MLFF_TRY(require_operator(ctx));
   if (k < 1 || k > ctx->N || k > 16384)
     return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 16384)");
   const auto t0 = std::chrono::steady_clock::now();
@@ -859,7 +910,7 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
 int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant,
                         double *seconds_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  MLFF_TRY(require_matrix(ctx));
+  MLFF_TRY(require_operator(ctx));
   if (variant != 0 && variant != 1) return set_error(ctx, MLFF_ERR_ARG, "variant must be 0 or 1");
   MLFF_TRY(check_idx(ctx, idx, k));
   const auto t0 = std::chrono::steady_clock::now();
@@ -935,7 +986,7 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, rd, ctx->tpart, nullptr, s);
     MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, rd, zd, ctx->nrows,
-                    ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s);
+                    ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s, ctx->zpart, ctx->zsplit);
   }
   MLFF_HIP(ctx, hipGetLastError());
   if (ctx->nrows > 0)
@@ -959,7 +1010,7 @@ int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
 
 int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out) {
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
-  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (!(lam > 0.0) || scores_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "lev_scores: bad args");
   MLFF_TRY(check_idx(ctx, idx, k));
   hipStream_t s = ctx->stream;

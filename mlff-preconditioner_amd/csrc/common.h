@@ -71,6 +71,7 @@ struct MfData {
   double *part = nullptr;                 // nz x ni x (M n_perms) pair partial sums
   int nz = 1;                             // descriptor slices of the pair sums
   int64_t dslice = 0;
+  std::vector<int32_t> perms, piinv;      // host copies (diagonal blocks)
 };
 
 struct Timing {
@@ -130,6 +131,8 @@ struct mlff_ctx {
   double *T = nullptr;    // k x blk (row stride blk)
   double sigma_p = 1.0;   // z = sigma_p * (r - T^T T r) / lam
   int tsplit = 1;         // column splits of the T GEMV
+  int zsplit = 1;         // row splits of the T^T t GEMV
+  double *zpart = nullptr;  // zsplit x blk partials
   double *tpart = nullptr;
 
   // pivoted Cholesky scratch
@@ -181,9 +184,16 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
                        const double *r, double *tpart, const int *status, hipStream_t s);
 int choose_tsplit(int64_t k, int64_t ncols);
 // z = sigma_p/lam * (r - T^T t), t = sum_sp tpart; rho partials (r . z)
+// (split-K over the k rows of T: zpart holds zsplit x ldt partial sums)
 void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
-                     double *rho_part, const int *status, hipStream_t s);
+                     double *rho_part, const int *status, hipStream_t s, double *zpart,
+                     int zsplit);
+// part[ks * ldw + c] = sum_{j in slice ks} W[j, c] * (sum_sp tsrc[sp * tstride + j])
+void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
+                         int tsplits, int64_t tstride, int ksplit, double *part,
+                         const int *status, hipStream_t s);
+int choose_ksplit(int64_t k, int64_t ncols);
 // rho partials of r . r (no preconditioner)
 void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
                      const int *status, hipStream_t s);
@@ -264,7 +274,13 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
 int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
              const int32_t *perms, int n_perms, double sig);
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
-                        const double *x_loc, const int *status);
+                        const double *x_loc, const int *status, double sigma, double lam);
+int mf_diag(mlff_ctx *ctx, double *out);
+// diag(sigma K) of this rank's rows: dense rows or the matrix-free sGDML data
+int operator_diag(mlff_ctx *ctx, double *out);
+int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, int n,
+               const int32_t *dP, const int32_t *perms_host, const int32_t *piinv_host,
+               int n_perms, double sig, double *diag_out);
 double mf_bytes(const mlff_ctx *ctx);
 void mf_free(MfData &mf);
 int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,

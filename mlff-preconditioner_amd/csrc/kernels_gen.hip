@@ -145,10 +145,13 @@ __global__ __launch_bounds__(256) void k_sgdml_uv(const double *__restrict__ Rd,
                                                   int n, int64_t D, int64_t i0,
                                                   const int32_t *__restrict__ Pt,  // n_perms x D
                                                   const int32_t *__restrict__ piinv,
-                                                  double sig, double *__restrict__ uv) {
-  const int64_t j = blockIdx.x;
+                                                  double sig, double *__restrict__ uv,
+                                                  int jdiag) {
+  // jdiag: only the diagonal blocks j = i (records indexed with j slot 0, M = 1)
   const int64_t iloc = blockIdx.y;
   const int64_t i = i0 + iloc;
+  const int64_t j = jdiag ? i : (int64_t)blockIdx.x;
+  const int64_t jslot = jdiag ? 0 : j;
   const int p = blockIdx.z;
   const int n_perms = gridDim.z;
   const int n3 = 3 * n;
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(256) void k_sgdml_uv(const double *__restrict__ Rd,
   const double norm = sqrt5 * sqrt(nrm2);
   const double mat52 = exp(-norm / sig) / (3.0 * sig * sig * sig * sig) * 5.0;
   const double w = (sig * sig + sig * norm) * mat52;
-  double *rec = uv + ((iloc * M + j) * n_perms + p) * (int64_t)(6 * n + 2);
+  double *rec = uv + ((iloc * M + jslot) * n_perms + p) * (int64_t)(6 * n + 2);
   if (threadIdx.x == 0) {
     rec[6 * n] = mat52;
     rec[6 * n + 1] = w;
@@ -255,11 +258,14 @@ __global__ __launch_bounds__(256) void k_sgdml_block(double *__restrict__ K, int
                                                      const int32_t *__restrict__ pi,
                                                      const int32_t *__restrict__ piinv,
                                                      int n_perms,
-                                                     const double *__restrict__ uv) {
+                                                     const double *__restrict__ uv, int jdiag,
+                                                     double *__restrict__ diag_out) {
   const int beta = blockIdx.x;
   const int64_t iloc = blockIdx.y;
   const int64_t i = i0 + iloc;
-  const int64_t j = blockIdx.z;
+  // jdiag: only the diagonal block j = i, written as its diagonal into diag_out
+  const int64_t j = jdiag ? i : (int64_t)blockIdx.z;
+  const int64_t jslot = jdiag ? 0 : j;
   const int n3 = 3 * n;
   const int64_t grow0 = i * n3 + 3 * beta;  // global row of c = 0
   bool any = false;
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(256) void k_sgdml_block(double *__restrict__ K, int
     const int alpha = t / 3, cc = t % 3;
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0;
     for (int p = 0; p < n_perms; ++p) {
-      const double *rec = uv + ((iloc * M + j) * n_perms + p) * rec_stride;
+      const double *rec = uv + ((iloc * M + jslot) * n_perms + p) * rec_stride;
       const double m5 = 5.0 * rec[6 * n];
       const double w = rec[6 * n + 1];
       const int32_t *pp = pi + (int64_t)p * n;
@@ -345,7 +351,12 @@ __global__ __launch_bounds__(256) void k_sgdml_block(double *__restrict__ K, int
     const double accs[3] = {acc0, acc1, acc2};
     for (int c = 0; c < 3; ++c) {
       const int64_t g = grow0 + c;
-      if (g >= row0 && g < row0 + nrows) K[(g - row0) * ld + pos] = accs[c];
+      if (g < row0 || g >= row0 + nrows) continue;
+      if (diag_out != nullptr) {
+        if (gcol == g) diag_out[g - row0] = accs[c];
+      } else {
+        K[(g - row0) * ld + pos] = accs[c];
+      }
     }
   }
 }
@@ -408,10 +419,11 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
   MLFF_HIP(ctx, hipMemcpyAsync(dpiinv, piinv.data(), sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->K, 0, sizeof(double) * ctx->blk * ctx->ld, s));
   hipLaunchKernelGGL(k_sgdml_uv, dim3((unsigned)M, (unsigned)mi, (unsigned)n_perms), dim3(256), 0,
-                     s, dRd, dRdd, M, n, D, i0, dP, dpiinv, sig, uv);
+                     s, dRd, dRdd, M, n, D, i0, dP, dpiinv, sig, uv, 0);
   hipLaunchKernelGGL(k_sgdml_block, dim3((unsigned)n, (unsigned)mi, (unsigned)M), dim3(256),
                      sizeof(double) * 9 * n_perms, s, ctx->K, ctx->ld, ctx->row0, ctx->nrows,
-                     ctx->rows_per, ctx->blk, dRdd, M, n, D, i0, dpi, dpiinv, n_perms, uv);
+                     ctx->rows_per, ctx->blk, dRdd, M, n, D, i0, dpi, dpiinv, n_perms, uv, 0,
+                     (double *)nullptr);
   MLFF_HIP(ctx, hipGetLastError());
   MLFF_HIP(ctx, hipFreeAsync(dRd, s));
   MLFF_HIP(ctx, hipFreeAsync(dRdd, s));
@@ -420,6 +432,39 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
   MLFF_HIP(ctx, hipFreeAsync(dpiinv, s));
   MLFF_HIP(ctx, hipFreeAsync(uv, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
+  return MLFF_OK;
+}
+
+// diag(sigma K) of this rank's rows from the sGDML inputs without assembling K:
+// the assembly kernels restricted to the diagonal blocks (diag_K of
+// iterative_cholesky.py:241-380, _assemble_kernel_mat_diag).
+int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, int n,
+               const int32_t *dP, const int32_t *perms_host, const int32_t *piinv_host,
+               int n_perms, double sig, double *diag_out) {
+  const int64_t D = (int64_t)n * (n - 1) / 2, n3 = 3 * (int64_t)n;
+  if (ctx->nrows == 0) return MLFF_OK;
+  const int64_t i0 = ctx->row0 / n3;
+  const int64_t mi = (ctx->row0 + ctx->nrows + n3 - 1) / n3 - i0;
+  hipStream_t s = ctx->stream;
+  double *uv = nullptr;
+  int32_t *dpi = nullptr, *dpiinv = nullptr;
+  const int64_t rec = 6 * n + 2;
+  MLFF_HIP(ctx, hipMallocAsync(&uv, sizeof(double) * mi * n_perms * rec, s));
+  MLFF_HIP(ctx, hipMallocAsync(&dpi, sizeof(int32_t) * n_perms * n, s));
+  MLFF_HIP(ctx, hipMallocAsync(&dpiinv, sizeof(int32_t) * n_perms * n, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(dpi, perms_host, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(dpiinv, piinv_host, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_sgdml_uv, dim3(1, (unsigned)mi, (unsigned)n_perms), dim3(256), 0, s, dRd, dRdd,
+                     (int64_t)1, n, D, i0, dP, dpiinv, sig, uv, 1);
+  hipLaunchKernelGGL(k_sgdml_block, dim3((unsigned)n, (unsigned)mi, 1), dim3(256),
+                     sizeof(double) * 9 * n_perms, s, (double *)nullptr, ctx->ld, ctx->row0,
+                     ctx->nrows, ctx->rows_per, ctx->blk, dRdd, (int64_t)1, n, D, i0, dpi, dpiinv,
+                     n_perms, uv, 1, diag_out);
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipFreeAsync(uv, s));
+  MLFF_HIP(ctx, hipFreeAsync(dpi, s));
+  MLFF_HIP(ctx, hipFreeAsync(dpiinv, s));
+  (void)M;
   return MLFF_OK;
 }
 

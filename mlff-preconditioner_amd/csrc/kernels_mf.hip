@@ -289,6 +289,8 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Pt, Pt.data(), sizeof(int32_t) * n_perms * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.ps, ps.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.pt, pt.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
+  mf.perms.assign(perms, perms + (size_t)n_perms * n);
+  mf.piinv = piinv;
   const unsigned gx = (unsigned)std::min<int64_t>((D + 255) / 256, 1024);
   hipLaunchKernelGGL(k_mf_rt, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rd, mf.Pt, M, n_perms, D,
                      mf.Rt);
@@ -314,7 +316,7 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
 }
 
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
-                        const double *x_loc, const int *status) {
+                        const double *x_loc, const int *status, double sigma, double lam) {
   const MfData &mf = ctx->mf;
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
@@ -330,8 +332,18 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 255) / 256), gi), dim3(256), 0, s, mf.Rd,
                      mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)mf.n, (unsigned)mf.ni), dim3(64), 0, s, mf.Rdd,
-                     mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows, ctx->sigma_K, ctx->lam, x_loc,
+                     mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows, sigma, lam, x_loc,
                      y_loc, status);
+}
+
+// diag(sigma K) of this rank's rows (assembly kernels on the diagonal blocks only)
+int mf_diag(mlff_ctx *ctx, double *out) {
+  MfData &mf = ctx->mf;
+  MLFF_TRY(sgdml_diag(ctx, mf.Rd, mf.Rdd, mf.M, mf.n, mf.Pt, mf.perms.data(), mf.piinv.data(),
+                      mf.n_perms, mf.sig, out));
+  if (ctx->nrows > 0) launch_scale_copy(out, out, ctx->nrows, ctx->sigma_K, ctx->stream);
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
 }
 
 double mf_bytes(const mlff_ctx *ctx) {

@@ -147,31 +147,41 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
 
 // new column of L for every not-yet-pivoted local row i:
 //   Lt[m, i] = (S[i, m_pi] - sum_{c<m} Lt[c, i] prow[c]) / sqrt_piv;  dwork[i] -= Lt[m,i]^2
-__global__ __launch_bounds__(256) void k_piv_column(const double *__restrict__ K, int64_t ld,
-                                                    double sigma, int64_t rows_per, int64_t blk,
-                                                    int64_t nrows, int64_t m,
-                                                    double *__restrict__ Lt, int64_t ldl,
-                                                    const double *__restrict__ prow,
-                                                    const int *__restrict__ pivflag,
-                                                    double *__restrict__ dwork,
-                                                    const DevState *__restrict__ st) {
-  extern __shared__ double ps[];
+// The sum comes from the split-K column GEMV (part, ksplit slices, row stride ldp);
+// S[i, m_pi] from the dense rows (sigma * K[i, pos(m_pi)]) or, for the matrix-free
+// operator, from colvec (= S e_{m_pi}, already scaled).
+__global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, int64_t ld,
+                                                 double sigma, const double *__restrict__ colvec,
+                                                 int64_t rows_per, int64_t blk, int64_t nrows,
+                                                 int64_t m, const double *__restrict__ part,
+                                                 int ksplit, int64_t ldp,
+                                                 double *__restrict__ Lt, int64_t ldl,
+                                                 const int *__restrict__ pivflag,
+                                                 double *__restrict__ dwork,
+                                                 const DevState *__restrict__ st) {
   const long long mpi = st->m_pi;
   if (mpi < 0) return;
   const double sq = st->sqrt_piv;
-  for (int64_t c = threadIdx.x; c < m; c += 256) ps[c] = prow[c];
-  __syncthreads();
   const int64_t pos = (mpi / rows_per) * blk + (mpi % rows_per);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrows;
        i += (int64_t)gridDim.x * 256) {
     if (pivflag[i]) continue;
-    const double col = sigma * K[i * ld + pos];
+    const double col = colvec != nullptr ? colvec[i] : sigma * K[i * ld + pos];
     double s0 = 0.0;
-    for (int64_t c = 0; c < m; ++c) s0 = fma(Lt[c * ldl + i], ps[c], s0);
+    for (int ks = 0; ks < ksplit; ++ks) s0 += part[(int64_t)ks * ldp + i];
     const double v = (col - s0) / sq;
     Lt[m * ldl + i] = v;
     dwork[i] -= v * v;
   }
+}
+
+// x[pos(m_pi)] = val: sets (1) and clears (0) the unit vector e_{m_pi} in the padded
+// global layout, the operand of the matrix-free column fetch
+__global__ void k_unit_pivot(double *__restrict__ x, int64_t rows_per, int64_t blk,
+                             const DevState *__restrict__ st, double val) {
+  if (threadIdx.x != 0) return;
+  const long long mpi = st->m_pi;
+  if (mpi >= 0) x[(mpi / rows_per) * blk + mpi % rows_per] = val;
 }
 
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
@@ -187,7 +197,17 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   std::vector<int64_t> hperm(N);
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->perm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
-  launch_diag_of(ctx->K, ctx->ld, nrows, ctx->row0, ctx->rows_per, blk, ctx->sigma_K, ctx->dwork, s);
+  const bool mfcols = !ctx->has_matrix;  // columns from the matrix-free operator
+  double *colbuf = nullptr, *part = nullptr;
+  if (mfcols) {
+    MLFF_TRY(operator_diag(ctx, ctx->dwork));
+    MLFF_HIP(ctx, hipMallocAsync(&colbuf, sizeof(double) * blk, s));
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
+  } else {
+    launch_diag_of(ctx->K, ctx->ld, nrows, ctx->row0, ctx->rows_per, blk, ctx->sigma_K, ctx->dwork, s);
+  }
+  const int kmax_split = choose_ksplit(k, blk);
+  MLFF_HIP(ctx, hipMallocAsync(&part, sizeof(double) * kmax_split * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
@@ -201,9 +221,19 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world, ctx->perm, m,
                        ctx->row0, nrows, ctx->T, blk, ctx->pivflag, ctx->prow, ctx->st);
     if (ctx->world > 1 && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
-    hipLaunchKernelGGL(k_piv_column, dim3(gcol), dim3(256), sizeof(double) * (m + 1), s, ctx->K,
-                       ctx->ld, ctx->sigma_K, ctx->rows_per, blk, nrows, m, ctx->T, blk,
-                       ctx->prow, ctx->pivflag, ctx->dwork, ctx->st);
+    if (mfcols) {
+      hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
+                         ctx->st, 1.0);
+      launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
+      hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
+                         ctx->st, 0.0);
+    }
+    const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
+    if (ks > 0)
+      launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s);
+    hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
+                       (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
+                       ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
   }
   MLFF_HIP(ctx, hipGetLastError());
@@ -214,6 +244,8 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                                  hipMemcpyDeviceToHost, s));
   MLFF_HIP(ctx, hipFreeAsync(pv, s));
   MLFF_HIP(ctx, hipFreeAsync(pp, s));
+  MLFF_HIP(ctx, hipFreeAsync(part, s));
+  if (colbuf) MLFF_HIP(ctx, hipFreeAsync(colbuf, s));
   MLFF_HIP(ctx, hipFreeAsync(wins, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   if (perr)

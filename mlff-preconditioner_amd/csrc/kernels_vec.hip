@@ -152,69 +152,89 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
 }
 
 // ---------------------------------------------------------------------------
-// z = sigma_p * (lam_inv * (r - T^T t)), t_j = sum_sp tpart[sp*k + j]; rho partials r.z
-// A workgroup owns 128 columns per pass; wave w accumulates rows j = w (mod 4).
-__global__ __launch_bounds__(256) void k_precon_z(const double *__restrict__ T, int64_t ldt,
-                                                  int64_t k, int splits,
-                                                  const double *__restrict__ tpart,
-                                                  const double *__restrict__ r,
-                                                  double *__restrict__ z, int64_t n,
-                                                  double sigma_p, double lam_inv,
-                                                  double *__restrict__ rho_part,
-                                                  const int *__restrict__ status) {
+// Split-K column GEMV  part[ks, c] = sum_{j in slice ks} W[j, c] t_j,
+// t_j = sum_{sp < tsplits} tsrc[sp * tstride + j].  Workgroup = 512 columns (one
+// double2 per thread, the 4 waves read 4 KB of every row) x one slice of rows, so
+// a k x N panel is spread over ~1024 workgroups whatever its shape.
+__global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__ W, int64_t ldw,
+                                                      int64_t k, const double *__restrict__ tsrc,
+                                                      int tsplits, int64_t tstride,
+                                                      int64_t kslice, double *__restrict__ part,
+                                                      const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  extern __shared__ double smem[];
-  double *t_sh = smem;                 // k
-  d2 *red = reinterpret_cast<d2 *>(smem + round_up(k, 2));  // 256 d2
-  double *sh = smem + round_up(k, 2) + 512;
-  for (int64_t j = threadIdx.x; j < k; j += 256) {
+  extern __shared__ double t_sh[];
+  const int64_t j0 = (int64_t)blockIdx.y * kslice;
+  const int64_t j1 = (j0 + kslice) < k ? (j0 + kslice) : k;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
     double a = 0.0;
-    for (int sp = 0; sp < splits; ++sp) a += tpart[(int64_t)sp * k + j];
-    t_sh[j] = a;
+    for (int sp = 0; sp < tsplits; ++sp) a += tsrc[(int64_t)sp * tstride + j];
+    t_sh[j - j0] = a;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c2 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (2 * c2 >= ldw) return;
+  const d2 *w2 = reinterpret_cast<const d2 *>(W) + c2;
+  const int64_t ld2 = ldw / 2;
+  d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+  int64_t j = j0;
+  for (; j + 3 < j1; j += 4) {
+    const d2 a0 = w2[j * ld2], a1 = w2[(j + 1) * ld2], a2 = w2[(j + 2) * ld2], a3 = w2[(j + 3) * ld2];
+    const double t0 = t_sh[j - j0], t1 = t_sh[j + 1 - j0], t2 = t_sh[j + 2 - j0], t3 = t_sh[j + 3 - j0];
+    acc0.x = fma(a0.x, t0, acc0.x);
+    acc0.y = fma(a0.y, t0, acc0.y);
+    acc1.x = fma(a1.x, t1, acc1.x);
+    acc1.y = fma(a1.y, t1, acc1.y);
+    acc0.x = fma(a2.x, t2, acc0.x);
+    acc0.y = fma(a2.y, t2, acc0.y);
+    acc1.x = fma(a3.x, t3, acc1.x);
+    acc1.y = fma(a3.y, t3, acc1.y);
+  }
+  for (; j < j1; ++j) {
+    const d2 a0 = w2[j * ld2];
+    const double t0 = t_sh[j - j0];
+    acc0.x = fma(a0.x, t0, acc0.x);
+    acc0.y = fma(a0.y, t0, acc0.y);
+  }
+  reinterpret_cast<d2 *>(part + (int64_t)blockIdx.y * ldw)[c2] = acc0 + acc1;
+}
+
+int choose_ksplit(int64_t k, int64_t ncols) {
+  const int64_t slabs = (ncols + 511) / 512;
+  int64_t sk = (1024 + slabs - 1) / slabs;
+  const int64_t cap = (k + 15) / 16;  // at least 16 rows per slice
+  if (sk > cap) sk = cap;
+  if (sk < 1) sk = 1;
+  if (sk > 256) sk = 256;
+  return (int)sk;
+}
+
+void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
+                         int tsplits, int64_t tstride, int ksplit, double *part,
+                         const int *status, hipStream_t s) {
+  const int64_t kslice = (k + ksplit - 1) / ksplit;
+  const dim3 grid((unsigned)((ldw / 2 + 255) / 256), (unsigned)ksplit);
+  hipLaunchKernelGGL(k_colgemv_part, grid, dim3(256), sizeof(double) * (kslice + 1), s, W, ldw, k,
+                     tsrc, tsplits, tstride, kslice, part, status);
+}
+
+// z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
+__global__ __launch_bounds__(256) void k_precon_fin(const double *__restrict__ part, int ksplit,
+                                                    int64_t ldp, const double *__restrict__ r,
+                                                    double *__restrict__ z, int64_t n,
+                                                    double sigma_p, double lam_inv,
+                                                    double *__restrict__ rho_part,
+                                                    const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[8];
   double rho_acc = 0.0;
-  for (int64_t c0 = (int64_t)blockIdx.x * 128; c0 < n; c0 += (int64_t)gridDim.x * 128) {
-    const int64_t c = c0 + 2 * lane;
-    d2 acc = {0.0, 0.0};
-    if (c < n) {
-      const double *base = T + c;
-      int64_t j = w;
-      for (; j + 12 < k; j += 16) {
-        const d2 a0 = *reinterpret_cast<const d2 *>(base + j * ldt);
-        const d2 a1 = *reinterpret_cast<const d2 *>(base + (j + 4) * ldt);
-        const d2 a2 = *reinterpret_cast<const d2 *>(base + (j + 8) * ldt);
-        const d2 a3 = *reinterpret_cast<const d2 *>(base + (j + 12) * ldt);
-        acc.x = fma(a0.x, t_sh[j], acc.x);
-        acc.y = fma(a0.y, t_sh[j], acc.y);
-        acc.x = fma(a1.x, t_sh[j + 4], acc.x);
-        acc.y = fma(a1.y, t_sh[j + 4], acc.y);
-        acc.x = fma(a2.x, t_sh[j + 8], acc.x);
-        acc.y = fma(a2.y, t_sh[j + 8], acc.y);
-        acc.x = fma(a3.x, t_sh[j + 12], acc.x);
-        acc.y = fma(a3.y, t_sh[j + 12], acc.y);
-      }
-      for (; j < k; j += 4) {
-        const d2 a0 = *reinterpret_cast<const d2 *>(base + j * ldt);
-        acc.x = fma(a0.x, t_sh[j], acc.x);
-        acc.y = fma(a0.y, t_sh[j], acc.y);
-      }
-    }
-    red[w * 64 + lane] = acc;
-    __syncthreads();
-    if (w == 0 && c < n) {
-      const d2 s = (red[lane] + red[64 + lane]) + (red[128 + lane] + red[192 + lane]);
-      const d2 rv = *reinterpret_cast<const d2 *>(r + c);
-      d2 zv;
-      zv.x = sigma_p * (lam_inv * (rv.x - s.x));
-      zv.y = sigma_p * (lam_inv * (rv.y - s.y));
-      if (c + 1 >= n) zv.y = 0.0;  // padding stays zero
-      *reinterpret_cast<d2 *>(z + c) = zv;
-      rho_acc = fma(rv.x, zv.x, rho_acc);
-      rho_acc = fma(rv.y, zv.y, rho_acc);
-    }
-    __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    double sv = 0.0;
+    for (int ks = 0; ks < ksplit; ++ks) sv += part[(int64_t)ks * ldp + i];
+    const double rv = r[i];
+    const double zv = sigma_p * (lam_inv * (rv - sv));
+    z[i] = zv;
+    rho_acc = fma(rv, zv, rho_acc);
   }
   const double tot = block_sum256(rho_acc, sh);
   if (threadIdx.x == 0 && rho_part != nullptr) rho_part[blockIdx.x] = tot;
@@ -222,10 +242,11 @@ __global__ __launch_bounds__(256) void k_precon_z(const double *__restrict__ T, 
 
 void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
-                     double *rho_part, const int *status, hipStream_t s) {
-  const size_t shbytes = (size_t)(round_up(k, 2) + 512 + 8) * sizeof(double);
-  hipLaunchKernelGGL(k_precon_z, dim3(kVecGrid), dim3(256), shbytes, s, T, ldt, k, splits,
-                     tpart, r, z, n, sigma_p, lam_inv, rho_part, status);
+                     double *rho_part, const int *status, hipStream_t s, double *zpart,
+                     int zsplit) {
+  launch_colgemv_part(T, ldt, k, tpart, splits, k, zsplit, zpart, status, s);
+  hipLaunchKernelGGL(k_precon_fin, dim3(kVecGrid), dim3(256), 0, s, zpart, zsplit, ldt, r, z, n,
+                     sigma_p, lam_inv, rho_part, status);
 }
 
 // ---------------------------------------------------------------------------

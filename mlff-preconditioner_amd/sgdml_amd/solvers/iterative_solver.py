@@ -9,8 +9,10 @@ the same exceptions (NotImplementedError for an unknown preconditioner,
 AssertionError for a non-PSD pivot, LinAlgError for a failed Cholesky).
 
 What runs where:
-  * the dense sGDML kernel matrix is assembled on the GPU from R_desc/R_d_desc
-    (replaces the matrix-free K_op of :383-445; equal to 5e-16 relative);
+  * the operator is the reference's matrix-free K_op (:383-445) evaluated on the GPU
+    from R_desc/R_d_desc; preconditioner builds fetch their columns through it (as
+    IterativeCholesky does), so no N x N matrix is formed -- except for the eigen
+    preconditioners, which factor all of K and assemble it on the GPU first;
   * every preconditioner build (pivoted Cholesky, Nystrom, _sb, leverage
     scores, eigen-decomposition) and the PCG iterations run in libmlffpcg.so;
   * column *selection* stays on the host with NumPy's global RNG exactly as in the
@@ -45,13 +47,20 @@ class Iterative(object):
         self.solver = None  # KernelSolver of the last solve (kept for inspection)
 
     # ------------------------------------------------------------ helpers
-    def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n):
+    def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n, dense):
+        """dense: assemble K on the device (the eigen preconditioners factor all of K);
+        otherwise only the matrix-free operator (the reference's K_op) is set up and
+        the preconditioner builds fetch their columns through it, as the reference's
+        IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory."""
         s = KernelSolver(n, device=self.device)
         perms = np.atleast_2d(np.asarray(task["perms"]))
         D = R_desc.shape[1]
         if len(tril_perms_lin) != perms.shape[0] * D:
             raise ValueError("tril_perms_lin does not match task['perms']")
-        s.assemble_sgdml(R_desc, R_d_desc, perms, float(task["sig"]))
+        if dense:
+            s.assemble_sgdml(R_desc, R_d_desc, perms, float(task["sig"]))
+        else:
+            s.sgdml_operator(R_desc, R_d_desc, perms, float(task["sig"]))
         # sGDML: K is negative semidefinite, the solved system is (-K + lam I) x = y
         s.set_operator(-1.0, float(task["lam"]))
         return s
@@ -97,8 +106,10 @@ class Iterative(object):
             n_inducing_pts_init = len(task["inducing_pts_idxs"]) // (3 * n_atoms)
         n_inducing_pts = min(n_train, n_inducing_pts_init)
 
+        dense = str_preconditioner in EIGVEC_KEYS or str_preconditioner in [
+            "rank_k_lev_scores", "rank_k_lev_scores_custom"]
         solver = self._kernel_solver(task, np.asarray(R_desc), np.asarray(R_d_desc),
-                                     tril_perms_lin, n)
+                                     tril_perms_lin, n, dense)
         self.solver = solver
         start_preconditioner = timeit.default_timer()
         info_cholesky = None

@@ -150,6 +150,155 @@ __global__ __launch_bounds__(NW * 64) void k_symv(const double *__restrict__ til
     body<RB, NW, PF, false>(A, t.x, t.y, v, P, Np, sh);
 }
 
+
+// variant: LDSROWS = row sums staged in LDS and written once per tile (coalesced);
+// IL = rows interleaved across waves (wave w takes batches w, w+NW, ...)
+template <int RB, bool LDSROWS, bool IL, bool DIAG>
+__device__ __forceinline__ void body2(const double *__restrict__ A, int I, int J,
+                                      const double *__restrict__ v, double *__restrict__ P,
+                                      long Np, double *sh) {
+  constexpr int NW = 4;
+  constexpr int RPW = B / NW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const d2 *v2 = reinterpret_cast<const d2 *>(v + (long)J * B);
+  d2 pc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+  double *vrow = sh;
+  double *rows = sh + (NW + 1) * B;  // B row sums
+  if (!DIAG) {
+    for (int i = threadIdx.x; i < B; i += NW * 64) vrow[i] = v[(long)I * B + i];
+  }
+  __syncthreads();
+  d2 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
+  double *Prow = P + (long)J * Np + (long)I * B;
+#pragma unroll 1
+  for (int g = 0; g < RPW / RB; ++g) {
+    const int rbase = IL ? (g * NW + w) * RB : w * RPW + g * RB;
+    const d2 *rowp = reinterpret_cast<const d2 *>(A + (long)rbase * B) + lane;
+    d2 a[RB][4];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+    double vals[RB];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      double s0 = a[rr][0].x * pc[0].x;
+      double s1 = a[rr][0].y * pc[0].y;
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        s0 = fma(a[rr][q].x, pc[q].x, s0);
+        s1 = fma(a[rr][q].y, pc[q].y, s1);
+      }
+      vals[rr] = s0 + s1;
+      if (!DIAG) {
+        const double pr = vrow[rbase + rr];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q].x = fma(a[rr][q].x, pr, acc[q].x);
+          acc[q].y = fma(a[rr][q].y, pr, acc[q].y);
+        }
+      }
+    }
+    const double rs = batch_reduce<RB>(vals, lane);
+    if (lane < RB) {
+      if (LDSROWS) rows[rbase + row_of_lane<RB>(lane)] = rs;
+      else Prow[rbase + row_of_lane<RB>(lane)] = rs;
+    }
+  }
+  if (LDSROWS || !DIAG) __syncthreads();
+  if (LDSROWS)
+    for (int c = threadIdx.x; c < B; c += NW * 64) Prow[c] = rows[c];
+  if (!DIAG) {
+    d2 *cs = reinterpret_cast<d2 *>(sh + B);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs[w * (B / 2) + lane + 64 * q] = acc[q];
+    __syncthreads();
+    double *Pcol = P + (long)I * Np + (long)J * B;
+    const double *csd = sh + B;
+    for (int c = threadIdx.x; c < B; c += NW * 64)
+      Pcol[c] = (csd[c] + csd[B + c]) + (csd[2 * B + c] + csd[3 * B + c]);
+  }
+}
+
+template <int RB, bool LDSROWS, bool IL>
+__global__ __launch_bounds__(256) void k_symv2(const double *__restrict__ tiles,
+                                               const int2 *__restrict__ list,
+                                               const double *__restrict__ v,
+                                               double *__restrict__ P, long Np) {
+  __shared__ double sh[6 * B];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body2<RB, LDSROWS, IL, true>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body2<RB, LDSROWS, IL, false>(A, t.x, t.y, v, P, Np, sh);
+}
+
+// variant 3 (GEMV-like): the 4 waves share every row; thread t owns columns 2t, 2t+1
+// (column partials stay in registers, no cross-wave column reduction); row sums
+// = wave butterfly + 4-way LDS sum per batch of RB rows.
+template <int RB, bool DIAG>
+__device__ __forceinline__ void body3(const double *__restrict__ A, int I, int J,
+                                      const double *__restrict__ v, double *__restrict__ P,
+                                      long Np, double *sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, t = threadIdx.x;
+  const d2 pc = reinterpret_cast<const d2 *>(v + (long)J * B)[t];
+  double *vrow = sh;            // B
+  double *part = sh + B;        // 2 x 4 x RB
+  double *rows = part + 8 * RB; // B
+  if (!DIAG)
+    for (int i = t; i < B; i += 256) vrow[i] = v[(long)I * B + i];
+  __syncthreads();
+  d2 acc = {0.0, 0.0};
+  const d2 *base = reinterpret_cast<const d2 *>(A) + t;
+#pragma unroll 1
+  for (int g = 0; g < B / RB; ++g) {
+    d2 a[RB];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) a[rr] = __builtin_nontemporal_load(base + (long)(g * RB + rr) * (B / 2));
+    double vals[RB];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      vals[rr] = fma(a[rr].x, pc.x, a[rr].y * pc.y);
+      if (!DIAG) {
+        const double pr = vrow[g * RB + rr];
+        acc.x = fma(a[rr].x, pr, acc.x);
+        acc.y = fma(a[rr].y, pr, acc.y);
+      }
+    }
+    const double rs = batch_reduce<RB>(vals, lane);
+    double *pb = part + (g & 1) * 4 * RB;
+    if (lane < RB) pb[w * RB + row_of_lane<RB>(lane)] = rs;
+    __syncthreads();
+    if (t < RB) rows[g * RB + t] = (pb[t] + pb[RB + t]) + (pb[2 * RB + t] + pb[3 * RB + t]);
+  }
+  __syncthreads();
+  double *Prow = P + (long)J * Np + (long)I * B;
+  for (int c = t; c < B; c += 256) Prow[c] = rows[c];
+  if (!DIAG) {
+    d2 *Pcol = reinterpret_cast<d2 *>(P + (long)I * Np + (long)J * B);
+    Pcol[t] = acc;
+  }
+}
+
+template <int RB>
+__global__ __launch_bounds__(256) void k_symv3(const double *__restrict__ tiles,
+                                               const int2 *__restrict__ list,
+                                               const double *__restrict__ v,
+                                               double *__restrict__ P, long Np) {
+  __shared__ double sh[2 * B + 8 * RB];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body3<RB, true>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body3<RB, false>(A, t.x, t.y, v, P, Np, sh);
+}
+
 __global__ void k_reduce(const double *__restrict__ P, long Np, int nb, long n,
                          double *__restrict__ y) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -168,6 +317,64 @@ __global__ __launch_bounds__(256) void k_stream(const d2 *__restrict__ A, long n
     acc += a;
   }
   if (acc.x == 12345.678) out[0] = acc.y;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_u(const d2 *__restrict__ A, long n2,
+                                                  double *__restrict__ out) {
+  d2 acc = {0.0, 0.0};
+  const long stride = (long)gridDim.x * 256;
+  long i = (long)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n2; i += U * stride) {
+    d2 a[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(A + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += a[u];
+  }
+  if (acc.x == 12345.678) out[0] = acc.y;
+}
+
+// copy of the library's dense row GEMV k_gemv<4,4,1>
+template <int R, int U>
+__global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, long ld, long rows,
+                                              const double *__restrict__ v, double *__restrict__ y) {
+  __shared__ double sh[4 * R];
+  const long r0 = (long)blockIdx.x * R;
+  const long n2 = ld / 2;
+  const d2 *v2 = reinterpret_cast<const d2 *>(v);
+  const d2 *rowp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) rowp[r] = reinterpret_cast<const d2 *>(M + (r0 + r) * ld);
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
+  for (long c = threadIdx.x; c + (long)(U - 1) * 256 < n2; c += 256L * U) {
+    d2 xv[U];
+    d2 kv[R][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) xv[u] = v2[c + u * 256];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < U; ++u) kv[r][u] = __builtin_nontemporal_load(rowp[r] + c + u * 256);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[r] = fma(kv[r][u].x, xv[u].x, acc[r]);
+        acc[r] = fma(kv[r][u].y, xv[u].y, acc[r]);
+      }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    double s = acc[r];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+    if (lane == 0) sh[w * R + r] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) y[r0 + threadIdx.x] = (sh[threadIdx.x] + sh[R + threadIdx.x]) + (sh[2 * R + threadIdx.x] + sh[3 * R + threadIdx.x]);
 }
 
 __global__ void k_fill(double *A, long n, unsigned seed) {
@@ -208,7 +415,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&tiles, sizeof(double) * nt * B * B));
   CK(hipMalloc(&v, sizeof(double) * Np));
   CK(hipMalloc(&P, sizeof(double) * nb * Np));
-  CK(hipMalloc(&y, sizeof(double) * Np));
+  CK(hipMalloc(&y, sizeof(double) * Np * 2));
   CK(hipMalloc(&out, sizeof(double)));
   CK(hipMalloc(&dl, sizeof(int2) * nt));
   CK(hipMemcpy(dl, list.data(), sizeof(int2) * nt, hipMemcpyHostToDevice));
@@ -229,13 +436,45 @@ int main(int argc, char **argv) {
   }, reps);                                                                                \
   printf("symv RB=%d NW=%d PF=%d  %.3f ms  %.0f GB/s\n", RB, NW, (int)PF, ms, bytes / ms / 1e6);
   RUN(8, 4, false)
-  RUN(4, 4, false)
-  RUN(4, 4, true)
   RUN(8, 4, true)
-  RUN(8, 8, false)
-  RUN(4, 8, false)
-  RUN(4, 8, true)
-  RUN(2, 4, true)
+#define RUN2(RB, LR, IL)                                                                   \
+  ms = time_it([&] {                                                                       \
+    hipLaunchKernelGGL((k_symv2<RB, LR, IL>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np); \
+  }, reps);                                                                                \
+  printf("symv2 RB=%d LDSROWS=%d IL=%d  %.3f ms  %.0f GB/s\n", RB, (int)LR, (int)IL, ms, bytes / ms / 1e6);
+  RUN2(8, true, true)
+#define RUN3(RB)                                                                           \
+  ms = time_it([&] {                                                                       \
+    hipLaunchKernelGGL((k_symv3<RB>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np); \
+  }, reps);                                                                                \
+  printf("symv3 RB=%d  %.3f ms  %.0f GB/s\n", RB, ms, bytes / ms / 1e6);
+  RUN3(8)
+  RUN3(16)
+  RUN3(32)
+  // tail test: the first multiple of 512 tiles only
+  {
+    const long nt2 = nt / 512 * 512;
+    ms = time_it([&] {
+      hipLaunchKernelGGL((k_symv<8, 4, true>), dim3((unsigned)nt2), dim3(256), 0, 0, tiles, dl, v, P, Np);
+    }, reps);
+    printf("symv 8,4,PF on %ld tiles  %.3f ms  %.0f GB/s\n", nt2, ms, 8.0 * nt2 * B * B / ms / 1e6);
+  }
+  ms = time_it([&] {
+    hipLaunchKernelGGL((k_stream_u<8>), dim3(4096), dim3(256), 0, 0, (const d2 *)tiles, nt * B * B / 2, out);
+  }, reps);
+  printf("stream-read U=8 g4096 %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  ms = time_it([&] {
+    hipLaunchKernelGGL((k_stream_u<8>), dim3(16384), dim3(256), 0, 0, (const d2 *)tiles, nt * B * B / 2, out);
+  }, reps);
+  printf("stream-read U=8 g16k %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  {
+    const long ld = 65536, rows = nt * B * B / ld;
+    ms = time_it([&] {
+      hipLaunchKernelGGL((k_gemv<4, 4>), dim3((unsigned)(rows / 4)), dim3(256), 0, 0, tiles, ld, rows, v, y);
+    }, reps);
+    printf("dense gemv<4,4> on same bytes (%ld x %ld)  %.3f ms  %.0f GB/s\n", rows, ld, ms,
+           8.0 * rows * ld / ms / 1e6);
+  }
   ms = time_it([&] {
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, 0, P, Np, nb, N, y);
   }, reps);

@@ -37,8 +37,8 @@ def test_matfree_matches_reference_kop(sg, golden_dir, name):
         s.set_operator(-1.0, lam)
         assert s.storage_info()[0] == "matfree"
         y = s.matvec(f["v"])
-        with pytest.raises(RuntimeError):  # builds need the assembled K
-            s.precon_pivchol(10)
+        with pytest.raises(RuntimeError):  # the eigen preconditioner factors all of K
+            s.precon_eig(5)
     ref = -f["Kop_v"]  # (-K + lam I) v
     assert np.linalg.norm(y - ref) <= 1e-13 * np.linalg.norm(ref)
 
@@ -122,3 +122,36 @@ def test_matfree_sharded(sg, golden_dir, world):
     y = np.concatenate(outs)
     ref = -f["Kop_v"]
     assert np.linalg.norm(y - ref) <= 1e-13 * np.linalg.norm(ref)
+
+
+@pytest.mark.parametrize("name", ["sgdml_ethanol_n621", "sgdml_ethanol_n270_perms"])
+def test_matfree_builds_match_dense(sg, golden_dir, name):
+    """Preconditioner builds without K: diagonal from the diagonal blocks, columns
+    through the operator (K_op e_i, iterative_cholesky.py:152-156)."""
+    f = load_golden(golden_dir, name)
+    n, lam, sig = f["y"].size, float(f["lam"]), float(f["sig"])
+    k = int(f["k_rot"])
+    idx = np.sort(f["nys_idx"]).astype(np.int64)
+    out = {}
+    for mode in ("dense", "matfree"):
+        with sg.KernelSolver(n) as s:
+            if mode == "dense":
+                s.assemble_sgdml(f["R_desc"], f["R_d_desc"], f["perms"], sig)
+                s.set_storage("dense")
+            else:
+                s.sgdml_operator(f["R_desc"], f["R_d_desc"], f["perms"], sig)
+            s.set_operator(-1.0, lam)
+            d = s.diag()
+            piv, _ = s.precon_pivchol(k)
+            Tp = s.precon_panel()
+            s.precon_nystrom(idx, variant=0)
+            Tn = s.precon_panel()
+            lev = s.lev_scores(idx, lam)
+            out[mode] = (d, piv, Tp, Tn, lev)
+    dd, pd, Tpd, Tnd, ld = out["dense"]
+    dm, pm, Tpm, Tnm, lm = out["matfree"]
+    np.testing.assert_allclose(dm, dd, rtol=1e-14, atol=0)
+    np.testing.assert_array_equal(pm[:k], pd[:k])
+    np.testing.assert_allclose(Tpm, Tpd, rtol=0, atol=1e-8 * np.abs(Tpd).max())
+    np.testing.assert_allclose(Tnm, Tnd, rtol=0, atol=1e-8 * np.abs(Tnd).max())
+    np.testing.assert_allclose(lm, ld, rtol=1e-8, atol=1e-12)
