@@ -1,0 +1,22 @@
+#!/bin/bash
+# default bench line (with CPU baseline, solve, parity) + rocprofv3 stats + PMC of the bench.
+set -u
+mkdir -p gpurun_out
+L=gpurun_out/bench_prof.log
+: > $L
+export TMPDIR=/tmp
+step() {
+  local t=$1 name=$2; shift 2
+  echo "=== $name" >> $L
+  timeout -k 10 $t "$@" >> $L 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >> $L
+  if [ $rc -ge 2 ]; then echo "stopping after $name (rc=$rc)" >> $L; exit $rc; fi
+  return 0
+}
+step 900 bench python bench.py
+step 600 stats rocprofv3 --kernel-trace --stats -d gpurun_out/r01_sym_stats -o bench --output-format csv -- python3 bench.py --steps 30 --warmup 3 --no-cpu --no-solve
+step 600 fetch rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r01_sym_fetch -o bench --output-format csv -- python3 bench.py --steps 6 --warmup 1 --no-cpu --no-solve
+step 600 write rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r01_sym_write -o bench --output-format csv -- python3 bench.py --steps 6 --warmup 1 --no-cpu --no-solve
+step 600 nt_stats rocprofv3 --kernel-trace --stats -d gpurun_out/r01_nt_stats -o bench --output-format csv -- python3 bench.py --workload nanotube --steps 30 --warmup 3
+echo done >> $L

@@ -299,6 +299,86 @@ __global__ __launch_bounds__(256) void k_symv3(const double *__restrict__ tiles,
     body3<RB, false>(A, t.x, t.y, v, P, Np, sh);
 }
 
+// variant 4: symv2 (IL, LDS rows) with p columns read from LDS and an occupancy target
+template <int RB, bool DIAG>
+__device__ __forceinline__ void body4(const double *__restrict__ A, int I, int J,
+                                      const double *__restrict__ v, double *__restrict__ P,
+                                      long Np, double *sh) {
+  constexpr int NW = 4;
+  constexpr int RPW = B / NW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double *vrow = sh;                // B
+  d2 *vcol = reinterpret_cast<d2 *>(sh + B);  // B doubles
+  double *rows = sh + 2 * B;        // B
+  double *cs = sh + 3 * B;          // 4 x B
+  for (int i = threadIdx.x; i < B; i += 256) {
+    if (!DIAG) vrow[i] = v[(long)I * B + i];
+    sh[B + i] = v[(long)J * B + i];
+  }
+  __syncthreads();
+  d2 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
+#pragma unroll 1
+  for (int g = 0; g < RPW / RB; ++g) {
+    const int rbase = (g * NW + w) * RB;
+    const d2 *rowp = reinterpret_cast<const d2 *>(A + (long)rbase * B) + lane;
+    d2 a[RB][4];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+    double vals[RB];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const d2 pc = vcol[lane + 64 * q];
+        s0 = fma(a[rr][q].x, pc.x, s0);
+        s1 = fma(a[rr][q].y, pc.y, s1);
+      }
+      vals[rr] = s0 + s1;
+      if (!DIAG) {
+        const double pr = vrow[rbase + rr];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q].x = fma(a[rr][q].x, pr, acc[q].x);
+          acc[q].y = fma(a[rr][q].y, pr, acc[q].y);
+        }
+      }
+    }
+    const double rs = batch_reduce<RB>(vals, lane);
+    if (lane < RB) rows[rbase + row_of_lane<RB>(lane)] = rs;
+  }
+  if (!DIAG) {
+    d2 *cs2 = reinterpret_cast<d2 *>(cs);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs2[w * (B / 2) + lane + 64 * q] = acc[q];
+  }
+  __syncthreads();
+  double *Prow = P + (long)J * Np + (long)I * B;
+  for (int c = threadIdx.x; c < B; c += 256) Prow[c] = rows[c];
+  if (!DIAG) {
+    double *Pcol = P + (long)I * Np + (long)J * B;
+    for (int c = threadIdx.x; c < B; c += 256)
+      Pcol[c] = (cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]);
+  }
+}
+
+template <int RB, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void k_symv4(const double *__restrict__ tiles, const int2 *__restrict__ list,
+             const double *__restrict__ v, double *__restrict__ P, long Np) {
+  __shared__ double sh[7 * B];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body4<RB, true>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body4<RB, false>(A, t.x, t.y, v, P, Np, sh);
+}
+
 __global__ void k_reduce(const double *__restrict__ P, long Np, int nb, long n,
                          double *__restrict__ y) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -435,7 +515,6 @@ int main(int argc, char **argv) {
                        dl, v, P, Np);                                                      \
   }, reps);                                                                                \
   printf("symv RB=%d NW=%d PF=%d  %.3f ms  %.0f GB/s\n", RB, NW, (int)PF, ms, bytes / ms / 1e6);
-  RUN(8, 4, false)
   RUN(8, 4, true)
 #define RUN2(RB, LR, IL)                                                                   \
   ms = time_it([&] {                                                                       \
@@ -448,9 +527,17 @@ int main(int argc, char **argv) {
     hipLaunchKernelGGL((k_symv3<RB>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np); \
   }, reps);                                                                                \
   printf("symv3 RB=%d  %.3f ms  %.0f GB/s\n", RB, ms, bytes / ms / 1e6);
-  RUN3(8)
-  RUN3(16)
-  RUN3(32)
+#define RUN4(RB, WPE)                                                                      \
+  ms = time_it([&] {                                                                       \
+    hipLaunchKernelGGL((k_symv4<RB, WPE>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np); \
+  }, reps);                                                                                \
+  printf("symv4 RB=%d WPE=%d  %.3f ms  %.0f GB/s\n", RB, WPE, ms, bytes / ms / 1e6);
+  RUN4(8, 1)
+  RUN4(8, 2)
+  RUN4(8, 3)
+  RUN4(12, 2)
+  RUN4(6, 3)
+  RUN4(4, 4)
   // tail test: the first multiple of 512 tiles only
   {
     const long nt2 = nt / 512 * 512;
