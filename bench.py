@@ -300,7 +300,10 @@ def main():
             "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            # BASELINE.md publishes a CG step time only for the nanotube (0.105 s/step at
+            # N = 15540, data/data/cg_performance_n=15750/..._nanotube_points14_meas31)
+            "vs_baseline": (args.steps / el) / (1.0 / 0.105)
+            if args.workload == "nanotube" and n == 15540 else None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": workload, "n": n, "k": k, "lambda": lam,
