@@ -69,6 +69,8 @@ struct MfData {
   double *m5 = nullptr, *w = nullptr;     // ni x (M n_perms), x independent
   double *c = nullptr, *F = nullptr;      // ni x (M n_perms), ni x D scratch
   double *part = nullptr;                 // nz x ni x (M n_perms) pair partial sums
+  double *ypart = nullptr;                // J^T partial rows (slices x nrows)
+  double *xc = nullptr;                   // contiguous operand (world > 1)
   int nz = 1;                             // descriptor slices of the pair sums
   int64_t dslice = 0;
   std::vector<int32_t> perms, piinv;      // host copies (diagonal blocks)

@@ -46,14 +46,25 @@ __global__ __launch_bounds__(256) void k_mf_rt(const double *__restrict__ Rd,
     Rt[jp * D + d] = Rd[j * D + Pt[p * D + d]];
 }
 
+// contiguous copy of the padded rank-block vector (several ranks only)
+__global__ __launch_bounds__(256) void k_mf_contig(const double *__restrict__ x, int64_t N,
+                                                   int64_t rows_per, int64_t blk,
+                                                   double *__restrict__ xc,
+                                                   const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g < N) xc[g] = x[xpos(g, rows_per, blk)];
+}
+
 // Zt[jp, d] = sum_c Rdd_j[e, c] (x_j[t_e, c] - x_j[s_e, c]),  e = P_p[d], pair e = (s_e > t_e)
+// (x contiguous in the global index)
 __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               const int32_t *__restrict__ Pt,
                                               const int32_t *__restrict__ ps,
                                               const int32_t *__restrict__ pt, int64_t M,
                                               int n, int n_perms, int64_t D,
-                                              const double *__restrict__ x, int64_t rows_per,
-                                              int64_t blk, double *__restrict__ Zt,
+                                              const double *__restrict__ x,
+                                              double *__restrict__ Zt,
                                               const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   const int64_t jp = blockIdx.y;
@@ -66,19 +77,22 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
     double z = 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const double xt = x[xpos(g0 + 3 * t + c, rows_per, blk)];
-      const double xs = x[xpos(g0 + 3 * s + c, rows_per, blk)];
+      const double xt = x[g0 + 3 * t + c];
+      const double xs = x[g0 + 3 * s + c];
       z = fma(r[c], xt - xs, z);
     }
     Zt[jp * D + d] = z;
   }
 }
 
-// Partial pair sums over the descriptor slice z of this workgroup, for the
-// points il in [ic0, ic0 + kIC):
+// Partial pair sums over the descriptor slice z of this workgroup for a tile of
+// 16 query points x 16 (training point, permutation) pairs; thread (ti, tj) owns
+// one pair, the slice is staged through LDS in chunks of 64 entries:
 //   MODE 0: |Rd_i - Rt[jp]|^2                (setup)
 //   MODE 1: (Rd_i - Rt[jp]) . Zt[jp]
-// part[(z * ni + il) * MP + jp]; k_mf_pair_fin sums the slices in order.
+// part[(z * ni + il) * MP + jp]; k_mf_pair_fin sums the slices in a fixed order.
+constexpr int kPT = 16;  // tile edge (points and pairs)
+constexpr int kDC = 64;  // descriptor chunk staged in LDS
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
                                                  const double *__restrict__ Rt,
@@ -87,45 +101,39 @@ __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
                                                  int64_t MP, double *__restrict__ part,
                                                  const int *__restrict__ status) {
   if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sh[4][kIC];
-  const int64_t jp = blockIdx.x;
-  const int64_t ic0 = (int64_t)blockIdx.y * kIC;
-  const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
+  __shared__ double sR[kPT][kDC + 1];
+  __shared__ double sT[kPT][kDC + 1];
+  __shared__ double sZ[MODE == 1 ? kPT : 1][kDC + 1];
+  const int64_t jp0 = (int64_t)blockIdx.x * kPT;
+  const int64_t ic0 = (int64_t)blockIdx.y * kPT;
   const int64_t d0 = (int64_t)blockIdx.z * dslice;
   const int64_t d1 = (d0 + dslice) < D ? (d0 + dslice) : D;
-  double acc[kIC];
-#pragma unroll
-  for (int k = 0; k < kIC; ++k) acc[k] = 0.0;
-  const double *rt = Rt + jp * D;
-  const double *zt = Zt + jp * D;
-  for (int64_t d = d0 + threadIdx.x; d < d1; d += 256) {
-    const double r = rt[d];
-    const double v = MODE == 1 ? zt[d] : 0.0;
-#pragma unroll
-    for (int k = 0; k < kIC; ++k) {
-      if (k < nk) {
-        const double df = Rd[(i0 + ic0 + k) * D + d] - r;
-        acc[k] = fma(df, MODE == 0 ? df : v, acc[k]);
-      }
+  const int tj = threadIdx.x & (kPT - 1), ti = threadIdx.x / kPT;
+  double acc = 0.0;
+  for (int64_t c0 = d0; c0 < d1; c0 += kDC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < kPT * kDC; e += 256) {
+      const int r = e / kDC, cc = e % kDC;
+      const int64_t d = c0 + cc;
+      const bool okd = d < d1;
+      const int64_t il = ic0 + r, jp = jp0 + r;
+      sR[r][cc] = (okd && il < ni) ? Rd[(i0 + il) * D + d] : 0.0;
+      sT[r][cc] = (okd && jp < MP) ? Rt[jp * D + d] : 0.0;
+      if (MODE == 1) sZ[r][cc] = (okd && jp < MP) ? Zt[jp * D + d] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int cc = 0; cc < kDC; ++cc) {
+      const double df = sR[ti][cc] - sT[tj][cc];
+      acc = fma(df, MODE == 0 ? df : sZ[MODE == 1 ? tj : 0][cc], acc);
     }
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kIC; ++k) {
-    double v = acc[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    if (lane == 0) sh[w][k] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < nk) {
-    const int k = threadIdx.x;
-    part[((int64_t)blockIdx.z * ni + ic0 + k) * MP + jp] =
-        (sh[0][k] + sh[1][k]) + (sh[2][k] + sh[3][k]);
-  }
+  const int64_t il = ic0 + ti, jp = jp0 + tj;
+  if (il < ni && jp < MP) part[((int64_t)blockIdx.z * ni + il) * MP + jp] = acc;
 }
 
-// MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot
+// MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot.  One wave per
+// output: lanes stride over the nz slices, fixed-order wave sum.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ part, int nz,
                                                      int64_t nout, double sig,
@@ -134,10 +142,14 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
                                                      double *__restrict__ out1,
                                                      const int *__restrict__ status) {
   if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
-  const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (o >= nout) return;
   double s = 0.0;
-  for (int z = 0; z < nz; ++z) s += part[(int64_t)z * nout + o];
+  for (int z = lane; z < nz; z += 64) s += part[(int64_t)z * nout + o];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  if (lane != 0) return;
   if (MODE == 0) {
     const double norm = sqrt(5.0) * sqrt(s);
     const double m = exp(-norm / sig) * 5.0 / (3.0 * sig * sig * sig * sig);
@@ -149,18 +161,20 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
 }
 
 // F[il, d] = sum_jp c[il, jp] (Rd_i[d] - Rt[jp, d]) - w[il, jp] Zt[jp, d]   (fixed jp order)
-__global__ __launch_bounds__(256) void k_mf_h(const double *__restrict__ Rd,
-                                              const double *__restrict__ Rt,
-                                              const double *__restrict__ Zt, int64_t D,
-                                              int64_t i0, int64_t ni, int64_t MP,
-                                              const double *__restrict__ cf,
-                                              const double *__restrict__ wf,
-                                              double *__restrict__ F,
-                                              const int *__restrict__ status) {
+// One wave per (64 descriptor entries, 16 query points); the coefficients of the
+// 16 points are staged in LDS 64 pairs at a time.
+__global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
+                                             const double *__restrict__ Rt,
+                                             const double *__restrict__ Zt, int64_t D,
+                                             int64_t i0, int64_t ni, int64_t MP,
+                                             const double *__restrict__ cf,
+                                             const double *__restrict__ wf,
+                                             double *__restrict__ F,
+                                             const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sc[kIC][256];
-  __shared__ double sw[kIC][256];
-  const int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double sc[kIC][64];
+  __shared__ double sw[kIC][64];
+  const int64_t d = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t ic0 = (int64_t)blockIdx.y * kIC;
   const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
   const bool act = d < D;
@@ -170,8 +184,8 @@ __global__ __launch_bounds__(256) void k_mf_h(const double *__restrict__ Rd,
     rdi[k] = (act && k < nk) ? Rd[(i0 + ic0 + k) * D + d] : 0.0;
     h[k] = 0.0;
   }
-  for (int64_t j0 = 0; j0 < MP; j0 += 256) {
-    const int cnt = (int)((MP - j0) < 256 ? (MP - j0) : 256);
+  for (int64_t j0 = 0; j0 < MP; j0 += 64) {
+    const int cnt = (int)((MP - j0) < 64 ? (MP - j0) : 64);
     __syncthreads();
     for (int k = 0; k < nk; ++k) {
       if (threadIdx.x < cnt) {
@@ -181,7 +195,21 @@ __global__ __launch_bounds__(256) void k_mf_h(const double *__restrict__ Rd,
     }
     __syncthreads();
     if (act) {
-      for (int jj = 0; jj < cnt; ++jj) {
+      int jj = 0;
+      for (; jj + 7 < cnt; jj += 8) {  // 16 loads in flight per lane
+        double r[8], z[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          r[u] = Rt[(j0 + jj + u) * D + d];
+          z[u] = Zt[(j0 + jj + u) * D + d];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int k = 0; k < kIC; ++k)
+            if (k < nk) h[k] = fma(sc[k][jj + u], rdi[k] - r[u], fma(-sw[k][jj + u], z[u], h[k]));
+      }
+      for (; jj < cnt; ++jj) {
         const double r = Rt[(j0 + jj) * D + d];
         const double z = Zt[(j0 + jj) * D + d];
 #pragma unroll
@@ -200,49 +228,120 @@ __device__ __forceinline__ int64_t pair_of(int a, int b) {
   return a > b ? (int64_t)a * (a - 1) / 2 + b : (int64_t)b * (b - 1) / 2 + a;
 }
 
-// rows of this rank: g = i 3n + 3a + c,  y = sum_{b != a} sgn J * Rdd_i[pair(a,b), c] F_i[pair(a,b)]
+// rows of this rank: g = i 3n + 3a + c,  y = sum_{b != a} sgn * Rdd_i[pair(a,b), c] F_i[pair(a,b)]
 // (J[pair, (t, c)] = +Rdd, J[pair, (s, c)] = -Rdd with s > t, desc.py:444-462).
-// One wave per (point, atom): lanes stride over the partner atoms b, 3 wave sums.
-__global__ __launch_bounds__(64) void k_mf_jt(const double *__restrict__ Rdd,
-                                              const double *__restrict__ F, int64_t D, int n,
-                                              int64_t i0, int64_t row0, int64_t nrows,
-                                              double sigma, double lam,
-                                              const double *__restrict__ xloc,
-                                              double *__restrict__ y,
-                                              const int *__restrict__ status) {
+// Workgroup = (point, block of 32 atoms a, slice of partner blocks); it walks the
+// 32 x 32 blocks (A, B) of the pair triangle: for B < A the pairs of one atom a are
+// 32 consecutive descriptor entries, for B > A those of one atom b are, so every
+// block is read with coalesced loads into registers and parked in LDS (the next
+// block's loads are issued before the current one is consumed).  8 threads per
+// atom sum 4 partners each; slices are summed in order by k_mf_jt_fin.
+constexpr int kAB = 32;
+constexpr int kJS = 4;  // partner-block slices
+
+__device__ __forceinline__ void jt_load(const double *__restrict__ Fi,
+                                        const double *__restrict__ Ri, int n, int A0, int B0,
+                                        double (&f)[4], double (&r)[4][3], int (&la)[4],
+                                        int (&lb)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int rr = e / kAB, q = e % kAB;
+    const int aa = B0 < A0 ? A0 + rr : A0 + q;
+    const int bb = B0 < A0 ? B0 + q : B0 + rr;
+    la[u] = aa - A0;
+    lb[u] = bb - B0;
+    f[u] = 0.0;
+    r[u][0] = r[u][1] = r[u][2] = 0.0;
+    if (aa < n && bb < n && aa != bb) {
+      const int64_t d = pair_of(aa, bb);
+      const double sg = aa > bb ? -1.0 : 1.0;
+      f[u] = sg * Fi[d];
+      r[u][0] = Ri[d * 3 + 0];
+      r[u][1] = Ri[d * 3 + 1];
+      r[u][2] = Ri[d * 3 + 2];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
+                                               const double *__restrict__ F, int64_t D, int n,
+                                               int64_t i0, int64_t row0, int64_t nrows,
+                                               double *__restrict__ part,
+                                               const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  const int a = blockIdx.x;
+  __shared__ double sF[kAB][kAB + 1];
+  __shared__ double sR[3][kAB][kAB + 1];
+  const int A0 = blockIdx.x * kAB;
   const int64_t i = i0 + blockIdx.y;
   const int64_t n3 = 3 * (int64_t)n;
-  const int64_t g0 = i * n3 + 3 * a;  // global row of component 0
-  if (g0 + 2 < row0 || g0 >= row0 + nrows) return;
+  const int64_t gfirst = i * n3 + 3 * (int64_t)A0;
+  const int64_t glast = i * n3 + 3 * (int64_t)(A0 + kAB < n ? A0 + kAB : n) - 1;
+  if (glast < row0 || gfirst >= row0 + nrows) return;
   const double *Fi = F + (int64_t)blockIdx.y * D;
   const double *Ri = Rdd + i * D * 3;
+  const int al = threadIdx.x >> 3, pt = threadIdx.x & 7;
+  const int a = A0 + al;
+  const int nblk = (n + kAB - 1) / kAB;
+  const int bz0 = (int)(((int64_t)nblk * blockIdx.z) / kJS);
+  const int bz1 = (int)(((int64_t)nblk * (blockIdx.z + 1)) / kJS);
   double acc[3] = {0.0, 0.0, 0.0};
-  for (int b = threadIdx.x; b < n; b += 64) {
-    if (b == a) continue;
-    const int64_t e = pair_of(a, b);
-    const double f = a > b ? -Fi[e] : Fi[e];
+  double f[4], r[4][3];
+  int la[4], lb[4];
+  if (bz0 < bz1) jt_load(Fi, Ri, n, A0, bz0 * kAB, f, r, la, lb);
+  for (int bk = bz0; bk < bz1; ++bk) {
+    __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 3; ++c) acc[c] = fma(Ri[e * 3 + c], f, acc[c]);
+    for (int u = 0; u < 4; ++u) {
+      sF[la[u]][lb[u]] = f[u];
+      sR[0][la[u]][lb[u]] = r[u][0];
+      sR[1][la[u]][lb[u]] = r[u][1];
+      sR[2][la[u]][lb[u]] = r[u][2];
+    }
+    __syncthreads();
+    if (bk + 1 < bz1) jt_load(Fi, Ri, n, A0, (bk + 1) * kAB, f, r, la, lb);
+#pragma unroll
+    for (int k = 0; k < kAB / 8; ++k) {
+      const int q = pt * (kAB / 8) + k;
+      const double fv = sF[al][q];
+      acc[0] = fma(sR[0][al][q], fv, acc[0]);
+      acc[1] = fma(sR[1][al][q], fv, acc[1]);
+      acc[2] = fma(sR[2][al][q], fv, acc[2]);
+    }
   }
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     double v = acc[c];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    v += __shfl_down(v, 4, 8);
+    v += __shfl_down(v, 2, 8);
+    v += __shfl_down(v, 1, 8);
     acc[c] = v;
   }
-  if (threadIdx.x == 0) {
+  if (pt == 0 && a < n) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const int64_t r = g0 + c - row0;
-      if (r < 0 || r >= nrows) continue;
-      double yv = sigma * acc[c];
-      if (xloc != nullptr) yv += lam * xloc[r];
-      y[r] = yv;
+      const int64_t rr = i * n3 + 3 * (int64_t)a + c - row0;
+      if (rr < 0 || rr >= nrows) continue;
+      part[(int64_t)blockIdx.z * nrows + rr] = acc[c];
     }
   }
+}
+
+// y = sigma * sum_z part[z] + lam * x (fixed slice order)
+__global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ part, int64_t nrows,
+                                                   double sigma, double lam,
+                                                   const double *__restrict__ xloc,
+                                                   double *__restrict__ y,
+                                                   const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nrows) return;
+  double s = 0.0;
+#pragma unroll
+  for (int z = 0; z < kJS; ++z) s += part[(int64_t)z * nrows + r];
+  double yv = sigma * s;
+  if (xloc != nullptr) yv += lam * xloc[r];
+  y[r] = yv;
 }
 
 }  // namespace
@@ -284,6 +383,8 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   MLFF_HIP(ctx, hipMalloc(&mf.w, sizeof(double) * nic * MP));
   MLFF_HIP(ctx, hipMalloc(&mf.c, sizeof(double) * nic * MP));
   MLFF_HIP(ctx, hipMalloc(&mf.F, sizeof(double) * nic * D));
+  if (ctx->world > 1) MLFF_HIP(ctx, hipMalloc(&mf.xc, sizeof(double) * ctx->N));
+  MLFF_HIP(ctx, hipMalloc(&mf.ypart, sizeof(double) * kJS * std::max<int64_t>(ctx->nrows, 1)));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Rd, R_desc, sizeof(double) * M * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Rdd, R_d_desc, sizeof(double) * M * D * 3, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Pt, Pt.data(), sizeof(int32_t) * n_perms * D, hipMemcpyHostToDevice, s));
@@ -295,17 +396,19 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   hipLaunchKernelGGL(k_mf_rt, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rd, mf.Pt, M, n_perms, D,
                      mf.Rt);
   // descriptor slices of the pair sums: enough workgroups to cover the chip
-  const int64_t gi = (mf.ni + kIC - 1) / kIC;
-  int64_t nz = (1024 + MP * gi - 1) / std::max<int64_t>(MP * gi, 1);
-  nz = std::max<int64_t>(1, std::min<int64_t>(nz, (D + 1023) / 1024));
-  mf.nz = (int)nz;
-  mf.dslice = round_up((D + nz - 1) / nz, 256);
+  const int64_t tiles = ((MP + kPT - 1) / kPT) * ((mf.ni + kPT - 1) / kPT);
+  int64_t nz = (1024 + tiles - 1) / std::max<int64_t>(tiles, 1);
+  nz = std::max<int64_t>(1, std::min<int64_t>(nz, (D + kDC - 1) / kDC));
+  mf.dslice = round_up((D + nz - 1) / nz, kDC);
+  mf.nz = (int)((D + mf.dslice - 1) / mf.dslice);
+  nz = mf.nz;
   MLFF_HIP(ctx, hipMalloc(&mf.part, sizeof(double) * nz * nic * MP));
   if (mf.ni > 0) {
-    hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)MP, (unsigned)gi, (unsigned)nz), dim3(256), 0,
+    hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)((MP + kPT - 1) / kPT),
+                       (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)nz), dim3(256), 0,
                        s, mf.Rd, mf.Rt, (const double *)nullptr, D, mf.dslice, mf.i0, mf.ni, MP,
                        mf.part, (const int *)nullptr);
-    hipLaunchKernelGGL(k_mf_pair_fin<0>, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(k_mf_pair_fin<0>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0,
                        s, mf.part, mf.nz, mf.ni * MP, sig, (const double *)nullptr, mf.m5, mf.w,
                        (const int *)nullptr);
   }
@@ -321,19 +424,29 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
   const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+  // on one rank the padded layout is the global index itself (rows_per = N)
+  const double *xc = x_full;
+  if (ctx->world > 1) {
+    hipLaunchKernelGGL(k_mf_contig, dim3((unsigned)((ctx->N + 255) / 256)), dim3(256), 0, s, x_full,
+                       ctx->N, ctx->rows_per, ctx->blk, mf.xc, status);
+    xc = mf.xc;
+  }
   hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
-                     mf.M, mf.n, mf.n_perms, mf.D, x_full, ctx->rows_per, ctx->blk, mf.Zt, status);
+                     mf.M, mf.n, mf.n_perms, mf.D, xc, mf.Zt, status);
   if (mf.ni == 0) return;
   const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
-  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)MP, gi, (unsigned)mf.nz), dim3(256), 0, s, mf.Rd,
-                     mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part, status);
-  hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)((MP + kPT - 1) / kPT),
+                     (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
+                     mf.Rd, mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part, status);
+  hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
                      mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
-  hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 255) / 256), gi), dim3(256), 0, s, mf.Rd,
+  hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 63) / 64), gi), dim3(64), 0, s, mf.Rd,
                      mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
-  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)mf.n, (unsigned)mf.ni), dim3(64), 0, s, mf.Rdd,
-                     mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows, sigma, lam, x_loc,
-                     y_loc, status);
+  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, kJS),
+                     dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
+                     mf.ypart, status);
+  hipLaunchKernelGGL(k_mf_jt_fin, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s,
+                     mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, status);
 }
 
 // diag(sigma K) of this rank's rows (assembly kernels on the diagonal blocks only)
@@ -357,7 +470,7 @@ double mf_bytes(const mlff_ctx *ctx) {
 void mf_free(MfData &mf) {
   for (void *p : {(void *)mf.Rd, (void *)mf.Rdd, (void *)mf.Rt, (void *)mf.Zt, (void *)mf.Pt,
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
-                  (void *)mf.F, (void *)mf.part})
+                  (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc})
     if (p) (void)hipFree(p);
   mf = MfData();
 }
