@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=65536)
-    ap.add_argument("--k", type=int, default=256)
+    ap.add_argument("--k", type=int, default=None,
+                    help="preconditioner rank (rbf: 256; sGDML: the rule of thumb, e.g. 2701 "
+                         "for the nanotube; configs[4] uses 1024)")
     ap.add_argument("--lam", type=float, default=1e-6)
     ap.add_argument("--ell", type=float, default=0.2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -202,7 +204,7 @@ def sgdml_workload(args, rank, world, local, pg):
     n_atoms = ds["R"].shape[1]
     n = 3 * n_atoms * M
     m, kmin, _ = get_params(name)
-    k = int(rule_of_thumb(n=n, k_min=kmin, m=m))
+    k = args.k if args.k else int(rule_of_thumb(n=n, k_min=kmin, m=m))
     y, _ = synthetic.labels(ds["F"])
     t0 = time.perf_counter()
     Rd, Rdd = sgdml_amd.sgdml_descriptors(ds["R"])
@@ -227,7 +229,7 @@ def main():
     import sgdml_amd
     from sgdml_amd import synthetic
 
-    n, k, lam, ell = args.n, args.k, args.lam, args.ell
+    n, k, lam, ell = args.n, (args.k or 256), args.lam, args.ell
     sg_info = None
     if args.workload == "rbf":
         workload = f"rbf_n{n}_nystrom{k}"

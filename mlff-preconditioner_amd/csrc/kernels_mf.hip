@@ -161,8 +161,10 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
 }
 
 // F[il, d] = sum_jp c[il, jp] (Rd_i[d] - Rt[jp, d]) - w[il, jp] Zt[jp, d]   (fixed jp order)
-// One wave per (64 descriptor entries, 16 query points); the coefficients of the
-// 16 points are staged in LDS 64 pairs at a time.
+// One wave per (64 descriptor entries, IC query points); the coefficients of the
+// IC points are staged in LDS 64 pairs at a time.  IC = 4 when 16 would leave the
+// chip with too few waves (few query points: latency bound).
+template <int IC>
 __global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
                                              const double *__restrict__ Rt,
                                              const double *__restrict__ Zt, int64_t D,
@@ -172,15 +174,15 @@ __global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
                                              double *__restrict__ F,
                                              const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sc[kIC][64];
-  __shared__ double sw[kIC][64];
+  __shared__ double sc[IC][64];
+  __shared__ double sw[IC][64];
   const int64_t d = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t ic0 = (int64_t)blockIdx.y * kIC;
-  const int nk = (int)((ni - ic0) < kIC ? (ni - ic0) : kIC);
+  const int64_t ic0 = (int64_t)blockIdx.y * IC;
+  const int nk = (int)((ni - ic0) < IC ? (ni - ic0) : IC);
   const bool act = d < D;
-  double rdi[kIC], h[kIC];
+  double rdi[IC], h[IC];
 #pragma unroll
-  for (int k = 0; k < kIC; ++k) {
+  for (int k = 0; k < IC; ++k) {
     rdi[k] = (act && k < nk) ? Rd[(i0 + ic0 + k) * D + d] : 0.0;
     h[k] = 0.0;
   }
@@ -206,21 +208,21 @@ __global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
 #pragma unroll
         for (int u = 0; u < 8; ++u)
 #pragma unroll
-          for (int k = 0; k < kIC; ++k)
+          for (int k = 0; k < IC; ++k)
             if (k < nk) h[k] = fma(sc[k][jj + u], rdi[k] - r[u], fma(-sw[k][jj + u], z[u], h[k]));
       }
       for (; jj < cnt; ++jj) {
         const double r = Rt[(j0 + jj) * D + d];
         const double z = Zt[(j0 + jj) * D + d];
 #pragma unroll
-        for (int k = 0; k < kIC; ++k)
+        for (int k = 0; k < IC; ++k)
           if (k < nk) h[k] = fma(sc[k][jj], rdi[k] - r, fma(-sw[k][jj], z, h[k]));
       }
     }
   }
   if (act)
 #pragma unroll
-    for (int k = 0; k < kIC; ++k)
+    for (int k = 0; k < IC; ++k)
       if (k < nk) F[(ic0 + k) * D + d] = h[k];
 }
 
@@ -397,7 +399,7 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
                      mf.Rt);
   // descriptor slices of the pair sums: enough workgroups to cover the chip
   const int64_t tiles = ((MP + kPT - 1) / kPT) * ((mf.ni + kPT - 1) / kPT);
-  int64_t nz = (1024 + tiles - 1) / std::max<int64_t>(tiles, 1);
+  int64_t nz = (2048 + tiles - 1) / std::max<int64_t>(tiles, 1);
   nz = std::max<int64_t>(1, std::min<int64_t>(nz, (D + kDC - 1) / kDC));
   mf.dslice = round_up((D + nz - 1) / nz, kDC);
   mf.nz = (int)((D + mf.dslice - 1) / mf.dslice);
@@ -440,8 +442,14 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                      mf.Rd, mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part, status);
   hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
                      mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
-  hipLaunchKernelGGL(k_mf_h, dim3((unsigned)((mf.D + 63) / 64), gi), dim3(64), 0, s, mf.Rd,
-                     mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+  const int64_t dblk = (mf.D + 63) / 64;
+  if (dblk * (int64_t)gi >= 4096) {
+    hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)dblk, gi), dim3(64), 0, s, mf.Rd, mf.Rt, mf.Zt,
+                       mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+  } else {
+    hipLaunchKernelGGL(k_mf_h<4>, dim3((unsigned)dblk, (unsigned)((mf.ni + 3) / 4)), dim3(64), 0, s,
+                       mf.Rd, mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+  }
   hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, kJS),
                      dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
                      mf.ypart, status);

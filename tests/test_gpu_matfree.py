@@ -155,3 +155,57 @@ def test_matfree_builds_match_dense(sg, golden_dir, name):
     np.testing.assert_allclose(Tpm, Tpd, rtol=0, atol=1e-8 * np.abs(Tpd).max())
     np.testing.assert_allclose(Tnm, Tnd, rtol=0, atol=1e-8 * np.abs(Tnd).max())
     np.testing.assert_allclose(lm, ld, rtol=1e-8, atol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_matfree_sharded_builds_and_solve(sg, golden_dir, world):
+    """Operator-only contexts on W ranks (in-process transport): pivoted Cholesky with
+    columns through the operator and a PCG solve match the single-rank run."""
+    f = load_golden(golden_dir, "sgdml_ethanol_n621")
+    n, lam, sig = f["y"].size, float(f["lam"]), float(f["sig"])
+    k = int(f["k_rot"])
+
+    def body(rank, w, key):
+        with sg.KernelSolver(n, device=0, rank=rank, world=w,
+                             comm_id=key if w > 1 else None) as s:
+            s.sgdml_operator(f["R_desc"], f["R_d_desc"], f["perms"], sig)
+            s.set_operator(-1.0, lam)
+            piv, _ = s.precon_pivchol(k)
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(f["y"][r0:r1]), tol=1e-6, maxiter=5 * n, chunk=16)
+            return piv, res
+
+    def run(w):
+        key = f"LOCAL:mfb-{w}-{np.random.default_rng().integers(1 << 60)}".encode().ljust(128, b"\0")
+        outs, errs = [None] * w, [None] * w
+
+        def th(r):
+            try:
+                outs[r] = body(r, w, key)
+            except BaseException as e:  # noqa: BLE001
+                errs[r] = e
+
+        ts = [threading.Thread(target=th, args=(r,), daemon=True) for r in range(w)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(300)
+            assert not t.is_alive()
+        for e in errs:
+            if e is not None:
+                raise e
+        return outs
+
+    ref = run(1)[0]
+    outs = run(world)
+    for piv, res in outs:
+        np.testing.assert_array_equal(piv[:k], ref[0][:k])
+        assert res.iters == outs[0][1].iters and res.info == 0
+    x = np.concatenate([res.x for _, res in outs])
+    r = ref[1]
+    # the operator and the panel agree to 1e-14 (scripts/dev/debug_mf_w3.py), but at
+    # lam = 1e-10 the iteration count is a rounding lottery (W = 3 measured 381 vs 509
+    # iterations to the same tolerance): hold the early curve and the solution instead
+    assert r.info == 0
+    np.testing.assert_allclose(outs[0][1].trace[:8], r.trace[:8], rtol=1e-6)
+    assert np.linalg.norm(x - r.x) <= 1e-5 * np.linalg.norm(r.x)
