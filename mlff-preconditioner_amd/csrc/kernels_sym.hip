@@ -16,9 +16,10 @@
 // (lane = 4 double2 columns, non-temporal 16-B loads) and forms
 //   row partials  s_i = sum_c A[i, c] v[J B + c]      -> slot J of row I B + i
 //   column partials t_c = sum_i A[i, c] v[I B + i]    -> slot I of row J B + c (I > J)
-// Row partials are reduced across the 64 lanes by a recursive-halving butterfly
-// over batches of 8 rows (10 exchanges per batch); column partials stay in
-// registers for the whole tile and are combined across the 4 waves through LDS.
+// Row partials of a batch of 8 rows are summed across the 64 lanes through a
+// wave-private LDS transpose (8 stores, 4 loads, 3 exchanges per batch); column
+// partials stay in registers for the whole tile and are combined across the 4
+// waves through LDS.
 // Every (slot, row) of the slot buffer P (nb x Np) is written by exactly one tile
 // (no atomics), and a second kernel sums the nb slots of each row in a fixed
 // order -> the result is bitwise deterministic.
@@ -34,36 +35,6 @@ constexpr int B = kSymTile;  // 512
 constexpr int kRowsPerWave = B / 4;
 constexpr int kRB = 8;  // rows per batch (loads in flight per wave: kRB x 4 KB)
 
-// Row-partial reduction of a batch of kRB rows: kRB/2 + ... + 1 halving exchanges
-// (lane bit s keeps one half of the remaining rows) then a plain xor-sum over the
-// remaining lane bits.  Afterwards every lane holds the full 64-lane sum of row
-// row_of_lane(lane) of the batch.
-__device__ __forceinline__ double batch_reduce(double (&v)[kRB], int lane) {
-#pragma unroll
-  for (int s = 0, half = kRB / 2; half >= 1; ++s, half >>= 1) {
-    const bool hi = (lane >> s) & 1;
-#pragma unroll
-    for (int k = 0; k < half; ++k) {
-      const double keep = hi ? v[k + half] : v[k];
-      const double send = hi ? v[k] : v[k + half];
-      v[k] = keep + __shfl_xor(send, 1 << s, 64);
-    }
-  }
-  double r = v[0];
-#pragma unroll
-  for (int m = kRB; m < 64; m <<= 1) r += __shfl_xor(r, m, 64);
-  return r;
-}
-
-__device__ __forceinline__ int row_of_lane(int lane) {
-  // halving step s (lane bit s) selects bit (log2(kRB) - 1 - s) of the row
-  int row = 0;
-#pragma unroll
-  for (int s = 0, half = kRB / 2; half >= 1; ++s, half >>= 1)
-    if ((lane >> s) & 1) row += half;
-  return row;
-}
-
 template <bool DIAG>
 __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, int J,
                                           const double *__restrict__ v,
@@ -74,25 +45,25 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
   d2 pc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
-  double *vrow = sh;  // v[I B .. I B + B) in LDS
-  if (!DIAG) {
+  double *vrow = sh;                       // v[I B .. I B + B)
+  double *rows = sh + B;                   // row partials of the tile
+  double *cs = sh + 2 * B;                 // 4 x B column partials
+  double *red = sh + 6 * B + w * kRB * 64; // wave-private kRB x 64 transpose buffer
+  if (!DIAG)
     for (int i = threadIdx.x; i < B; i += 256) vrow[i] = v[(int64_t)I * B + i];
-    __syncthreads();
-  }
+  __syncthreads();
   d2 acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
-  double *Prow = P + (int64_t)J * Np + (int64_t)I * B;
 #pragma unroll 1
   for (int g = 0; g < kRowsPerWave / kRB; ++g) {
-    const int rbase = w * kRowsPerWave + g * kRB;
+    const int rbase = (g * 4 + w) * kRB;  // batches interleaved across the 4 waves
     const d2 *rowp = reinterpret_cast<const d2 *>(A + (int64_t)rbase * B) + lane;
     d2 a[kRB][4];
 #pragma unroll
     for (int rr = 0; rr < kRB; ++rr)
 #pragma unroll
       for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
-    double vals[kRB];
 #pragma unroll
     for (int rr = 0; rr < kRB; ++rr) {
       double s0 = a[rr][0].x * pc[0].x;
@@ -102,7 +73,7 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
         s0 = fma(a[rr][q].x, pc[q].x, s0);
         s1 = fma(a[rr][q].y, pc[q].y, s1);
       }
-      vals[rr] = s0 + s1;
+      red[rr * 64 + lane] = s0 + s1;
       if (!DIAG) {
         const double pr = vrow[rbase + rr];
 #pragma unroll
@@ -112,20 +83,35 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
         }
       }
     }
-    const double rs = batch_reduce(vals, lane);
-    if (lane < kRB) Prow[rbase + row_of_lane(lane)] = rs;
+    // row sums: lane 8 r + c adds lanes 8c .. 8c + 7 of row r, then xor over c
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const d2 *rp = reinterpret_cast<const d2 *>(red + (lane >> 3) * 64 + (lane & 7) * 8);
+    const d2 t0 = rp[0], t1 = rp[1], t2 = rp[2], t3 = rp[3];
+    double t = ((t0.x + t0.y) + (t1.x + t1.y)) + ((t2.x + t2.y) + (t3.x + t3.y));
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 4, 64);
+    if ((lane & 7) == 0) rows[rbase + (lane >> 3)] = t;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
   if (!DIAG) {
-    // column partials: combine the 4 waves in a fixed order
-    d2 *cs = reinterpret_cast<d2 *>(sh + B);  // 4 x B doubles
-    __syncthreads();
+    d2 *cs2 = reinterpret_cast<d2 *>(cs);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cs[w * (B / 2) + lane + 64 * q] = acc[q];
-    __syncthreads();
+    for (int q = 0; q < 4; ++q) cs2[w * (B / 2) + lane + 64 * q] = acc[q];
+  }
+  __syncthreads();
+  // slot stores are non-temporal: interleaved with the tile stream they cost ~4 %
+  // of the kernel as ordinary stores (scripts/probe_symv.hip)
+  double *Prow = P + (int64_t)J * Np + (int64_t)I * B;
+  for (int c = threadIdx.x; c < B; c += 256) __builtin_nontemporal_store(rows[c], Prow + c);
+  if (!DIAG) {
     double *Pcol = P + (int64_t)I * Np + (int64_t)J * B;
-    const double *csd = sh + B;
     for (int c = threadIdx.x; c < B; c += 256)
-      Pcol[c] = (csd[c] + csd[B + c]) + (csd[2 * B + c] + csd[3 * B + c]);
+      __builtin_nontemporal_store((cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]), Pcol + c);
   }
 }
 
@@ -135,7 +121,7 @@ __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ t
                                                     double *__restrict__ P, int64_t Np,
                                                     const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sh[5 * B];
+  __shared__ double sh[6 * B + 4 * kRB * 64];
   const int2 t = list[blockIdx.x];
   const double *A = tiles + (int64_t)blockIdx.x * B * B;
   if (t.x == t.y)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -140,10 +141,11 @@ template <int RB, int NW, bool PF>
 __global__ __launch_bounds__(NW * 64) void k_symv(const double *__restrict__ tiles,
                                                   const int2 *__restrict__ list,
                                                   const double *__restrict__ v,
-                                                  double *__restrict__ P, long Np) {
+                                                  double *__restrict__ P, long Np,
+                                                  long pitch = (long)B * B) {
   __shared__ double sh[(NW + 1) * B];
   const int2 t = list[blockIdx.x];
-  const double *A = tiles + (long)blockIdx.x * B * B;
+  const double *A = tiles + (long)blockIdx.x * pitch;
   if (t.x == t.y)
     body<RB, NW, PF, true>(A, t.x, t.y, v, P, Np, sh);
   else
@@ -379,6 +381,155 @@ void k_symv4(const double *__restrict__ tiles, const int2 *__restrict__ list,
     body4<RB, false>(A, t.x, t.y, v, P, Np, sh);
 }
 
+// variant 6: row sums reduced through a wave-private LDS transpose instead of the
+// select-heavy butterfly (8 ds_write_b64 + 4 ds_read_b128 + 7 adds + 3 xor-shuffles
+// per 8 rows); rows interleaved across waves, row sums staged for one coalesced write.
+template <bool DIAG, bool NOWRITE, bool NOCOL, bool NTST = false>
+__device__ __forceinline__ void body6(const double *__restrict__ A, int I, int J,
+                                      const double *__restrict__ v, double *__restrict__ P,
+                                      long Np, double *sh) {
+  constexpr int NW = 4, RB = 8;
+  constexpr int RPW = B / NW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const d2 *v2 = reinterpret_cast<const d2 *>(v + (long)J * B);
+  d2 pc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+  double *vrow = sh;                  // B
+  double *rows = sh + B;              // B
+  double *cs = sh + 2 * B;            // 4 x B
+  double *red = sh + 6 * B + w * RB * 64;  // wave-private 8 x 64
+  if (!DIAG)
+    for (int i = threadIdx.x; i < B; i += 256) vrow[i] = v[(long)I * B + i];
+  __syncthreads();
+  d2 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
+#pragma unroll 1
+  for (int g = 0; g < RPW / RB; ++g) {
+    const int rbase = (g * NW + w) * RB;
+    const d2 *rowp = reinterpret_cast<const d2 *>(A + (long)rbase * B) + lane;
+    d2 a[RB][4];
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+#pragma unroll
+    for (int rr = 0; rr < RB; ++rr) {
+      double s0 = a[rr][0].x * pc[0].x;
+      double s1 = a[rr][0].y * pc[0].y;
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        s0 = fma(a[rr][q].x, pc[q].x, s0);
+        s1 = fma(a[rr][q].y, pc[q].y, s1);
+      }
+      red[rr * 64 + lane] = s0 + s1;
+      if (!DIAG && !NOCOL) {
+        const double pr = vrow[rbase + rr];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q].x = fma(a[rr][q].x, pr, acc[q].x);
+          acc[q].y = fma(a[rr][q].y, pr, acc[q].y);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane = 8 * row + c: sums red[row][8c .. 8c + 8)
+    const d2 *rp = reinterpret_cast<const d2 *>(red + (lane >> 3) * 64 + (lane & 7) * 8);
+    const d2 t0 = rp[0], t1 = rp[1], t2 = rp[2], t3 = rp[3];
+    double t = ((t0.x + t0.y) + (t1.x + t1.y)) + ((t2.x + t2.y) + (t3.x + t3.y));
+    t += __shfl_xor(t, 1, 64);
+    t += __shfl_xor(t, 2, 64);
+    t += __shfl_xor(t, 4, 64);
+    if ((lane & 7) == 0) rows[rbase + (lane >> 3)] = t;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (!DIAG) {
+    d2 *cs2 = reinterpret_cast<d2 *>(cs);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs2[w * (B / 2) + lane + 64 * q] = acc[q];
+  }
+  __syncthreads();
+  double *Prow = P + (long)J * Np + (long)I * B;
+  if (NOWRITE) {
+    double t = 0.0;
+    for (int c = threadIdx.x; c < B; c += 256) t += rows[c] + cs[c];
+    if (t == 1234.5678) Prow[0] = t;
+    return;
+  }
+  if (NTST) {
+    for (int c = threadIdx.x; c < B; c += 256) __builtin_nontemporal_store(rows[c], Prow + c);
+    if (!DIAG) {
+      double *Pcol = P + (long)I * Np + (long)J * B;
+      for (int c = threadIdx.x; c < B; c += 256)
+        __builtin_nontemporal_store((cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]), Pcol + c);
+    }
+    return;
+  }
+  for (int c = threadIdx.x; c < B; c += 256) Prow[c] = rows[c];
+  if (!DIAG) {
+    double *Pcol = P + (long)I * Np + (long)J * B;
+    for (int c = threadIdx.x; c < B; c += 256)
+      Pcol[c] = (cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_symv6nt(const double *__restrict__ tiles,
+                                                 const int2 *__restrict__ list,
+                                                 const double *__restrict__ v,
+                                                 double *__restrict__ P, long Np) {
+  __shared__ double sh[6 * B + 4 * 8 * 64];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body6<true, false, false, true>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body6<false, false, false, true>(A, t.x, t.y, v, P, Np, sh);
+}
+
+// writes only (same P pattern, no tile reads): what do the slot writes cost alone?
+__global__ __launch_bounds__(256) void k_pwrite(const int2 *__restrict__ list, double *__restrict__ P,
+                                                long Np) {
+  const int2 t = list[blockIdx.x];
+  double *Prow = P + (long)t.y * Np + (long)t.x * B;
+  for (int c = threadIdx.x; c < B; c += 256) Prow[c] = 1.0;
+  if (t.x != t.y) {
+    double *Pcol = P + (long)t.x * Np + (long)t.y * B;
+    for (int c = threadIdx.x; c < B; c += 256) Pcol[c] = 2.0;
+  }
+}
+
+template <bool NOWRITE, bool NOCOL>
+__global__ __launch_bounds__(256) void k_symv6x(const double *__restrict__ tiles,
+                                                const int2 *__restrict__ list,
+                                                const double *__restrict__ v,
+                                                double *__restrict__ P, long Np) {
+  __shared__ double sh[6 * B + 4 * 8 * 64];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body6<true, NOWRITE, NOCOL>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body6<false, NOWRITE, NOCOL>(A, t.x, t.y, v, P, Np, sh);
+}
+
+__global__ __launch_bounds__(256) void k_symv6(const double *__restrict__ tiles,
+                                               const int2 *__restrict__ list,
+                                               const double *__restrict__ v,
+                                               double *__restrict__ P, long Np) {
+  __shared__ double sh[6 * B + 4 * 8 * 64];
+  const int2 t = list[blockIdx.x];
+  const double *A = tiles + (long)blockIdx.x * B * B;
+  if (t.x == t.y)
+    body6<true, false, false>(A, t.x, t.y, v, P, Np, sh);
+  else
+    body6<false, false, false>(A, t.x, t.y, v, P, Np, sh);
+}
+
 __global__ void k_reduce(const double *__restrict__ P, long Np, int nb, long n,
                          double *__restrict__ y) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -538,6 +689,51 @@ int main(int argc, char **argv) {
   RUN4(12, 2)
   RUN4(6, 3)
   RUN4(4, 4)
+  ms = time_it([&] {
+    hipLaunchKernelGGL(k_symv6, dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+  }, reps);
+  printf("symv6 (LDS transpose rows)  %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  ms = time_it([&] {
+    hipLaunchKernelGGL(k_symv6nt, dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+  }, reps);
+  printf("symv6 nontemporal P stores %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  ms = time_it([&] {
+    hipLaunchKernelGGL(k_pwrite, dim3((unsigned)nt), dim3(256), 0, 0, dl, P, Np);
+  }, reps);
+  printf("P writes alone (67 MB)      %.3f ms\n", ms);
+  ms = time_it([&] {
+    hipLaunchKernelGGL((k_symv6x<true, false>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+  }, reps);
+  printf("symv6 no P writes           %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  ms = time_it([&] {
+    hipLaunchKernelGGL((k_symv6x<false, true>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+  }, reps);
+  printf("symv6 no column FMAs        %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  ms = time_it([&] {
+    hipLaunchKernelGGL((k_symv6x<true, true>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+  }, reps);
+  printf("symv6 no writes, no col     %.3f ms  %.0f GB/s\n", ms, bytes / ms / 1e6);
+  {  // correctness of symv6 vs symv (row + column partials)
+    std::vector<double> h1((size_t)nb * Np), h2((size_t)nb * Np);
+    CK(hipMemset(P, 0, sizeof(double) * nb * Np));
+    hipLaunchKernelGGL((k_symv<8, 4, true>), dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np, (long)B * B);
+    CK(hipMemcpy(h1.data(), P, sizeof(double) * nb * Np, hipMemcpyDeviceToHost));
+    CK(hipMemset(P, 0, sizeof(double) * nb * Np));
+    hipLaunchKernelGGL(k_symv6, dim3((unsigned)nt), dim3(256), 0, 0, tiles, dl, v, P, Np);
+    CK(hipMemcpy(h2.data(), P, sizeof(double) * nb * Np, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < h1.size(); ++i) { md = fmax(md, fabs(h1[i] - h2[i])); mx = fmax(mx, fabs(h1[i])); }
+    printf("symv6 vs symv max|diff| %.3e (max %.3e)\n", md, mx);
+  }
+  // tile pitch experiment: pad each tile by `pad` doubles (alignment phase of the WGs)
+  for (long pad : {64L, 512L, 4096L + 64L}) {
+    const long pitch = (long)B * B + pad;
+    const long nt3 = nt * (long)B * B / pitch;  // same buffer, slightly fewer tiles
+    ms = time_it([&] {
+      hipLaunchKernelGGL((k_symv<8, 4, true>), dim3((unsigned)nt3), dim3(256), 0, 0, tiles, dl, v, P, Np, pitch);
+    }, reps);
+    printf("symv 8,4,PF pitch+%ld (%ld tiles) %.3f ms  %.0f GB/s\n", pad, nt3, ms, 8.0 * nt3 * B * B / ms / 1e6);
+  }
   // tail test: the first multiple of 512 tiles only
   {
     const long nt2 = nt / 512 * 512;
