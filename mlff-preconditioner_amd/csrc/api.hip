@@ -223,14 +223,19 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
     (void)hipFree(ctx->T);
     ctx->T = nullptr;
   }
-  if (ctx->tpart != nullptr) {
-    (void)hipFree(ctx->tpart);
+  if (ctx->tpart_base != nullptr) {
+    (void)hipFree(ctx->tpart_base);
+    ctx->tpart_base = nullptr;
     ctx->tpart = nullptr;
   }
+  ctx->spec_t = false;
   MLFF_HIP(ctx, hipMalloc(&ctx->T, sizeof(double) * round_up(k, 8) * ctx->blk));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * ctx->blk, ctx->stream));
   ctx->tsplit = choose_tsplit(k, ctx->blk);
-  MLFF_HIP(ctx, hipMalloc(&ctx->tpart, sizeof(double) * k * ctx->tsplit));
+  // [rr partials (kVecGrid) | tpart (k x tsplit)]: on several ranks the end-of-iteration
+  // ||r||^2 reduction and the next iteration's T r reduction share one all-reduce
+  MLFF_HIP(ctx, hipMalloc(&ctx->tpart_base, sizeof(double) * (kVecGrid + k * ctx->tsplit)));
+  ctx->tpart = ctx->tpart_base + kVecGrid;
   if (ctx->zpart != nullptr) {
     (void)hipFree(ctx->zpart);
     ctx->zpart = nullptr;
@@ -512,10 +517,17 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) 
   hipStream_t s = ctx->stream;
   const int *status = &ctx->st->status;
   double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
+  const bool lowrank = ctx->precon_kind != MLFF_PRECON_NONE;
+  // several ranks + low-rank preconditioner: T r of the next iteration is computed
+  // right after r is updated and reduced together with ||r||^2 (one collective
+  // fewer per iteration; same values, the stop test still gates everything after)
+  const bool merge = lowrank && ctx->world > 1;
   const double *zsrc;
-  if (ctx->precon_kind != MLFF_PRECON_NONE) {
-    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
-    MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
+  if (lowrank) {
+    if (!(merge && ctx->spec_t)) {
+      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+      MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
+    }
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
                     ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
     zsrc = ctx->z;
@@ -541,10 +553,16 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) 
   }
   launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
   MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
-  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
-                   status, s);
-  MLFF_TRY(allreduce(ctx, rr_part(ctx), kVecGrid));
-  launch_stoptest(rr_part(ctx), ctx->st, ctx->trace, it, s);
+  double *rrp = merge ? ctx->tpart_base : rr_part(ctx);
+  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rrp, ctx->st, status, s);
+  if (merge) {
+    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
+    ctx->spec_t = true;
+  } else {
+    MLFF_TRY(allreduce(ctx, rrp, kVecGrid));
+  }
+  launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
   return MLFF_OK;
 }
 
@@ -675,7 +693,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
                   (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
-                  (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart,
+                  (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart_base,
                   (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart})
     dev_free(p);
   sym_free(ctx->sym);
@@ -983,6 +1001,7 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
   if (ctx->precon_kind == MLFF_PRECON_NONE) {
     MLFF_HIP(ctx, hipMemcpyAsync(zd, rd, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
   } else {
+    ctx->spec_t = false;  // tpart is reused below
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, rd, ctx->tpart, nullptr, s);
     MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, rd, zd, ctx->nrows,
@@ -1096,6 +1115,7 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->trace, &r0, sizeof(double), hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   *ctx->h_st = h;
+  ctx->spec_t = false;
   ctx->tol = tol;
   ctx->bnorm = bnorm;
   ctx->pcg_done = 0;
@@ -1149,6 +1169,7 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
     while (ctx->h_st->status == ST_RECHECK) {
       MLFF_TRY(do_recheck(ctx));
       MLFF_TRY(poll_state(ctx));
+      ctx->spec_t = false;  // r was recomputed: the speculative T r is stale
     }
     ctx->pcg_done = ctx->h_st->iters;
   }

@@ -135,7 +135,9 @@ struct mlff_ctx {
   int tsplit = 1;         // column splits of the T GEMV
   int zsplit = 1;         // row splits of the T^T t GEMV
   double *zpart = nullptr;  // zsplit x blk partials
-  double *tpart = nullptr;
+  double *tpart = nullptr;       // = tpart_base + kVecGrid
+  double *tpart_base = nullptr;
+  bool spec_t = false;           // tpart already holds T r of the current r (merged collective)
 
   // pivoted Cholesky scratch
   int64_t *perm = nullptr;   // global permutation (replicated)

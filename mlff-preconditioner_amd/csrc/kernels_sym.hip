@@ -150,12 +150,23 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
   if (i >= n_out) return;
   const int bi = (int)(i / B);
   double s = 0.0;
-  for (int t = 0; t < nb; ++t) {
-    if (!ALL) {
+  if (ALL) {
+    // 8 slot loads in flight per thread; the additions stay in slot order
+    int t = 0;
+    for (; t + 7 < nb; t += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; t < nb; ++t) s += P[(int64_t)t * Np + i];
+  } else {
+    for (int t = 0; t < nb; ++t) {
       const int I = bi > t ? bi : t, J = bi > t ? t : bi;
       if (owner_of(I, J, tiles_per_rank) != rank) continue;
+      s += P[(int64_t)t * Np + i];
     }
-    s += P[(int64_t)t * Np + i];
   }
   if (EPI) {
     double yv = sigma * s;

@@ -177,17 +177,18 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
   const int64_t ld2 = ldw / 2;
   d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
   int64_t j = j0;
-  for (; j + 3 < j1; j += 4) {
-    const d2 a0 = w2[j * ld2], a1 = w2[(j + 1) * ld2], a2 = w2[(j + 2) * ld2], a3 = w2[(j + 3) * ld2];
-    const double t0 = t_sh[j - j0], t1 = t_sh[j + 1 - j0], t2 = t_sh[j + 2 - j0], t3 = t_sh[j + 3 - j0];
-    acc0.x = fma(a0.x, t0, acc0.x);
-    acc0.y = fma(a0.y, t0, acc0.y);
-    acc1.x = fma(a1.x, t1, acc1.x);
-    acc1.y = fma(a1.y, t1, acc1.y);
-    acc0.x = fma(a2.x, t2, acc0.x);
-    acc0.y = fma(a2.y, t2, acc0.y);
-    acc1.x = fma(a3.x, t3, acc1.x);
-    acc1.y = fma(a3.y, t3, acc1.y);
+  for (; j + 7 < j1; j += 8) {  // 8 rows (128 B per lane) in flight
+    d2 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = w2[(j + u) * ld2];
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      const double t0 = t_sh[j + u - j0], t1 = t_sh[j + u + 1 - j0];
+      acc0.x = fma(a[u].x, t0, acc0.x);
+      acc0.y = fma(a[u].y, t0, acc0.y);
+      acc1.x = fma(a[u + 1].x, t1, acc1.x);
+      acc1.y = fma(a[u + 1].y, t1, acc1.y);
+    }
   }
   for (; j < j1; ++j) {
     const d2 a0 = w2[j * ld2];
