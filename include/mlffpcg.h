@@ -167,7 +167,9 @@ int mlff_precon_none(mlff_ctx *ctx);
  * current permuted order, incomplete_cholesky.py:53) then Woodbury with lam:
  * T = chol(lam I + L^T L)^-1 L^T, apply z = (r - T^T T r) / lam.
  * index_columns_out (N, int64, optional): the permutation (first k = pivots).
- * build_woodbury = 0 only computes the pivots (truncated_cholesky selector). */
+ * build_woodbury = 0 only computes the pivots (truncated_cholesky selector); the
+ * panel then holds L^T (k x N, rows in the original index order, as the
+ * reference's L), readable with mlff_precon_get_panel, and PCG runs unpreconditioned. */
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out);
 /* Nystrom from sorted column indices idx (k).  variant 0 = _init_precon_operator

@@ -913,10 +913,10 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
   ctx->prow = nullptr;
   MLFF_HIP(ctx, hipMalloc(&ctx->prow, sizeof(double) * (k + 1)));
   MLFF_TRY(pivoted_cholesky(ctx, k, index_columns_out));
+  ctx->k = k;  // without Woodbury the panel holds L^T (mlff_precon_get_panel), unused by PCG
   if (build_woodbury) {
     MLFF_TRY(woodbury_inplace(ctx, ctx->T, k));
     ctx->precon_kind = MLFF_PRECON_PIVCHOL;
-    ctx->k = k;
     ctx->sigma_p = 1.0;
   }
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));

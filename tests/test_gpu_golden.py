@@ -182,3 +182,31 @@ def test_dropin_unknown_preconditioner(sg, golden_dir):
     f = load(golden_dir, "sgdml_ethanol_n270")
     with pytest.raises(NotImplementedError):
         run_dropin(f, "sgdml_ethanol_n270", "does_not_exist")
+
+
+def test_rbf_reference_generator_and_preconditioner(sg, golden_dir):
+    """tools/utils.create_kernel_mat (sklearn RBF, l = 1, d = 2, + 1e-10 I; utils.py:173-187)
+    generated on the device, the reference's pivoted Cholesky on it (incomplete_cholesky.py
+    :24-93, index order and L), and IterativeCholesky._init_precon_operator's Woodbury
+    apply (iterative_cholesky.py:115-150) on the l = 0.2 kernel."""
+    f = load(golden_dir, "rbf_reference")
+    n = f["X"].shape[0]
+    k = int(f["k"])
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(f["X"], length_scale=1.0, jitter=1e-10)
+        K = s.get_matrix_rows()
+        np.testing.assert_allclose(K, f["K"], rtol=0, atol=2e-15)
+        s.set_operator(1.0, 1e-10)
+        piv, _ = s.precon_pivchol(k, build_woodbury=False)
+        np.testing.assert_array_equal(piv[:k], f["index_columns"][:k])
+        Lt = s.precon_panel()
+    np.testing.assert_allclose(Lt.T, f["L"], rtol=0, atol=1e-12 * np.abs(f["L"]).max())
+    lam, k3 = float(f["lam"]), int(f["k3"])
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(f["X3"], length_scale=0.2, jitter=0.0)
+        np.testing.assert_allclose(s.get_matrix_rows(), f["K3"], rtol=0, atol=2e-15)
+        s.set_operator(1.0, lam)
+        piv3, _ = s.precon_pivchol(k3)
+        np.testing.assert_array_equal(piv3[:k3], f["index_columns3"][:k3])
+        z = s.precon_apply(f["r"])
+    np.testing.assert_allclose(z, f["z"], rtol=1e-9, atol=1e-9 * np.abs(f["z"]).max())
