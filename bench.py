@@ -321,8 +321,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc_traffic(workload, storage, world),
-                         "kernel": "k_symv_tiles + k_sym_reduce (K mat-vec, lower-triangle tiles)"
-                         if storage == "sym" else "k_gemv<4,4,1> (K mat-vec)",
+                         "kernel": {"sym": "k_symv_tiles + k_sym_reduce (K mat-vec, lower-triangle tiles)",
+                                    "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
+                                    "matfree": "k_mf_z + k_mf_pair + k_mf_pair_fin + k_mf_h + k_mf_jt "
+                                               "(matrix-free sGDML operator)"}.get(storage, storage),
                          "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms},
             "matvec_gbs": achieved,
             # with half storage also report against the dense 8 N^2 bytes
