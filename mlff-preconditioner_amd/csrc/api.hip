@@ -466,12 +466,13 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
   SymPack &sp = ctx->sym;
   launch_symv(sp, v_full, sp.P, status, s);
   if (ctx->world == 1) {
-    launch_sym_reduce(sp, 0, 1, ctx->nrows, y_loc, true, ctx->sigma_K, ctx->lam, v_loc, status, s);
+    launch_sym_reduce(sp, ctx->nrows, y_loc, true, ctx->sigma_K, ctx->lam, v_loc, status, s);
     return MLFF_OK;
   }
-  launch_sym_reduce(sp, ctx->rank, ctx->world, ctx->ld, sp.yg, false, 0.0, 0.0, nullptr, status, s);
-  MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, y_loc, (size_t)ctx->blk));
-  launch_axpby_loc(y_loc, ctx->nrows, ctx->sigma_K, ctx->lam, v_loc, status, s);
+  launch_sym_reduce_ranks(sp, ctx->rank, ctx->world, ctx->blk, nullptr, nullptr, nullptr, 0.0, 0.0,
+                          status, s);
+  MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
+  launch_axpby_loc(sp.yr, y_loc, ctx->nrows, ctx->sigma_K, ctx->lam, v_loc, status, s);
   return MLFF_OK;
 }
 
@@ -512,8 +513,85 @@ struct GemvMark {
   long long it;
 };
 
+void mark_begin(mlff_ctx *ctx, std::vector<GemvMark> *marks, hipEvent_t *e0) {
+  *e0 = nullptr;
+  if (ctx->timing.on && marks != nullptr) {
+    *e0 = timing_event(ctx);
+    if (*e0) hipEventRecord(*e0, ctx->stream);
+  }
+}
+
+void mark_end(mlff_ctx *ctx, std::vector<GemvMark> *marks, hipEvent_t e0, long long it) {
+  if (e0 == nullptr) return;
+  hipEvent_t e1 = timing_event(ctx);
+  if (e1) {
+    hipEventRecord(e1, ctx->stream);
+    marks->push_back({ctx->timing.used - 2, it});
+  }
+}
+
+// One PCG iteration on several ranks: three collectives (two for the dense / matrix-free
+// operators without a preconditioner, ... ) instead of five:
+//   allgather(z_g | rho partials)  -> rho and the whole p on every rank
+//   [symmetric tiles] reduce-scatter(K p partial rows | p.q shares) -> q rows and p.q
+//   [other storages]  allreduce(p.q partials)
+//   allreduce(rr partials | T r partials of the next iteration)   (low-rank precon)
+// Same recurrence as launch_iteration; the sums are over the same terms in another
+// (fixed) order, bitwise identical on all ranks.
+int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) {
+  hipStream_t s = ctx->stream;
+  const int *status = &ctx->st->status;
+  double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
+  double *zg = ctx->gb + (int64_t)ctx->rank * ctx->gstride;  // this rank's gather block
+  const bool lowrank = ctx->precon_kind != MLFF_PRECON_NONE;
+  if (lowrank) {
+    if (!ctx->spec_t) {
+      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+      MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
+    }
+    launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, zg, ctx->nrows,
+                    ctx->sigma_p, 1.0 / ctx->lam, zg + ctx->blk, status, s, ctx->zpart, ctx->zsplit);
+  } else {
+    launch_copy_dot(ctx->r, ctx->nrows, zg, zg + ctx->blk, status, s);
+  }
+  MLFF_TRY(comm_allgather(ctx, zg, ctx->gb, (size_t)ctx->gstride));
+  launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
+                           status, s);
+  hipEvent_t e0;
+  mark_begin(ctx, marks, &e0);
+  if (ctx->use_sym) {
+    SymPack &sp = ctx->sym;
+    launch_symv(sp, ctx->p_full, sp.P, status, s);
+    launch_sym_reduce_ranks(sp, ctx->rank, ctx->world, ctx->blk, ctx->p_full, pq_part(ctx),
+                            pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s);
+    MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
+    mark_end(ctx, marks, e0, it);
+    launch_update_xr_shares(ctx->x, ctx->r, p_loc, sp.yr, sp.yr + ctx->blk, ctx->world, ctx->nrows,
+                            ctx->sigma_K, ctx->lam, lowrank ? ctx->tpart_base : rr_part(ctx),
+                            ctx->st, status, s);
+  } else {
+    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
+    mark_end(ctx, marks, e0, it);
+    launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
+    MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
+    launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx),
+                     lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
+  }
+  double *rrp = lowrank ? ctx->tpart_base : rr_part(ctx);
+  if (lowrank) {
+    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
+    ctx->spec_t = true;
+  } else {
+    MLFF_TRY(allreduce(ctx, rrp, kVecGrid));
+  }
+  launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
+  return MLFF_OK;
+}
+
 // one PCG iteration (ITER = it), all launches status gated
 int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) {
+  if (ctx->world > 1) return launch_iteration_ranks(ctx, it, marks);
   hipStream_t s = ctx->stream;
   const int *status = &ctx->st->status;
   double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
@@ -677,6 +755,12 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
       hipMalloc(&ctx->pivflag, sizeof(int) * ctx->blk) != hipSuccess ||
       hipMalloc(&ctx->perm, sizeof(int64_t) * n_global) != hipSuccess)
     return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
+  if (world > 1) {
+    ctx->gstride = ctx->blk + kVecGrid;
+    if (hipMalloc(&ctx->gb, sizeof(double) * world * ctx->gstride) != hipSuccess)
+      return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
+    hipMemset(ctx->gb, 0, sizeof(double) * world * ctx->gstride);
+  }
   hipMemset(ctx->p_full, 0, sizeof(double) * ldp);
   hipMemset(ctx->xg, 0, sizeof(double) * ldp);
   hipMemset(ctx->part, 0, sizeof(double) * 4 * kMaxPart);
@@ -694,7 +778,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
                   (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart_base,
-                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart})
+                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->gb})
     dev_free(p);
   sym_free(ctx->sym);
   mf_free(ctx->mf);
@@ -1073,6 +1157,8 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
   for (double *v : {ctx->b, ctx->x, ctx->r, ctx->z, ctx->q})
     MLFF_HIP(ctx, hipMemsetAsync(v, 0, sizeof(double) * ctx->blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->p_full, 0, sizeof(double) * ctx->ld, s));
+  if (ctx->gb != nullptr)
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->gb, 0, sizeof(double) * ctx->world * ctx->gstride, s));
   if (ctx->nrows > 0) {
     MLFF_HIP(ctx, hipMemcpyAsync(ctx->b, b_local, sizeof(double) * ctx->nrows, hipMemcpyHostToDevice, s));
     if (x0_local)

@@ -53,7 +53,15 @@ struct SymPack {
   int64_t nb = 0;            // Np / B
   int64_t tiles_per_rank = 0;
   double *P = nullptr;       // slot buffer nb x Np
-  double *yg = nullptr;      // this rank's partial y over [0, Np) (world > 1)
+  // the last (ntiles - nwhole) tiles of `list` run as 4 quarter-tile workgroups each;
+  // their column partials of quarters 1..3 go to Pq (3 planes of nb x Np)
+  int64_t nwhole = 0;
+  double *Pq = nullptr;
+  unsigned char *split = nullptr;  // nb x nb: tile (I, J) is split
+  int64_t t_split = 0;             // smallest I of a split tile (nb if none)
+  double *yg = nullptr;      // world > 1: this rank's partial y, rank blocks of ystride
+  double *yr = nullptr;      // world > 1: reduce-scatter result (ystride)
+  int64_t ystride = 0;       // blk + tail (p.q shares of every rank)
 };
 
 // Matrix-free sGDML operator data (kernels_mf.hip).
@@ -118,6 +126,8 @@ struct mlff_ctx {
   // CG vectors.  local: blk entries; p_full / xg: ld entries (rank blocks)
   double *x = nullptr, *r = nullptr, *z = nullptr, *q = nullptr, *b = nullptr;
   double *p_full = nullptr, *xg = nullptr;
+  double *gb = nullptr;    // world > 1: allgather buffer, world blocks of gstride
+  int64_t gstride = 0;     // blk + kVecGrid (z block + its rho partials)
   double *part = nullptr;  // partial sums: 3 * kMaxPart + tpart (k * S)
   mlff::DevState *st = nullptr;
   mlff::DevState *h_st = nullptr;  // pinned mirror
@@ -204,6 +214,19 @@ void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
 // p = z + (rho/rho1) p   (p = z at iteration 1); rho = sum(rho_part)
 void launch_update_p(const double *z, double *p, int64_t n, const double *rho_part,
                      DevState *st, long long it, const int *status, hipStream_t s);
+// several ranks (gather buffer gb: rank blocks of gstride = blk + kVecGrid holding z_g
+// and its rho partials): dst = r with r.r partials (no preconditioner);
+// p_full = z_full + (rho/rho1) p_full with rho summed from all ranks' partials
+void launch_copy_dot(const double *r, int64_t n, double *dst, double *part, const int *status,
+                     hipStream_t s);
+void launch_update_p_gathered(const double *gb, int64_t gstride, int64_t blk, int world,
+                              double *p_full, DevState *st, long long it, const int *status,
+                              hipStream_t s);
+// several ranks, symmetric tiles: pq = sum of the world shares; q = sigma y + lam p;
+// alpha = rho/pq; x += alpha p; r -= alpha q; rr partials
+void launch_update_xr_shares(double *x, double *r, const double *p, const double *y,
+                             const double *shares, int world, int64_t n, double sigma, double lam,
+                             double *rr_part, DevState *st, const int *status, hipStream_t s);
 // pq = sum(pq_part); alpha = rho/pq; x += alpha p; r -= alpha q; rr partials
 void launch_update_xr(double *x, double *r, const double *p, const double *q, int64_t n,
                       const double *pq_part, double *rr_part, DevState *st, const int *status,
@@ -264,13 +287,18 @@ void sym_free(SymPack &sp);
 // P <- slot partials of K v_full over the stored tiles
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
                  hipStream_t s);
-// y[i] = sum of this rank's slots of row i (i < n_out); epilogue (world 1 only):
-// y = sigma * y + lam * vloc
-void launch_sym_reduce(const SymPack &sp, int rank, int world, int64_t n_out, double *y,
-                       bool epilogue, double sigma, double lam, const double *vloc,
-                       const int *status, hipStream_t s);
-void launch_axpby_loc(double *y, int64_t n, double sigma, double lam, const double *vloc,
-                      const int *status, hipStream_t s);
+// one rank: y[i] = sum of the slots of row i (i < n_out); epilogue y = sigma y + lam vloc
+void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogue, double sigma,
+                       double lam, const double *vloc, const int *status, hipStream_t s);
+// several ranks: sp.yg = this rank's slot sums of every row (rank blocks of sp.ystride);
+// with p_full: also this rank's share sigma p.y_g + lam ||p_loc||^2 published into the
+// tail slot `rank` of every block (pq_part / pp_part: kVecGrid scratch each)
+void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
+                             const double *p_full, double *pq_part, double *pp_part,
+                             double sigma, double lam, const int *status, hipStream_t s);
+// y = sigma * src + lam * vloc over n entries (src may alias y)
+void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, double lam,
+                      const double *vloc, const int *status, hipStream_t s);
 // reduce-scatter (sum) of ld doubles into blk doubles per rank
 int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t count);
 

@@ -25,6 +25,8 @@
 // order -> the result is bitwise deterministic.
 #include "common.h"
 
+#include <algorithm>
+
 namespace mlff {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -35,10 +37,14 @@ constexpr int B = kSymTile;  // 512
 constexpr int kRowsPerWave = B / 4;
 constexpr int kRB = 8;  // rows per batch (loads in flight per wave: kRB x 4 KB)
 
+// rows [row0, row0 + 32 * ngroups) of tile (I, J): ngroups = 16 -> the whole tile,
+// 4 -> one quarter (the last tiles of a launch, see sym_build); column partials go
+// to plane Pc (P for a whole tile or quarter 0, Pq[h - 1] for quarter h)
 template <bool DIAG>
 __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, int J,
                                           const double *__restrict__ v,
-                                          double *__restrict__ P, int64_t Np,
+                                          double *__restrict__ P, double *__restrict__ Pc,
+                                          int64_t Np, int row0, int ngroups,
                                           double *__restrict__ sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)J * B);
@@ -49,15 +55,16 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
   double *rows = sh + B;                   // row partials of the tile
   double *cs = sh + 2 * B;                 // 4 x B column partials
   double *red = sh + 6 * B + w * kRB * 64; // wave-private kRB x 64 transpose buffer
+  const int nrows = 32 * ngroups;
   if (!DIAG)
-    for (int i = threadIdx.x; i < B; i += 256) vrow[i] = v[(int64_t)I * B + i];
+    for (int i = threadIdx.x; i < nrows; i += 256) vrow[row0 + i] = v[(int64_t)I * B + row0 + i];
   __syncthreads();
   d2 acc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
 #pragma unroll 1
-  for (int g = 0; g < kRowsPerWave / kRB; ++g) {
-    const int rbase = (g * 4 + w) * kRB;  // batches interleaved across the 4 waves
+  for (int g = 0; g < ngroups; ++g) {
+    const int rbase = row0 + (g * 4 + w) * kRB;  // batches interleaved across the 4 waves
     const d2 *rowp = reinterpret_cast<const d2 *>(A + (int64_t)rbase * B) + lane;
     d2 a[kRB][4];
 #pragma unroll
@@ -106,28 +113,58 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
   __syncthreads();
   // slot stores are non-temporal: interleaved with the tile stream they cost ~4 %
   // of the kernel as ordinary stores (scripts/probe_symv.hip)
-  double *Prow = P + (int64_t)J * Np + (int64_t)I * B;
-  for (int c = threadIdx.x; c < B; c += 256) __builtin_nontemporal_store(rows[c], Prow + c);
+  double *Prow = P + (int64_t)J * Np + (int64_t)I * B + row0;
+  for (int c = threadIdx.x; c < nrows; c += 256) __builtin_nontemporal_store(rows[row0 + c], Prow + c);
   if (!DIAG) {
-    double *Pcol = P + (int64_t)I * Np + (int64_t)J * B;
+    double *Pcol = Pc + (int64_t)I * Np + (int64_t)J * B;
     for (int c = threadIdx.x; c < B; c += 256)
       __builtin_nontemporal_store((cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]), Pcol + c);
   }
 }
 
+// workgroups [0, nwhole): one whole tile each; then 4 workgroups per remaining tile,
+// one quarter (128 rows) each, so the launch ends on quarter-tile units instead of a
+// partial round of whole tiles (a lone 2-MB tile streams at one CU's rate)
 __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ tiles,
                                                     const int2 *__restrict__ list,
                                                     const double *__restrict__ v,
-                                                    double *__restrict__ P, int64_t Np,
+                                                    double *__restrict__ P,
+                                                    double *__restrict__ Pq, int64_t Np,
+                                                    int nwhole, int nb,
                                                     const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[6 * B + 4 * kRB * 64];
-  const int2 t = list[blockIdx.x];
-  const double *A = tiles + (int64_t)blockIdx.x * B * B;
+  int tile = blockIdx.x, h = 0, ng = kRowsPerWave / kRB;
+  if (tile >= nwhole) {
+    const int u = tile - nwhole;
+    tile = nwhole + (u >> 2);
+    h = u & 3;
+    ng = kRowsPerWave / kRB / 4;
+  }
+  const int2 t = list[tile];
+  const double *A = tiles + (int64_t)tile * B * B;
+  double *Pc = h == 0 ? P : Pq + (int64_t)(h - 1) * nb * Np;
+  const int row0 = h * (B / 4);
   if (t.x == t.y)
-    tile_body<true>(A, t.x, t.y, v, P, Np, sh);
+    tile_body<true>(A, t.x, t.y, v, P, Pc, Np, row0, ng, sh);
   else
-    tile_body<false>(A, t.x, t.y, v, P, Np, sh);
+    tile_body<false>(A, t.x, t.y, v, P, Pc, Np, row0, ng, sh);
+}
+
+// column partials of slot t for rows of block bi: tile (t, bi), t > bi; a split tile
+// adds its quarters 1..3 (planes Pq) to quarter 0 (P) in quarter order
+__device__ __forceinline__ double slot_val(const double *__restrict__ P,
+                                           const double *__restrict__ Pq,
+                                           const unsigned char *__restrict__ split, int nb,
+                                           int64_t Np, int t, int bi, int64_t i) {
+  double v = P[(int64_t)t * Np + i];
+  if (t > bi && split[(int64_t)t * nb + bi]) {
+    const int64_t pl = (int64_t)nb * Np;
+    v += Pq[(int64_t)t * Np + i];
+    v += Pq[pl + (int64_t)t * Np + i];
+    v += Pq[2 * pl + (int64_t)t * Np + i];
+  }
+  return v;
 }
 
 __device__ __forceinline__ int owner_of(int I, int J, int tiles_per_rank) {
@@ -138,9 +175,11 @@ __device__ __forceinline__ int owner_of(int I, int J, int tiles_per_rank) {
 
 // y[i] = sum_{t=0}^{nb-1} P[t, i] over the slots whose tile this rank owns
 // (all slots on one rank); EPI: y = sigma * y + lam * vloc for rows < n_out
-template <bool ALL, bool EPI>
-__global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P, int64_t Np,
-                                                    int nb, int rank, int tiles_per_rank,
+template <bool EPI>
+__global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P,
+                                                    const double *__restrict__ Pq,
+                                                    const unsigned char *__restrict__ split,
+                                                    int t_split, int64_t Np, int nb,
                                                     int64_t n_out, double *__restrict__ y,
                                                     double sigma, double lam,
                                                     const double *__restrict__ vloc,
@@ -150,24 +189,20 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
   if (i >= n_out) return;
   const int bi = (int)(i / B);
   double s = 0.0;
-  if (ALL) {
-    // 8 slot loads in flight per thread; the additions stay in slot order
-    int t = 0;
-    for (; t + 7 < nb; t += 8) {
-      double v[8];
+  // slots below t_split hold no split tile for this row block (t_split: the first
+  // slot t > bi whose tile (t, bi) is split, nb if none).  8 slot loads in flight per
+  // thread; the additions stay in slot order
+  const int tend = t_split > bi ? t_split : bi + 1;
+  const int t8 = tend < nb ? tend : nb;
+  int t = 0;
+  for (; t + 7 < t8; t += 8) {
+    double v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; t < nb; ++t) s += P[(int64_t)t * Np + i];
-  } else {
-    for (int t = 0; t < nb; ++t) {
-      const int I = bi > t ? bi : t, J = bi > t ? t : bi;
-      if (owner_of(I, J, tiles_per_rank) != rank) continue;
-      s += P[(int64_t)t * Np + i];
-    }
+    for (int u = 0; u < 8; ++u) s += v[u];
   }
+  for (; t < nb; ++t) s += slot_val(P, Pq, split, nb, Np, t, bi, i);
   if (EPI) {
     double yv = sigma * s;
     if (vloc != nullptr) yv += lam * vloc[i];
@@ -177,13 +212,105 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
   }
 }
 
-__global__ __launch_bounds__(256) void k_axpby_loc(double *__restrict__ y, int64_t n, double sigma,
-                                                   double lam, const double *__restrict__ vloc,
+// several ranks: y_g = sum over this rank's slots for every row of [0, ld), written
+// into rank blocks of stride `bstride` (= blk + tail: the reduce-scatter operand).
+// PQ: also the partial p.y_g (all rows) + (lam/sigma-free) ||p_loc||^2 partials, one
+// pair per workgroup (fixed order), for k_pq_publish.
+template <bool PQ>
+__global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__ P,
+                                                      const double *__restrict__ Pq,
+                                                      const unsigned char *__restrict__ split,
+                                                      int64_t Np,
+                                                      int nb, int rank, int tiles_per_rank,
+                                                      int64_t ld, int64_t blk, int64_t bstride,
+                                                      double *__restrict__ yg,
+                                                      const double *__restrict__ p,
+                                                      double *__restrict__ pq_part,
+                                                      double *__restrict__ pp_part,
+                                                      const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  double apq = 0.0, app = 0.0;
+  const int64_t lo = (int64_t)rank * blk, hi = lo + blk;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
+       i += (int64_t)gridDim.x * 256) {
+    const int bi = (int)(i / B);
+    double s = 0.0;
+    for (int t = 0; t < nb; ++t) {
+      const int I = bi > t ? bi : t, J = bi > t ? t : bi;
+      if (owner_of(I, J, tiles_per_rank) != rank) continue;
+      s += slot_val(P, Pq, split, nb, Np, t, bi, i);
+    }
+    yg[(i / blk) * bstride + i % blk] = s;
+    if (PQ) {
+      const double pv = p[i];
+      apq = fma(pv, s, apq);
+      if (i >= lo && i < hi) app = fma(pv, pv, app);
+    }
+  }
+  if (PQ) {
+    double t = apq;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o, 64);
+    double u = app;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) u += __shfl_down(u, o, 64);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+      sh[w] = t;
+      sh[4 + w] = u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      pq_part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+      pp_part[blockIdx.x] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
+    }
+  }
+}
+
+// s_rank = sigma * sum(pq_part) + lam * sum(pp_part) (this rank's share of p.q), put
+// into tail slot `rank` of every rank block of the reduce-scatter operand; the other
+// tail slots stay zero, so the reduce-scatter hands every rank the exact vector of
+// shares (x + 0 is exact in any order) and each rank sums it in rank order: p.q is
+// bitwise identical on all ranks without a separate allreduce.
+__global__ __launch_bounds__(256) void k_pq_publish(const double *__restrict__ pq_part,
+                                                    const double *__restrict__ pp_part, int np,
+                                                    double sigma, double lam, int rank, int world,
+                                                    int64_t blk, int64_t bstride,
+                                                    double *__restrict__ yg,
+                                                    const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) {
+    a += pq_part[i];
+    b += pp_part[i];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64);
+    b += __shfl_down(b, o, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[w] = a;
+    sh[4 + w] = b;
+  }
+  __syncthreads();
+  const double share = sigma * ((sh[0] + sh[1]) + (sh[2] + sh[3])) +
+                       lam * ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+  for (int g = threadIdx.x; g < world; g += 256) yg[(int64_t)g * bstride + blk + rank] = share;
+}
+
+// y[i] = sigma * src[i] + lam * vloc[i]  (src may alias y)
+__global__ __launch_bounds__(256) void k_axpby_loc(const double *__restrict__ src, double *y,
+                                                   int64_t n, double sigma, double lam,
+                                                   const double *__restrict__ vloc,
                                                    const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  double yv = sigma * y[i];
+  double yv = sigma * src[i];
   if (vloc != nullptr) yv += lam * vloc[i];
   y[i] = yv;
 }
@@ -235,35 +362,48 @@ __global__ __launch_bounds__(256) void k_sym_pack(const double *__restrict__ K, 
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
                  hipStream_t s) {
   if (sp.ntiles == 0) return;
-  hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)sp.ntiles), dim3(256), 0, s, sp.tiles, sp.list,
-                     v_full, P, sp.Np, status);
+  const int64_t grid = sp.nwhole + 4 * (sp.ntiles - sp.nwhole);
+  hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)grid), dim3(256), 0, s, sp.tiles, sp.list, v_full,
+                     P, sp.Pq, sp.Np, (int)sp.nwhole, (int)sp.nb, status);
 }
 
-void launch_sym_reduce(const SymPack &sp, int rank, int world, int64_t n_out, double *y,
-                       bool epilogue, double sigma, double lam, const double *vloc,
-                       const int *status, hipStream_t s) {
+void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogue, double sigma,
+                       double lam, const double *vloc, const int *status, hipStream_t s) {
   if (n_out <= 0) return;
   const dim3 grid((unsigned)((n_out + 255) / 256));
-  if (world == 1) {
-    if (epilogue)
-      hipLaunchKernelGGL((k_sym_reduce<true, true>), grid, dim3(256), 0, s, sp.P, sp.Np, (int)sp.nb,
-                         rank, (int)sp.tiles_per_rank, n_out, y, sigma, lam, vloc, status);
-    else
-      hipLaunchKernelGGL((k_sym_reduce<true, false>), grid, dim3(256), 0, s, sp.P, sp.Np,
-                         (int)sp.nb, rank, (int)sp.tiles_per_rank, n_out, y, sigma, lam, vloc,
-                         status);
-  } else {
-    hipLaunchKernelGGL((k_sym_reduce<false, false>), grid, dim3(256), 0, s, sp.P, sp.Np,
-                       (int)sp.nb, rank, (int)sp.tiles_per_rank, n_out, y, sigma, lam, vloc,
-                       status);
-  }
+  if (epilogue)
+    hipLaunchKernelGGL((k_sym_reduce<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc, status);
+  else
+    hipLaunchKernelGGL((k_sym_reduce<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc, status);
 }
 
-void launch_axpby_loc(double *y, int64_t n, double sigma, double lam, const double *vloc,
-                      const int *status, hipStream_t s) {
+void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
+                             const double *p_full, double *pq_part, double *pp_part,
+                             double sigma, double lam, const int *status, hipStream_t s) {
+  const int64_t ld = (int64_t)world * blk;
+  const dim3 grid(kVecGrid);
+  if (p_full == nullptr) {
+    hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
+                       (int)sp.nb, rank,
+                       (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
+                       status);
+    return;
+  }
+  hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
+                     (int)sp.nb, rank,
+                     (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
+                     status);
+  hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
+                     rank, world, blk, sp.ystride, sp.yg, status);
+}
+
+void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, double lam,
+                      const double *vloc, const int *status, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_axpby_loc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, y, n, sigma,
-                     lam, vloc, status);
+  hipLaunchKernelGGL(k_axpby_loc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, y, n,
+                     sigma, lam, vloc, status);
 }
 
 // host-side tile assignment (same rule as owner_of)
@@ -289,6 +429,17 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
       trans.push_back(ctx->world > 1 && (I / tpr) != ctx->rank ? 1 : 0);
     }
   const int64_t nt = (int64_t)list.size();
+  // Tail split: with C workgroups resident at once (2 per CU: 208 VGPRs -> 2 waves per
+  // SIMD), whole tiles fill floor(nt / C) full rounds and the nt mod C remaining tiles
+  // run as quarters instead of a partial round of lone 2-MB tiles.  Measured (one
+  // MI355X, round 1): 1035 tiles 0.354 -> 0.338 ms, 528 tiles 0.198 -> 0.181 ms; more
+  // quarters cost more than they save (all tiles as quarters: 2.51 -> 2.67 ms at 8256).
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess ||
+      cus < 1)
+    cus = 256;
+  const int64_t C = 2 * (int64_t)cus;
+  const int64_t nwhole = (nt / C) * C;
   if (sp.tiles == nullptr || sp.ntiles != nt || sp.Np != Np) {
     sym_free(sp);
     if (nt > 0) {
@@ -296,14 +447,35 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
       MLFF_HIP(ctx, hipMalloc(&sp.list, sizeof(int2) * nt));
     }
     MLFF_HIP(ctx, hipMalloc(&sp.P, sizeof(double) * (int64_t)nb * Np));
-    MLFF_HIP(ctx, hipMalloc(&sp.yg, sizeof(double) * Np));
     MLFF_HIP(ctx, hipMemsetAsync(sp.P, 0, sizeof(double) * (int64_t)nb * Np, s));
-    MLFF_HIP(ctx, hipMemsetAsync(sp.yg, 0, sizeof(double) * Np, s));
+    MLFF_HIP(ctx, hipMalloc(&sp.Pq, sizeof(double) * 3 * (int64_t)nb * Np));
+    MLFF_HIP(ctx, hipMemsetAsync(sp.Pq, 0, sizeof(double) * 3 * (int64_t)nb * Np, s));
+    MLFF_HIP(ctx, hipMalloc(&sp.split, (size_t)nb * nb));
+    if (ctx->world > 1) {
+      // reduce-scatter operand: rank blocks of blk rows + a tail of p.q shares
+      sp.ystride = ctx->blk + round_up(ctx->world, kPad);
+      const int64_t ny = (int64_t)ctx->world * sp.ystride;
+      MLFF_HIP(ctx, hipMalloc(&sp.yg, sizeof(double) * ny));
+      MLFF_HIP(ctx, hipMalloc(&sp.yr, sizeof(double) * sp.ystride));
+      MLFF_HIP(ctx, hipMemsetAsync(sp.yg, 0, sizeof(double) * ny, s));
+      MLFF_HIP(ctx, hipMemsetAsync(sp.yr, 0, sizeof(double) * sp.ystride, s));
+    }
   }
   sp.ntiles = nt;
   sp.Np = Np;
   sp.nb = nb;
   sp.tiles_per_rank = tpr;
+  sp.nwhole = nwhole;
+  {
+    std::vector<unsigned char> split((size_t)nb * nb, 0);
+    sp.t_split = nb;
+    for (int64_t t = nwhole; t < nt; ++t) {
+      split[(size_t)list[t].x * nb + list[t].y] = 1;
+      sp.t_split = std::min<int64_t>(sp.t_split, list[t].x);
+    }
+    MLFF_HIP(ctx, hipMemcpyAsync(sp.split, split.data(), split.size(), hipMemcpyHostToDevice, s));
+    MLFF_HIP(ctx, hipStreamSynchronize(s));
+  }
   unsigned char *dtrans = nullptr;
   int *dflag = nullptr;
   if (nt > 0) {
@@ -338,12 +510,16 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
 }
 
 void sym_free(SymPack &sp) {
-  for (void *p : {(void *)sp.tiles, (void *)sp.list, (void *)sp.P, (void *)sp.yg})
+  for (void *p : {(void *)sp.tiles, (void *)sp.list, (void *)sp.P, (void *)sp.yg, (void *)sp.yr,
+                  (void *)sp.Pq, (void *)sp.split})
     if (p) (void)hipFree(p);
+  sp.Pq = nullptr;
+  sp.split = nullptr;
   sp.tiles = nullptr;
   sp.list = nullptr;
   sp.P = nullptr;
   sp.yg = nullptr;
+  sp.yr = nullptr;
   sp.ntiles = 0;
   sp.ready = false;
 }

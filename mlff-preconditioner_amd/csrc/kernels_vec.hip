@@ -298,6 +298,118 @@ void launch_update_p(const double *z, double *p, int64_t n, const double *rho_pa
                      status);
 }
 
+// ---------------------------------------------------------------------------
+// Several ranks: the search direction is formed from the all-gathered z instead of
+// all-gathering p.  Rank g's block of the gather buffer gb (stride gstride) holds
+// z_g (blk entries, zero padded) followed by its kVecGrid rho partials (r_g . z_g),
+// so one allgather replaces allreduce(rho) + allgather(p).  Every rank then sums the
+// world x kVecGrid rho partials in the same fixed order (bitwise identical rho on all
+// ranks) and updates the whole p_full = z_full + beta p_full, whose rank blocks are
+// exactly what the local update would produce.
+
+// no preconditioner: z = r, copied into the gather block with its rho partials
+__global__ __launch_bounds__(256) void k_copy_dot(const double *__restrict__ r, int64_t n,
+                                                  double *__restrict__ dst,
+                                                  double *__restrict__ part,
+                                                  const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const double v = r[i];
+    dst[i] = v;
+    acc = fma(v, v, acc);
+  }
+  const double t = block_sum256(acc, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+void launch_copy_dot(const double *r, int64_t n, double *dst, double *part, const int *status,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_copy_dot, dim3(kVecGrid), dim3(256), 0, s, r, n, dst, part, status);
+}
+
+__global__ __launch_bounds__(256) void k_update_p_gathered(const double *__restrict__ gb,
+                                                           int64_t gstride, int64_t blk,
+                                                           int world, double *__restrict__ p,
+                                                           DevState *st, long long it,
+                                                           const int *__restrict__ status) {
+  if (*status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  double v = 0.0;
+  const int np = world * kVecGrid;
+  for (int f = threadIdx.x; f < np; f += 256)
+    v += gb[(int64_t)(f / kVecGrid) * gstride + blk + (f % kVecGrid)];
+  v = block_sum256(v, sh);
+  __syncthreads();
+  if (threadIdx.x == 0) sh[4] = v;
+  __syncthreads();
+  const double rho = sh[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->rho = rho;
+  const int64_t ld = (int64_t)world * blk;
+  if (it > 1) {
+    const double beta = rho / st->rho1;
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ld;
+         j += (int64_t)gridDim.x * 256)
+      p[j] = fma(beta, p[j], gb[(j / blk) * gstride + j % blk]);
+  } else {
+    for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < ld;
+         j += (int64_t)gridDim.x * 256)
+      p[j] = gb[(j / blk) * gstride + j % blk];
+  }
+}
+
+void launch_update_p_gathered(const double *gb, int64_t gstride, int64_t blk, int world,
+                              double *p_full, DevState *st, long long it, const int *status,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_update_p_gathered, dim3(256), dim3(256), 0, s, gb, gstride, blk, world,
+                     p_full, st, it, status);
+}
+
+// Several ranks, symmetric tiles: y = this rank's reduce-scattered rows of K p,
+// shares[0..world) = every rank's share of p.q (k_pq_publish).  pq = the shares
+// summed in rank order; q = sigma y + lam p (as k_axpby_loc); then as k_update_xr.
+__global__ __launch_bounds__(256) void k_update_xr_shares(double *__restrict__ x,
+                                                          double *__restrict__ r,
+                                                          const double *__restrict__ p,
+                                                          const double *__restrict__ y,
+                                                          const double *__restrict__ shares,
+                                                          int world, int64_t n, double sigma,
+                                                          double lam,
+                                                          double *__restrict__ rr_part,
+                                                          DevState *st,
+                                                          const int *__restrict__ status) {
+  if (*status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  double pq = 0.0;
+  for (int g = 0; g < world; ++g) pq += shares[g];
+  const double alpha = st->rho / pq;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->pq = pq;
+    st->alpha = alpha;
+  }
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 256) {
+    const double pi = p[i];
+    const double qi = sigma * y[i] + lam * pi;
+    x[i] = fma(alpha, pi, x[i]);
+    const double ri = fma(-alpha, qi, r[i]);
+    r[i] = ri;
+    acc = fma(ri, ri, acc);
+  }
+  const double t = block_sum256(acc, sh);
+  if (threadIdx.x == 0) rr_part[blockIdx.x] = t;
+}
+
+void launch_update_xr_shares(double *x, double *r, const double *p, const double *y,
+                             const double *shares, int world, int64_t n, double sigma, double lam,
+                             double *rr_part, DevState *st, const int *status, hipStream_t s) {
+  hipLaunchKernelGGL(k_update_xr_shares, dim3(kVecGrid), dim3(256), 0, s, x, r, p, y, shares, world,
+                     n, sigma, lam, rr_part, st, status);
+}
+
 // alpha = rho / (p.q); x += alpha p; r -= alpha q; rr partials
 __global__ __launch_bounds__(256) void k_update_xr(double *__restrict__ x, double *__restrict__ r,
                                                    const double *__restrict__ p,
