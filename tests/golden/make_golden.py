@@ -318,21 +318,26 @@ def _nystrom_apply(it, task, R_desc, R_d_desc, tril_perms_lin, idx, variant, r):
     return P_op.matvec(r)
 
 
-def fx_sgdml(M, name, precons, seed=3, perms=None, with_K=True, none_tol=(1e-4,)):
-    ds = synthetic.ethanol_like(M, seed=seed)
-    task = make_task(ds, perms=perms)
+def fx_sgdml(M, name, precons, seed=3, perms=None, with_K=True, none_tol=(1e-4,), geom="ethanol",
+             k_rows=64):
+    """geom: 'ethanol' (9 atoms) or 'nanotube' (370 atoms, D = 68265: descriptors are not
+    stored, the consumer recomputes them from R with its own tested descriptor code)."""
+    ds = (synthetic.ethanol_like if geom == "ethanol" else synthetic.nanotube_like)(M, seed=seed)
+    task = make_task(ds, perms=perms, dataset_name=geom)
     desc, tpl, R_desc, R_d_desc, y, y_std = prepare(task)
     n = y.size
     out = {"R": ds["R"], "F": ds["F"], "E": ds["E"], "z": ds["z"], "perms": task["perms"],
-           "R_desc": R_desc, "R_d_desc": R_d_desc, "tril_perms_lin": tpl, "y": y,
+           "tril_perms_lin": tpl, "y": y,
            "y_std": np.float64(y_std), "sig": np.float64(10.0), "lam": np.float64(1e-10),
            "solver_tol": np.float64(task["solver_tol"])}
+    if geom == "ethanol":
+        out["R_desc"], out["R_d_desc"] = R_desc, R_d_desc
     K = gdml_train()._assemble_kernel_mat(R_desc, R_d_desc, tpl, 10, desc, use_E_cstr=False,
                                           col_idxs=np.s_[:], callback=noop)
     if with_K:
         out["K"] = np.array(K)
     else:  # too large to commit: keep a row sample for the assembly check
-        out["K_rows"] = np.array(K[:64])
+        out["K_rows"] = np.array(K[:k_rows])
     # operator and preconditioner applies on a fixed vector
     it, K_op = kernel_operator(task, desc, R_desc, R_d_desc, tpl, n)
     rng = np.random.default_rng(seed + 100)
@@ -352,7 +357,7 @@ def fx_sgdml(M, name, precons, seed=3, perms=None, with_K=True, none_tol=(1e-4,)
         except np.linalg.LinAlgError as e:  # the reference raises: record it
             out[f"nys{variant}_error"] = np.array(type(e).__name__)
     # solves at the boundary (Iterative.solve)
-    m, kmin, _ = plot_data.get_params("ethanol")
+    m, kmin, _ = plot_data.get_params(geom)
     k_rot = int(plot_data.rule_of_thumb(n=n, k_min=kmin, m=m))
     bp = k_rot / n
     out["k_rot"] = np.int64(k_rot)
@@ -433,6 +438,11 @@ FIXTURES = {
     "sgdml_n2997": lambda: fx_sgdml(
         111, "sgdml_ethanol_n2997", ["cholesky", "random_scores"], seed=9, with_K=False,
         none_tol=(1e-4,)),
+    # nanotube-like geometry (370 atoms, BASELINE configs[1] molecule), M = 3 -> N = 3330,
+    # nanotube rule-of-thumb rank; the reference's K_op costs ~0.1 s here
+    "sgdml_nanotube_n3330": lambda: fx_sgdml(
+        3, "sgdml_nanotube_n3330", ["cholesky", "random_scores"], seed=4, with_K=False,
+        none_tol=(), geom="nanotube", k_rows=16),
     "sgdml_n621": lambda: fx_sgdml(
         23, "sgdml_ethanol_n621", ["cholesky", "random_scores", "truncated_cholesky"], seed=7,
         none_tol=(1e-4,)),

@@ -36,7 +36,8 @@ def task_of(f):
 
 
 SEEDS = {"sgdml_ethanol_n270": 3, "sgdml_ethanol_n270_perms": 5, "sgdml_ethanol_n621": 7,
-         "sgdml_ethanol_n2997": 9, "sgdml_ethanol_n270_nongroup": 5}
+         "sgdml_ethanol_n2997": 9, "sgdml_ethanol_n270_nongroup": 5, "sgdml_nanotube_n3330": 4}
+NANOTUBE = "sgdml_nanotube_n3330"
 
 
 @pytest.mark.parametrize("name", ["sgdml_ethanol_n270", "sgdml_ethanol_n621",
@@ -87,15 +88,62 @@ def test_nystrom_apply_vs_reference(sg, golden_dir, name, variant):
     assert np.linalg.norm(z - ref) <= 1e-6 * np.linalg.norm(ref)
 
 
-def run_dropin(f, name, precon):
+def run_dropin(f, name, precon, desc=None):
     from sgdml_amd.solvers import Iterative
 
     n = f["y"].size
     bp = int(f["k_rot"]) / n
+    Rd, Rdd = desc if desc is not None else (f["R_desc"], f["R_d_desc"])
     np.random.seed(1000 + SEEDS[name])
     it = Iterative(None, None, device=0)
-    return it.solve(task_of(f), f["R_desc"], f["R_d_desc"], f["tril_perms_lin"], f["y"],
+    return it.solve(task_of(f), Rd, Rdd, f["tril_perms_lin"], f["y"],
                     float(f["y_std"]), break_percentage=bp, str_preconditioner=precon)
+
+
+@pytest.fixture(scope="module")
+def nanotube(sg, golden_dir):
+    """370-atom nanotube-like fixture: descriptors are computed here on the GPU (the
+    fixture stores only R; D = 68265)."""
+    f = load(golden_dir, NANOTUBE)
+    return f, sg.sgdml_descriptors(f["R"])
+
+
+def test_nanotube_operator_vs_reference(sg, nanotube):
+    f, (Rd, Rdd) = nanotube
+    n, lam, sig = f["y"].size, float(f["lam"]), float(f["sig"])
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, f["perms"], sig)
+        s.set_operator(-1.0, lam)
+        assert s.storage_info()[0] == "matfree"
+        Av = s.matvec(f["v"])
+        d = s.diag()
+        zs = []
+        for variant in (0, 1):
+            s.precon_nystrom(f["nys_idx"], variant=variant)
+            zs.append(s.precon_apply(f["v"]))
+    assert np.linalg.norm(-Av - f["Kop_v"]) <= 1e-13 * np.linalg.norm(f["Kop_v"])
+    np.testing.assert_allclose(d, f["diag_K"], rtol=1e-12)
+    for variant, z in enumerate(zs):
+        ref = f[f"nys{variant}_z"]
+        assert np.linalg.norm(z - ref) <= 1e-6 * np.linalg.norm(ref)
+    with sg.KernelSolver(n) as s:
+        s.assemble_sgdml(Rd, Rdd, f["perms"], sig)
+        K = s.get_matrix_rows(0, 16)
+    assert np.max(np.abs(K - f["K_rows"])) <= 1e-13 * np.abs(f["K_rows"]).max()
+
+
+@pytest.mark.parametrize("precon", ["cholesky", "random_scores"])
+def test_dropin_solve_nanotube(sg, nanotube, precon):
+    """Residual curve and coefficients against the reference's own solve on the
+    nanotube molecule (rule-of-thumb rank k = 873 at N = 3330)."""
+    f, desc = nanotube
+    alphas, num_iters, resid, rmse, idxs, is_conv, info = run_dropin(f, NANOTUBE, precon, desc)
+    assert is_conv and bool(f[f"{precon}__is_conv"])
+    assert np.array_equal(idxs, f[f"{precon}__inducing_pts_idxs"])
+    if precon == "cholesky":
+        assert np.array_equal(info["index_columns"], f["cholesky__index_columns"])
+    assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
 
 
 PRECONS = ["cholesky", "random_scores", "lev_scores", "inverse_lev", "lev_random",
