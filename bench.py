@@ -56,7 +56,10 @@ def parse():
     ap.add_argument("--ell", type=float, default=0.2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-1e-6 legs")
-    ap.add_argument("--cpu-iters", type=int, default=12)
+    ap.add_argument("--cpu-iters", type=int, default=100,
+                    help="PCG iterations of the CPU baseline (~10-20 s of host work at N=65536)")
+    ap.add_argument("--cpu-iters-1t", type=int, default=3,
+                    help="PCG iterations of the single-thread CPU baseline")
     ap.add_argument("--workload", choices=["rbf", "nanotube", "ethanol"], default="rbf",
                     help="rbf: configs[2] (default); nanotube: configs[1] (sGDML N=15540, "
                          "pivoted Cholesky k=2701 built on the GPU); ethanol: configs[0] geometry")
@@ -126,9 +129,20 @@ def pmc_traffic(workload: str, storage: str, world: int):
         return None
 
 
-def cpu_baseline(solver, X, b, idx, lam, ell, iters):
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
     """Oracle PCG iterations (NumPy/SciPy port of the reference CPU path) on the same
-    matrix, copied from the device; timed per iteration after one warm-up iteration."""
+    matrix, copied from the device; timed per iteration after one warm-up iteration,
+    with all BLAS threads and (a shorter sample) with one thread."""
     import threadpoolctl
 
     from oracle.pcg import cg_legacy
@@ -145,21 +159,33 @@ def cpu_baseline(solver, X, b, idx, lam, ell, iters):
         y += lam * v
         return y
 
-    cg_legacy(mv, b, tol=0.0, maxiter=1, psolve=lambda r: apply_panel(B, sp, lam, r))
-    t0 = time.perf_counter()
-    cg_legacy(mv, b, tol=0.0, maxiter=iters, psolve=lambda r: apply_panel(B, sp, lam, r))
-    el = time.perf_counter() - t0 - 0.0
-    # cg_legacy spends one extra mat-vec on the legacy ||A x0 - b|| check
-    t_mv = time.perf_counter()
-    mv(b)
-    t_mv = time.perf_counter() - t_mv
-    per_it = max(el - t_mv, 1e-9) / iters
+    def per_iter(m):
+        cg_legacy(mv, b, tol=0.0, maxiter=1, psolve=lambda r: apply_panel(B, sp, lam, r))
+        t0 = time.perf_counter()
+        cg_legacy(mv, b, tol=0.0, maxiter=m, psolve=lambda r: apply_panel(B, sp, lam, r))
+        el = time.perf_counter() - t0
+        # cg_legacy spends one extra mat-vec on the legacy ||A x0 - b|| check
+        t_mv = time.perf_counter()
+        mv(b)
+        t_mv = time.perf_counter() - t_mv
+        return max(el - t_mv, 1e-9) / m, t_mv
+
+    per_it, t_mv = per_iter(iters)
+    one = None
+    if iters_1t > 0:
+        with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+            p1, t1 = per_iter(iters_1t)
+        one = {"value": 1.0 / p1, "cores": 1, "ms_per_iter": p1 * 1e3,
+               "matvec_gbs": (8.0 * n * n) / (t1 * 1e9), "sample": f"{iters_1t} PCG iterations"}
     del K
     return {"value": 1.0 / per_it, "unit": "CG iters/s", "cores": int(threads), "kind": "port",
             "sample": f"{iters} PCG iterations (oracle cg_legacy + Nystrom apply, NumPy/OpenBLAS) "
                       f"on the same N={n} fp64 matrix copied from the GPU",
             "ms_per_iter": per_it * 1e3,
-            "matvec_gbs": (8.0 * n * n) / (t_mv * 1e9)}
+            "matvec_gbs": (8.0 * n * n) / (t_mv * 1e9),
+            "host_cpu": _cpu_model(),
+            "os_cpu_count": os.cpu_count(),
+            "single_thread": one}
 
 
 def parity_small(n, k, lam, ell, tol=1e-6):
@@ -288,7 +314,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
-                cpu = cpu_baseline(solver, X, b, idx, lam, ell, args.cpu_iters)
+                cpu = cpu_baseline(solver, X, b, idx, lam, ell, args.cpu_iters, args.cpu_iters_1t)
             except Exception as e:  # a baseline failure must not hide the GPU number
                 cpu = {"value": None, "error": repr(e)}
         par = None

@@ -202,7 +202,28 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += v[u];
   }
-  for (; t < nb; ++t) s += slot_val(P, Pq, split, nb, Np, t, bi, i);
+  // the remaining slots (split tiles among them) in batches of 8 as well; every slot
+  // value is ((P + Pq0) + Pq1) + Pq2 as in slot_val, added in slot order
+  const int64_t pl = (int64_t)nb * Np;
+  for (; t < nb; t += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      v[u] = 0.0;
+      const int tu = t + u;
+      if (tu < nb) {
+        v[u] = P[(int64_t)tu * Np + i];
+        if (tu > bi && split[(int64_t)tu * nb + bi]) {
+          const double q0 = Pq[(int64_t)tu * Np + i], q1 = Pq[pl + (int64_t)tu * Np + i],
+                       q2 = Pq[2 * pl + (int64_t)tu * Np + i];
+          v[u] = ((v[u] + q0) + q1) + q2;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (t + u < nb) s += v[u];
+  }
   if (EPI) {
     double yv = sigma * s;
     if (vloc != nullptr) yv += lam * vloc[i];

@@ -48,7 +48,7 @@ __device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ 
 // R rows per workgroup share every 16-B load of v (v is L2 resident); M is
 // streamed once with non-temporal 16-B loads, U loads in flight per row.
 // `rows` of M must be allocated up to a multiple of R (padding rows are zero).
-template <int R, int U, int EPI>
+template <int R, int U, int EPI, bool NT = true>
 __global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int64_t ld,
                                               int64_t rows, int64_t n2, int64_t cs2,
                                               const double *__restrict__ v,
@@ -80,7 +80,8 @@ __global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int6
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int u = 0; u < U; ++u) kv[r][u] = __builtin_nontemporal_load(rowp[r] + c + u * 256);
+      for (int u = 0; u < U; ++u)
+        kv[r][u] = NT ? __builtin_nontemporal_load(rowp[r] + c + u * 256) : rowp[r][c + u * 256];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int6
     const d2 xv = v2[c];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const d2 kv = __builtin_nontemporal_load(rowp[r] + c);
+      const d2 kv = NT ? __builtin_nontemporal_load(rowp[r] + c) : rowp[r][c];
       acc[r] = fma(kv.x, xv.x, acc[r]);
       acc[r] = fma(kv.y, xv.y, acc[r]);
     }
@@ -147,8 +148,11 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
   const int64_t n2 = ncols / 2;  // ncols is the padded local length (even)
   const int64_t cs2 = (n2 + splits - 1) / splits;
   dim3 grid((unsigned)((k + R - 1) / R), (unsigned)splits);
-  hipLaunchKernelGGL((k_gemv<R, U, 0>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart, k,
-                     1.0, 0.0, (const double *)nullptr, status);
+  // default-policy loads: the panel (k x N, 134 MB at k = 256, N = 65536) can stay in
+  // the 256 MB MALL between this pass, the T^T t pass and the next iteration, since the
+  // operator streams K with non-temporal loads
+  hipLaunchKernelGGL((k_gemv<R, U, 0, false>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
+                     k, 1.0, 0.0, (const double *)nullptr, status);
 }
 
 // ---------------------------------------------------------------------------

@@ -258,3 +258,34 @@ def test_rbf_reference_generator_and_preconditioner(sg, golden_dir):
         np.testing.assert_array_equal(piv3[:k3], f["index_columns3"][:k3])
         z = s.precon_apply(f["r"])
     np.testing.assert_allclose(z, f["z"], rtol=1e-9, atol=1e-9 * np.abs(f["z"]).max())
+
+
+def test_dropin_info_dict_schema(sg, golden_dir, tmp_path):
+    """The info dict carries the reference's keys (iterative_solver.py:1094-1105, plus the
+    pivoted-Cholesky info of incomplete_cholesky.py:86-88), so the reference's consumers
+    work unchanged: create_model/model.update (train.py:925-940), tools/create_data.cg_steps
+    (create_data.py:117-148) and store_model's np.savez_compressed (train_models.py:152-154)."""
+    name = "sgdml_ethanol_n270"
+    f = load(golden_dir, name)
+    alphas, num_iters, resid, rmse, idxs, is_conv, info = run_dropin(f, name, "cholesky")
+    ref_keys = {"is_conv", "total_time_cholesky", "total_time_cg", "total_time_solve",
+                "total_time_preconditioner", "time_cholesky", "L.shape", "index_columns"}
+    assert ref_keys <= set(info)
+    k = int(f["k_rot"])
+    n = f["y"].size
+    t = info["time_cholesky"]
+    assert t.shape == (k,) and np.all(t >= 0)
+    # cg_steps' arithmetic
+    t_begin, t_end = np.median(t[:20]), np.median(t[20:])
+    assert np.isfinite(t_end / t_begin - 1)
+    assert info["total_time_cg"] / num_iters > 0
+    assert len(idxs) / len(alphas) == k / n
+    # store_model: the solver's fields and info values round-trip through savez_compressed
+    model = dict(info, alphas_F=alphas, solver_iters=num_iters, solver_resid=resid,
+                 inducing_pts_idxs=idxs, norm_y_train=np.linalg.norm(f["y"]))
+    path = tmp_path / "model.npz"
+    np.savez_compressed(path, **model)
+    back = np.load(path, allow_pickle=False)
+    np.testing.assert_array_equal(back["alphas_F"], alphas)
+    np.testing.assert_array_equal(back["index_columns"], info["index_columns"])
+    assert tuple(back["L.shape"]) == (n, k)
