@@ -538,21 +538,28 @@ void mark_end(mlff_ctx *ctx, std::vector<GemvMark> *marks, hipEvent_t e0, long l
 //   allreduce(rr partials | T r partials of the next iteration)   (low-rank precon)
 // Same recurrence as launch_iteration; the sums are over the same terms in another
 // (fixed) order, bitwise identical on all ranks.
-int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) {
+int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks,
+                           bool fold_in, bool stop_out) {
   hipStream_t s = ctx->stream;
   const int *status = &ctx->st->status;
   double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
   double *zg = ctx->gb + (int64_t)ctx->rank * ctx->gstride;  // this rank's gather block
   const bool lowrank = ctx->precon_kind != MLFF_PRECON_NONE;
+  double *rrp = lowrank ? ctx->tpart_base : rr_part(ctx);
+  StopFold fold;  // stop test of iteration it - 1 in this iteration's first kernel
+  if (fold_in) fold = StopFold{rrp, ctx->st, ctx->trace, it - 1};
   if (lowrank) {
     if (!ctx->spec_t) {
-      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s,
+                        fold);
+      fold = StopFold{};
       MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     }
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, zg, ctx->nrows,
-                    ctx->sigma_p, 1.0 / ctx->lam, zg + ctx->blk, status, s, ctx->zpart, ctx->zsplit);
+                    ctx->sigma_p, 1.0 / ctx->lam, zg + ctx->blk, status, s, ctx->zpart, ctx->zsplit,
+                    fold);
   } else {
-    launch_copy_dot(ctx->r, ctx->nrows, zg, zg + ctx->blk, status, s);
+    launch_copy_dot(ctx->r, ctx->nrows, zg, zg + ctx->blk, status, s, fold);
   }
   MLFF_TRY(comm_allgather(ctx, zg, ctx->gb, (size_t)ctx->gstride));
   launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
@@ -577,7 +584,6 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
     launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx),
                      lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
   }
-  double *rrp = lowrank ? ctx->tpart_base : rr_part(ctx);
   if (lowrank) {
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
     MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
@@ -585,62 +591,50 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   } else {
     MLFF_TRY(allreduce(ctx, rrp, kVecGrid));
   }
-  launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
+  if (stop_out) launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
   return MLFF_OK;
 }
 
-// one PCG iteration (ITER = it), all launches status gated
-int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks) {
-  if (ctx->world > 1) return launch_iteration_ranks(ctx, it, marks);
+// one PCG iteration (ITER = it), all launches status gated.  fold_in: the stop test of
+// iteration it - 1 runs in this iteration's first kernel (StopFold); stop_out: the stop
+// test of this iteration runs as its own launch (last iteration of a chunk)
+int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, bool fold_in,
+                     bool stop_out) {
+  if (ctx->world > 1) return launch_iteration_ranks(ctx, it, marks, fold_in, stop_out);
   hipStream_t s = ctx->stream;
   const int *status = &ctx->st->status;
   double *p_loc = ctx->p_full + (int64_t)ctx->rank * ctx->blk;
   const bool lowrank = ctx->precon_kind != MLFF_PRECON_NONE;
-  // several ranks + low-rank preconditioner: T r of the next iteration is computed
-  // right after r is updated and reduced together with ||r||^2 (one collective
-  // fewer per iteration; same values, the stop test still gates everything after)
-  const bool merge = lowrank && ctx->world > 1;
+  StopFold fold;
+  if (fold_in) fold = StopFold{rr_part(ctx), ctx->st, ctx->trace, it - 1};
   const double *zsrc;
   if (lowrank) {
-    if (!(merge && ctx->spec_t)) {
-      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
-      MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
-    }
+    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s,
+                      fold);
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
                     ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
     zsrc = ctx->z;
   } else {
-    launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s);
+    launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s, fold);
     zsrc = ctx->r;
   }
-  MLFF_TRY(allreduce(ctx, rho_part(ctx), kVecGrid));
   launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
-  MLFF_TRY(allgather_blocks(ctx, ctx->p_full));
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (ctx->timing.on && marks != nullptr) {
-    e0 = timing_event(ctx);
-    if (e0) hipEventRecord(e0, s);
-  }
-  MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
-  if (e0 != nullptr) {
-    e1 = timing_event(ctx);
-    if (e1) {
-      hipEventRecord(e1, s);
-      marks->push_back({ctx->timing.used - 2, it});
-    }
-  }
-  launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
-  MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
-  double *rrp = merge ? ctx->tpart_base : rr_part(ctx);
-  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rrp, ctx->st, status, s);
-  if (merge) {
-    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
-    MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
-    ctx->spec_t = true;
+  hipEvent_t e0;
+  mark_begin(ctx, marks, &e0);
+  if (ctx->use_sym) {
+    // q = sigma K p + lam p and the p.q partials from the slot reduction (no dot launch)
+    launch_symv(ctx->sym, ctx->p_full, ctx->sym.P, status, s);
+    launch_sym_reduce_pq(ctx->sym, ctx->nrows, ctx->q, ctx->sigma_K, ctx->lam, p_loc,
+                         pq_part(ctx), status, s);
+    mark_end(ctx, marks, e0, it);
   } else {
-    MLFF_TRY(allreduce(ctx, rrp, kVecGrid));
+    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
+    mark_end(ctx, marks, e0, it);
+    launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
   }
-  launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
+  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
+                   status, s);
+  if (stop_out) launch_stoptest(rr_part(ctx), ctx->st, ctx->trace, it, s);
   return MLFF_OK;
 }
 
@@ -1229,7 +1223,8 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
       c0 = timing_event(ctx);
       if (c0) hipEventRecord(c0, s);
     }
-    for (int64_t it = first; it <= last; ++it) MLFF_TRY(launch_iteration(ctx, it, &marks));
+    for (int64_t it = first; it <= last; ++it)
+      MLFF_TRY(launch_iteration(ctx, it, &marks, it > first, it == last));
     if (ctx->timing.on) {
       c1 = timing_event(ctx);
       if (c1) hipEventRecord(c1, s);

@@ -84,6 +84,15 @@ struct MfData {
   std::vector<int32_t> perms, piinv;      // host copies (diagonal blocks)
 };
 
+// The scipy stop test of iteration `it` (k_stoptest), done by every workgroup of the
+// next iteration's first kernel instead of a launch of its own (rr_part == nullptr: none).
+struct StopFold {
+  const double *rr_part = nullptr;
+  DevState *st = nullptr;
+  double *trace = nullptr;
+  long long it = 0;
+};
+
 struct Timing {
   bool on = false;
   std::vector<hipEvent_t> ev;  // pool, pairs (start, stop)
@@ -195,22 +204,23 @@ void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v
                       hipStream_t s);
 // partial T GEMV: tpart[sp * k + j] = sum_{c in split sp} T[j, c] * r[c]
 void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
-                       const double *r, double *tpart, const int *status, hipStream_t s);
+                       const double *r, double *tpart, const int *status, hipStream_t s,
+                       StopFold fold = StopFold{});
 int choose_tsplit(int64_t k, int64_t ncols);
 // z = sigma_p/lam * (r - T^T t), t = sum_sp tpart; rho partials (r . z)
 // (split-K over the k rows of T: zpart holds zsplit x ldt partial sums)
 void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
                      double *rho_part, const int *status, hipStream_t s, double *zpart,
-                     int zsplit);
+                     int zsplit, StopFold fold = StopFold{});
 // part[ks * ldw + c] = sum_{j in slice ks} W[j, c] * (sum_sp tsrc[sp * tstride + j])
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
-                         const int *status, hipStream_t s);
+                         const int *status, hipStream_t s, StopFold fold = StopFold{});
 int choose_ksplit(int64_t k, int64_t ncols);
 // rho partials of r . r (no preconditioner)
 void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
-                     const int *status, hipStream_t s);
+                     const int *status, hipStream_t s, StopFold fold = StopFold{});
 // p = z + (rho/rho1) p   (p = z at iteration 1); rho = sum(rho_part)
 void launch_update_p(const double *z, double *p, int64_t n, const double *rho_part,
                      DevState *st, long long it, const int *status, hipStream_t s);
@@ -218,7 +228,7 @@ void launch_update_p(const double *z, double *p, int64_t n, const double *rho_pa
 // and its rho partials): dst = r with r.r partials (no preconditioner);
 // p_full = z_full + (rho/rho1) p_full with rho summed from all ranks' partials
 void launch_copy_dot(const double *r, int64_t n, double *dst, double *part, const int *status,
-                     hipStream_t s);
+                     hipStream_t s, StopFold fold = StopFold{});
 void launch_update_p_gathered(const double *gb, int64_t gstride, int64_t blk, int world,
                               double *p_full, DevState *st, long long it, const int *status,
                               hipStream_t s);
@@ -290,6 +300,10 @@ void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *
 // one rank: y[i] = sum of the slots of row i (i < n_out); epilogue y = sigma y + lam vloc
 void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogue, double sigma,
                        double lam, const double *vloc, const int *status, hipStream_t s);
+// one rank, PCG: q = sigma (slot sums) + lam p over n_out rows, and the p.q partial sums
+// of the kVecGrid workgroups into pq_part
+void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
+                          const double *p, double *pq_part, const int *status, hipStream_t s);
 // several ranks: sp.yg = this rank's slot sums of every row (rank blocks of sp.ystride);
 // with p_full: also this rank's share sigma p.y_g + lam ||p_loc||^2 published into the
 // tail slot `rank` of every block (pq_part / pp_part: kVecGrid scratch each)

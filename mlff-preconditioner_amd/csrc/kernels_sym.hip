@@ -175,7 +175,10 @@ __device__ __forceinline__ int owner_of(int I, int J, int tiles_per_rank) {
 
 // y[i] = sum_{t=0}^{nb-1} P[t, i] over the slots whose tile this rank owns
 // (all slots on one rank); EPI: y = sigma * y + lam * vloc for rows < n_out
-template <bool EPI>
+// y[i] = sum_{t=0}^{nb-1} of the slots of row i (one rank); EPI: y = sigma y + lam vloc;
+// PQ (with EPI): also the p.q partial sums (vloc = p) of each workgroup -> pq_part
+// (grid = kVecGrid workgroups, grid-stride over the rows)
+template <bool EPI, bool PQ>
 __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P,
                                                     const double *__restrict__ Pq,
                                                     const unsigned char *__restrict__ split,
@@ -183,53 +186,65 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
                                                     int64_t n_out, double *__restrict__ y,
                                                     double sigma, double lam,
                                                     const double *__restrict__ vloc,
+                                                    double *__restrict__ pq_part,
                                                     const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n_out) return;
-  const int bi = (int)(i / B);
-  double s = 0.0;
-  // slots below t_split hold no split tile for this row block (t_split: the first
-  // slot t > bi whose tile (t, bi) is split, nb if none).  8 slot loads in flight per
-  // thread; the additions stay in slot order
-  const int tend = t_split > bi ? t_split : bi + 1;
-  const int t8 = tend < nb ? tend : nb;
-  int t = 0;
-  for (; t + 7 < t8; t += 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-  }
-  // the remaining slots (split tiles among them) in batches of 8 as well; every slot
-  // value is ((P + Pq0) + Pq1) + Pq2 as in slot_val, added in slot order
+  double apq = 0.0;
   const int64_t pl = (int64_t)nb * Np;
-  for (; t < nb; t += 8) {
-    double v[8];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_out;
+       i += (int64_t)gridDim.x * 256) {
+    const int bi = (int)(i / B);
+    double s = 0.0;
+    // slots below t_split hold no split tile for this row block (t_split: the smallest
+    // row-block index of a split tile, nb if none).  8 slot loads in flight per
+    // thread; the additions stay in slot order
+    const int tend = t_split > bi ? t_split : bi + 1;
+    const int t8 = tend < nb ? tend : nb;
+    int t = 0;
+    for (; t + 7 < t8; t += 8) {
+      double v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      v[u] = 0.0;
-      const int tu = t + u;
-      if (tu < nb) {
-        v[u] = P[(int64_t)tu * Np + i];
-        if (tu > bi && split[(int64_t)tu * nb + bi]) {
-          const double q0 = Pq[(int64_t)tu * Np + i], q1 = Pq[pl + (int64_t)tu * Np + i],
-                       q2 = Pq[2 * pl + (int64_t)tu * Np + i];
-          v[u] = ((v[u] + q0) + q1) + q2;
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    // the remaining slots (split tiles among them) in batches of 8 as well; every slot
+    // value is ((P + Pq0) + Pq1) + Pq2 as in slot_val, added in slot order
+    for (; t < nb; t += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = 0.0;
+        const int tu = t + u;
+        if (tu < nb) {
+          v[u] = P[(int64_t)tu * Np + i];
+          if (tu > bi && split[(int64_t)tu * nb + bi]) {
+            const double q0 = Pq[(int64_t)tu * Np + i], q1 = Pq[pl + (int64_t)tu * Np + i],
+                         q2 = Pq[2 * pl + (int64_t)tu * Np + i];
+            v[u] = ((v[u] + q0) + q1) + q2;
+          }
         }
       }
-    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (t + u < nb) s += v[u];
+      for (int u = 0; u < 8; ++u)
+        if (t + u < nb) s += v[u];
+    }
+    if (EPI) {
+      double yv = sigma * s;
+      if (vloc != nullptr) yv += lam * vloc[i];
+      y[i] = yv;
+      if (PQ) apq = fma(vloc[i], yv, apq);
+    } else {
+      y[i] = s;
+    }
   }
-  if (EPI) {
-    double yv = sigma * s;
-    if (vloc != nullptr) yv += lam * vloc[i];
-    y[i] = yv;
-  } else {
-    y[i] = s;
+  if (PQ) {
+    __shared__ double sh[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) apq += __shfl_down(apq, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = apq;
+    __syncthreads();
+    if (threadIdx.x == 0) pq_part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   }
 }
 
@@ -393,11 +408,20 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
   if (n_out <= 0) return;
   const dim3 grid((unsigned)((n_out + 255) / 256));
   if (epilogue)
-    hipLaunchKernelGGL((k_sym_reduce<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
-                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc, status);
+    hipLaunchKernelGGL((k_sym_reduce<true, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
+                       (double *)nullptr, status);
   else
-    hipLaunchKernelGGL((k_sym_reduce<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
-                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc, status);
+    hipLaunchKernelGGL((k_sym_reduce<false, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
+                       (double *)nullptr, status);
+}
+
+void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
+                          const double *p, double *pq_part, const int *status, hipStream_t s) {
+  hipLaunchKernelGGL((k_sym_reduce<true, true>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
+                     sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, p, pq_part,
+                     status);
 }
 
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,

@@ -42,6 +42,34 @@ __device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ 
   return sh[4];
 }
 
+// Stop test of iteration f.it (as k_stoptest) at the start of the next iteration's first
+// kernel: every workgroup reduces the same partials in the same order and reaches the
+// same decision; workgroup (0, 0) writes the state.  All threads of the block call it.
+// Returns false when the solver stops (the caller returns).
+__device__ __forceinline__ bool stop_prologue(const StopFold &f, double *sh) {
+  if (f.rr_part == nullptr) return true;
+  const double rr = reduce_parts_bcast(f.rr_part, kVecGrid, sh);
+  __syncthreads();  // sh is reused by the caller
+  const double resid = sqrt(rr);
+  DevState *st = f.st;
+  int dec = ST_RUNNING;
+  if (resid <= st->atol)
+    dec = f.it > 1 ? ST_RECHECK : ST_CONVERGED;
+  else if (f.it >= st->maxiter)
+    dec = ST_MAXITER;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    st->rr = rr;
+    st->resid = resid;
+    st->iters = f.it;
+    f.trace[f.it] = resid;
+    if (dec != ST_RUNNING)
+      st->status = dec;
+    else
+      st->rho1 = st->rho;
+  }
+  return dec == ST_RUNNING;
+}
+
 // ---------------------------------------------------------------------------
 // Dense row GEMV: y[row] = sigma * sum_c M[row, c] v[c] + lam * vloc[row]   (EPI=1)
 //                 part[split * out_stride + row] = sum_{c in split} M[row,c] v[c] (EPI=0)
@@ -55,9 +83,10 @@ __global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int6
                                               double *__restrict__ out, int64_t out_stride,
                                               double sigma, double lam,
                                               const double *__restrict__ vloc,
-                                              const int *__restrict__ status) {
+                                              const int *__restrict__ status, StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sh[4 * R];
+  __shared__ double sh[4 * R > 8 ? 4 * R : 8];
+  if (!stop_prologue(fold, sh)) return;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int64_t c_begin = (int64_t)blockIdx.y * cs2;
   int64_t c_end = c_begin + cs2;
@@ -129,7 +158,7 @@ void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v
   const int64_t n2 = ld / 2;
   dim3 grid((unsigned)((rows + R - 1) / R), 1);
   hipLaunchKernelGGL((k_gemv<R, U, 1>), grid, dim3(256), 0, s, M, ld, rows, n2, n2, v, y,
-                     (int64_t)0, sigma, lam, vloc, status);
+                     (int64_t)0, sigma, lam, vloc, status, StopFold{});
 }
 
 int choose_tsplit(int64_t k, int64_t ncols) {
@@ -143,7 +172,8 @@ int choose_tsplit(int64_t k, int64_t ncols) {
 }
 
 void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
-                       const double *r, double *tpart, const int *status, hipStream_t s) {
+                       const double *r, double *tpart, const int *status, hipStream_t s,
+                       StopFold fold) {
   constexpr int R = 4, U = 2;
   const int64_t n2 = ncols / 2;  // ncols is the padded local length (even)
   const int64_t cs2 = (n2 + splits - 1) / splits;
@@ -152,7 +182,7 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
   // the 256 MB MALL between this pass, the T^T t pass and the next iteration, since the
   // operator streams K with non-temporal loads
   hipLaunchKernelGGL((k_gemv<R, U, 0, false>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
-                     k, 1.0, 0.0, (const double *)nullptr, status);
+                     k, 1.0, 0.0, (const double *)nullptr, status, fold);
 }
 
 // ---------------------------------------------------------------------------
@@ -164,9 +194,11 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
                                                       int64_t k, const double *__restrict__ tsrc,
                                                       int tsplits, int64_t tstride,
                                                       int64_t kslice, double *__restrict__ part,
-                                                      const int *__restrict__ status) {
+                                                      const int *__restrict__ status,
+                                                      StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
   extern __shared__ double t_sh[];
+  if (!stop_prologue(fold, t_sh)) return;
   const int64_t j0 = (int64_t)blockIdx.y * kslice;
   const int64_t j1 = (j0 + kslice) < k ? (j0 + kslice) : k;
   for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
@@ -215,11 +247,12 @@ int choose_ksplit(int64_t k, int64_t ncols) {
 
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
-                         const int *status, hipStream_t s) {
+                         const int *status, hipStream_t s, StopFold fold) {
   const int64_t kslice = (k + ksplit - 1) / ksplit;
   const dim3 grid((unsigned)((ldw / 2 + 255) / 256), (unsigned)ksplit);
-  hipLaunchKernelGGL(k_colgemv_part, grid, dim3(256), sizeof(double) * (kslice + 1), s, W, ldw, k,
-                     tsrc, tsplits, tstride, kslice, part, status);
+  const size_t shm = sizeof(double) * (kslice + 1 > 8 ? kslice + 1 : 8);
+  hipLaunchKernelGGL(k_colgemv_part, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits, tstride,
+                     kslice, part, status, fold);
 }
 
 // z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
@@ -248,8 +281,8 @@ __global__ __launch_bounds__(256) void k_precon_fin(const double *__restrict__ p
 void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
                      double *rho_part, const int *status, hipStream_t s, double *zpart,
-                     int zsplit) {
-  launch_colgemv_part(T, ldt, k, tpart, splits, k, zsplit, zpart, status, s);
+                     int zsplit, StopFold fold) {
+  launch_colgemv_part(T, ldt, k, tpart, splits, k, zsplit, zpart, status, s, fold);
   hipLaunchKernelGGL(k_precon_fin, dim3(kVecGrid), dim3(256), 0, s, zpart, zsplit, ldt, r, z, n,
                      sigma_p, lam_inv, rho_part, status);
 }
@@ -258,9 +291,11 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
 __global__ __launch_bounds__(256) void k_dot_part(const double *__restrict__ a,
                                                   const double *__restrict__ b, int64_t n,
                                                   double *__restrict__ part,
-                                                  const int *__restrict__ status) {
+                                                  const int *__restrict__ status,
+                                                  StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[8];
+  if (!stop_prologue(fold, sh)) return;
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256)
@@ -270,8 +305,8 @@ __global__ __launch_bounds__(256) void k_dot_part(const double *__restrict__ a,
 }
 
 void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
-                     const int *status, hipStream_t s) {
-  hipLaunchKernelGGL(k_dot_part, dim3(kVecGrid), dim3(256), 0, s, a, b, n, part, status);
+                     const int *status, hipStream_t s, StopFold fold) {
+  hipLaunchKernelGGL(k_dot_part, dim3(kVecGrid), dim3(256), 0, s, a, b, n, part, status, fold);
 }
 
 // p = z + beta p  (Fortran: DAXPY(beta, P, Z); DCOPY(Z, P)); p = z at ITER == 1
@@ -315,9 +350,11 @@ void launch_update_p(const double *z, double *p, int64_t n, const double *rho_pa
 __global__ __launch_bounds__(256) void k_copy_dot(const double *__restrict__ r, int64_t n,
                                                   double *__restrict__ dst,
                                                   double *__restrict__ part,
-                                                  const int *__restrict__ status) {
+                                                  const int *__restrict__ status,
+                                                  StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[8];
+  if (!stop_prologue(fold, sh)) return;
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
@@ -330,8 +367,8 @@ __global__ __launch_bounds__(256) void k_copy_dot(const double *__restrict__ r, 
 }
 
 void launch_copy_dot(const double *r, int64_t n, double *dst, double *part, const int *status,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(k_copy_dot, dim3(kVecGrid), dim3(256), 0, s, r, n, dst, part, status);
+                     hipStream_t s, StopFold fold) {
+  hipLaunchKernelGGL(k_copy_dot, dim3(kVecGrid), dim3(256), 0, s, r, n, dst, part, status, fold);
 }
 
 __global__ __launch_bounds__(256) void k_update_p_gathered(const double *__restrict__ gb,
