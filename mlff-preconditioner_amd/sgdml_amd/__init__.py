@@ -7,6 +7,7 @@ numerics run in libmlffpcg.so (hand-written HIP kernels, include/mlffpcg.h).
 """
 from ._native import load_library, device_count, comm_unique_id  # noqa: F401
 from .solver import KernelSolver, PCGResult, sgdml_descriptors  # noqa: F401
+from .sharded import ShardedKernelSolver  # noqa: F401
 from .rule_of_thumb import get_params, rule_of_thumb  # noqa: F401
 
 __version__ = "0.1.0"

@@ -19,9 +19,11 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def padded_block(n: int, world: int) -> int:
-    """Padded per-rank length (multiple of 64 doubles) of the device vectors."""
+    """Padded per-rank length of the device vectors (mlff_ctx_create: a multiple of 64
+    doubles on one rank, of the 512-row tile edge on several)."""
     rows_per = (n + world - 1) // world
-    return (rows_per + 63) // 64 * 64
+    q = 64 if world == 1 else 512
+    return (rows_per + q - 1) // q * q
 
 
 def broadcast_comm_id(pg, rank: int) -> bytes:

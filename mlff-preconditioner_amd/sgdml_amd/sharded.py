@@ -1,0 +1,200 @@
+"""Several GPUs inside one process: the drop-in's multi-GPU mode.
+
+The reference runs its GPU operator on every GPU of a node from ONE process
+(`torch.nn.DataParallel`, src/sGDML/sgdml/predict.py:335-341); `Iterative.solve` is a
+single-process API.  `ShardedKernelSolver` keeps that shape: it owns one
+`KernelSolver` per device, each driven by its own worker thread (ctypes releases the
+GIL, so the ranks' blocking collectives run concurrently), joined by one RCCL
+communicator created in-process (`ncclCommInitRank` per thread), or by the library's
+in-process transport ("LOCAL:") when two ranks share a device (tests on one GPU).
+
+The methods mirror `KernelSolver` with GLOBAL arrays: inputs are whole N-vectors,
+outputs are gathered over the row blocks.  Every call runs on all ranks in the same
+order, exactly as the one-process-per-GPU launch of bench.py does.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+
+import numpy as np
+
+from . import _native as nat
+from .solver import KernelSolver, PCGResult
+
+
+class _Worker(threading.Thread):
+    def __init__(self):
+        super().__init__(daemon=True)
+        self.q: queue.Queue = queue.Queue()
+        self.start()
+
+    def run(self):
+        while True:
+            item = self.q.get()
+            if item is None:
+                return
+            fn, box, done = item
+            try:
+                box["value"] = fn()
+            except BaseException as e:  # noqa: BLE001 - re-raised by the caller
+                box["error"] = e
+            done.set()
+
+
+class ShardedKernelSolver:
+    def __init__(self, n: int, devices, comm: str | None = None):
+        devices = [int(d) for d in devices]
+        if len(devices) < 2:
+            raise ValueError("ShardedKernelSolver needs at least two ranks")
+        self.n, self.world, self.devices = int(n), len(devices), devices
+        if comm is None:
+            comm = "local" if len(set(devices)) < len(devices) else "rccl"
+        if comm == "rccl":
+            comm_id = nat.comm_unique_id()
+        elif comm == "local":
+            key = f"LOCAL:sharded-{id(self)}-{np.random.default_rng().integers(1 << 62)}"
+            comm_id = key.encode().ljust(128, b"\0")
+        else:
+            raise ValueError("comm must be 'rccl' or 'local'")
+        self.comm = comm
+        self._workers = [_Worker() for _ in devices]
+        self.ranks: list[KernelSolver | None] = [None] * self.world
+        self._all(lambda r: KernelSolver(n, device=devices[r], rank=r, world=self.world,
+                                         comm_id=comm_id), assign=True)
+        self.spans = [s.row_range() for s in self.ranks]
+
+    # ------------------------------------------------------------------ dispatch
+    def _all(self, fn, assign=False):
+        """fn(rank) on every rank's worker thread; returns the per-rank results."""
+        boxes, events = [], []
+        for r, w in enumerate(self._workers):
+            box, done = {}, threading.Event()
+            w.q.put((lambda r=r: fn(r), box, done))
+            boxes.append(box)
+            events.append(done)
+        for e in events:
+            e.wait()
+        for b in boxes:
+            if "error" in b:
+                raise b["error"]
+        out = [b.get("value") for b in boxes]
+        if assign:
+            self.ranks = out
+        return out
+
+    def _each(self, name, *args, **kw):
+        return self._all(lambda r: getattr(self.ranks[r], name)(*args, **kw))
+
+    def _gather(self, parts):
+        return np.concatenate(parts)
+
+    def _local(self, v, r):
+        a, b = self.spans[r]
+        return np.ascontiguousarray(v[a:b])
+
+    # --------------------------------------------------------------- lifecycle
+    def close(self):
+        if getattr(self, "_workers", None) is None:
+            return
+        try:
+            if all(s is not None for s in self.ranks):
+                self._each("close")
+        finally:
+            for w in self._workers:
+                w.q.put(None)
+            self._workers = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ same on all
+    def sgdml_operator(self, *a, **k):
+        self._each("sgdml_operator", *a, **k)
+
+    def assemble_sgdml(self, *a, **k):
+        self._each("assemble_sgdml", *a, **k)
+
+    def gen_rbf(self, *a, **k):
+        self._each("gen_rbf", *a, **k)
+
+    def set_operator(self, *a, **k):
+        self._each("set_operator", *a, **k)
+
+    def set_storage(self, *a, **k):
+        self._each("set_storage", *a, **k)
+
+    def storage_info(self):
+        out = self._each("storage_info")
+        return out[0][0], float(sum(b for _, b in out))
+
+    def precon_none(self):
+        self._each("precon_none")
+
+    def precon_pivchol(self, k, build_woodbury=True):
+        out = self._each("precon_pivchol", k, build_woodbury)
+        return out[0]  # index_columns are replicated on every rank
+
+    def precon_nystrom(self, idx, variant=0):
+        return max(self._each("precon_nystrom", idx, variant))
+
+    def precon_eig(self, *a, **k):
+        raise NotImplementedError("the eigen preconditioners factor all of K on one GPU "
+                                  "(rocSOLVER dsyevd); use a single device")
+
+    def lev_scores(self, idx, lam):
+        return self._each("lev_scores", idx, lam)[0]  # global scores on every rank
+
+    def timing(self, on=True):
+        self._each("timing", on)
+
+    def timing_reset(self):
+        self._each("timing_reset")
+
+    def timing_read(self):
+        out = self._each("timing_read")
+        # the slowest rank bounds the step
+        return max(out, key=lambda t: t["iter_ms"])
+
+    # ------------------------------------------------------- gathered results
+    def matvec(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        return self._gather(self._each("matvec", v))
+
+    def diag(self):
+        return self._gather(self._each("diag"))
+
+    def precon_apply(self, r):
+        r = np.ascontiguousarray(r, dtype=np.float64)
+        return self._gather(self._all(lambda q: self.ranks[q].precon_apply(self._local(r, q))))
+
+    def pcg(self, b, x0=None, tol=1e-5, maxiter=None, callback=None, cb_every=0, chunk=0):
+        """KernelSolver.pcg over all ranks (global b / x0 / x); callback(x, iters, resid)
+        sees the gathered iterate."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x0 = None if x0 is None else np.ascontiguousarray(x0, dtype=np.float64)
+        early = self._all(lambda r: self.ranks[r].pcg_start(
+            self._local(b, r), None if x0 is None else self._local(x0, r), tol, maxiter))[0]
+        maxiter = self.ranks[0]._maxiter
+        status = self.ranks[0].pcg_result()[1]
+        step = int(cb_every) if cb_every and cb_every > 0 else maxiter
+        while status == nat.PCG_RUNNING:
+            status = self._each("pcg_run", step, chunk)[0]
+            if callback is not None and status == nat.PCG_RUNNING:
+                it, _, res, _ = self.ranks[0].pcg_result()
+                callback(self._gather(self._each("pcg_x")), it, res)
+        it, status, resid, info = self.ranks[0].pcg_result()
+        x = self._gather(self._each("pcg_x"))
+        trace = self.ranks[0].pcg_trace()
+        callbacks = 0 if early else max(it, 1)
+        return PCGResult(x=x, info=info, iters=it, resid=resid, trace=trace, early_exit=early,
+                         callbacks=callbacks)

@@ -16,16 +16,23 @@ What runs where:
   * every preconditioner build (pivoted Cholesky, Nystrom, _sb, leverage
     scores, eigen-decomposition) and the PCG iterations run in libmlffpcg.so;
   * column *selection* stays on the host with NumPy's global RNG exactly as in the
-    reference (:683-757), so a seeded run draws the same indices.
+    reference (:683-757), so a seeded run draws the same indices;
+  * several GPUs (`devices=[0, 1, ...]`, or MLFF_DEVICES="0,1,..." / "all"): the rows of
+    the operator and of the preconditioner panel are sharded over the devices from this
+    one process (sgdml_amd.sharded, RCCL), as the reference spreads its GPU operator
+    with DataParallel (predict.py:335-341).  The eigen preconditioners factor all of K
+    on the first device.
 """
 from __future__ import annotations
 
+import os
 import timeit
 from functools import partial
 
 import numpy as np
 
 from .. import _native as nat
+from ..sharded import ShardedKernelSolver
 from ..solver import KernelSolver
 
 LEV_SCORES_KEYS = ["lev_scores", "random_scores", "inverse_lev", "lev_random",
@@ -37,13 +44,20 @@ EIGVEC_KEYS = ["eigvec_precon", "eigvec_precon_block_diagonal",
 
 class Iterative(object):
     def __init__(self, gdml_train, desc, callback=None, max_processes=None, use_torch=False,
-                 device=None):
+                 device=None, devices=None):
         self.gdml_train = gdml_train
         self.desc = desc
         self.callback = callback
         self._max_processes = max_processes
         self._use_torch = use_torch
         self.device = device
+        if devices is None:
+            env = os.environ.get("MLFF_DEVICES", "").strip()
+            if env == "all":
+                devices = list(range(nat.device_count()))
+            elif env:
+                devices = [int(d) for d in env.split(",")]
+        self.devices = None if devices is None or len(devices) < 2 else [int(d) for d in devices]
         self.solver = None  # KernelSolver of the last solve (kept for inspection)
 
     # ------------------------------------------------------------ helpers
@@ -52,7 +66,11 @@ class Iterative(object):
         otherwise only the matrix-free operator (the reference's K_op) is set up and
         the preconditioner builds fetch their columns through it, as the reference's
         IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory."""
-        s = KernelSolver(n, device=self.device)
+        if self.devices is not None and not dense:
+            s = ShardedKernelSolver(n, self.devices)
+        else:
+            dev = self.device if self.devices is None else self.devices[0]
+            s = KernelSolver(n, device=dev)
         perms = np.atleast_2d(np.asarray(task["perms"]))
         D = R_desc.shape[1]
         if len(tril_perms_lin) != perms.shape[0] * D:
@@ -195,7 +213,7 @@ class Iterative(object):
                 "cg_iterations": res.iters,
                 "gbps_matvec": (8.0 * n * n + 16.0 * n) / (t["gemv_ms"] / t["gemv_count"]) / 1e6
                 if t["gemv_count"] else float("nan"),
-                "n_gpus": 1}
+                "n_gpus": getattr(solver, "world", 1)}
         if info_cholesky is not None:
             info.update(info_cholesky)
         train_rmse = resid / np.sqrt(len(y))
