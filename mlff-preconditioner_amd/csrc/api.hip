@@ -786,7 +786,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
 }
 
 int mlff_shard_range(mlff_ctx *ctx, int64_t *row0_out, int64_t *nrows_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (row0_out) *row0_out = ctx->row0;
   if (nrows_out) *nrows_out = ctx->nrows;
   return MLFF_OK;
@@ -799,7 +799,7 @@ int mlff_matrix_ld(mlff_ctx *ctx, int64_t *ld_out) {
 }
 
 int mlff_synchronize(mlff_ctx *ctx) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
 }
@@ -811,7 +811,7 @@ int mlff_stream(mlff_ctx *ctx, void **stream_out) {
 }
 
 int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (K_local == nullptr && ctx->nrows > 0) return set_error(ctx, MLFF_ERR_ARG, "null K");
   if (ld_host < ctx->N) return set_error(ctx, MLFF_ERR_ARG, "ld_host < N");
   MLFF_TRY(ensure_matrix(ctx));
@@ -833,7 +833,8 @@ int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) 
 }
 
 int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int64_t ld_out) {
-  if (ctx == nullptr || out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  MLFF_ENTER(ctx);
+  if (out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
   if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (r0 < 0 || nr < 0 || r0 + nr > ctx->nrows || ld_out < ctx->N)
     return set_error(ctx, MLFF_ERR_ARG, "row range / ld_out");
@@ -851,7 +852,7 @@ int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int
 }
 
 int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, double jitter) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (X == nullptr || d < 1 || d > 8 || !(length_scale > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "gen_rbf: need X, 1 <= d <= 8, length_scale > 0");
   MLFF_TRY(ensure_matrix(ctx));
@@ -878,7 +879,7 @@ int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, dou
 
 int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: null input or sig <= 0");
   MLFF_TRY(ensure_matrix(ctx));
@@ -893,7 +894,7 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
 
 int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "sgdml_operator: null input or sig <= 0");
   MLFF_TRY(mf_setup(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
@@ -913,7 +914,7 @@ int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_de
 }
 
 int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!(lam > 0.0)) return set_error(ctx, MLFF_ERR_ARG, "lam must be > 0");
   if (sigma_K != 1.0 && sigma_K != -1.0) return set_error(ctx, MLFF_ERR_ARG, "sigma_K must be +-1");
   ctx->sigma_K = sigma_K;
@@ -923,7 +924,7 @@ int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
 }
 
 int mlff_set_storage(mlff_ctx *ctx, int mode) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (mode != MLFF_STORAGE_DENSE && mode != MLFF_STORAGE_SYMTILE && mode != MLFF_STORAGE_AUTO &&
       mode != MLFF_STORAGE_MATFREE)
     return set_error(ctx, MLFF_ERR_ARG, "bad storage mode");
@@ -937,7 +938,7 @@ int mlff_set_storage(mlff_ctx *ctx, int mode) {
 }
 
 int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   MLFF_TRY(resolve_storage(ctx));
   if (mode_out)
@@ -948,7 +949,7 @@ int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out
 }
 
 int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (v_global == nullptr || (y_local == nullptr && ctx->nrows > 0)) return set_error(ctx, MLFF_ERR_ARG, "null vector");
   MLFF_TRY(resolve_storage(ctx));
@@ -962,7 +963,7 @@ int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
 }
 
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   MLFF_TRY(operator_diag(ctx, ctx->dwork));
   if (ctx->nrows > 0)
@@ -972,7 +973,7 @@ int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
 }
 
 int mlff_precon_none(mlff_ctx *ctx) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   ctx->precon_kind = MLFF_PRECON_NONE;
   ctx->k = 0;
   return MLFF_OK;
@@ -980,7 +981,7 @@ int mlff_precon_none(mlff_ctx *ctx) {
 
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (k < 1 || k > ctx->N || k > 16384)
     return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 16384)");
@@ -1005,7 +1006,7 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
 
 int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant,
                         double *seconds_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (variant != 0 && variant != 1) return set_error(ctx, MLFF_ERR_ARG, "variant must be 0 or 1");
   MLFF_TRY(check_idx(ctx, idx, k));
@@ -1022,7 +1023,7 @@ int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int varian
 }
 
 int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (k < 1 || k > ctx->N || (Lt_local == nullptr && ctx->nrows > 0))
     return set_error(ctx, MLFF_ERR_ARG, "lowrank: bad factor");
@@ -1041,7 +1042,7 @@ int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
 
 int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
                     double *evals_out, double *rowlev_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_matrix(ctx));
   if (ctx->world != 1) return set_error(ctx, MLFF_ERR_ARG, "eigen preconditioner needs a single rank");
   if (k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "eig: need 1 <= k <= N");
@@ -1060,14 +1061,14 @@ int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int 
 }
 
 int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (kind_out) *kind_out = ctx->precon_kind;
   if (k_out) *k_out = ctx->k;
   return MLFF_OK;
 }
 
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   hipStream_t s = ctx->stream;
   double *rd = nullptr, *zd = nullptr;
@@ -1095,7 +1096,7 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
 }
 
 int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (ctx->T == nullptr || ctx->k < 1) return set_error(ctx, MLFF_ERR_STATE, "no low-rank panel");
   if (T_local == nullptr || ld_out < ctx->nrows) return set_error(ctx, MLFF_ERR_ARG, "bad output");
   if (ctx->nrows > 0)
@@ -1106,7 +1107,7 @@ int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
 }
 
 int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (!(lam > 0.0) || scores_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "lev_scores: bad args");
   MLFF_TRY(check_idx(ctx, idx, k));
@@ -1136,7 +1137,7 @@ int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, do
 
 int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local, double tol,
                    int64_t maxiter, int *early_exit_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if ((b_local == nullptr && ctx->nrows > 0) || maxiter < 1 || !(tol >= 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "pcg_start: need b, maxiter >= 1, tol >= 0");
@@ -1205,7 +1206,7 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
 }
 
 int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
   if (n_iter < 0) return set_error(ctx, MLFF_ERR_ARG, "n_iter < 0");
   if (chunk <= 0) chunk = 32;
@@ -1260,7 +1261,7 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
 
 int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *resid_out,
                     int *info_out) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
   MLFF_TRY(poll_state(ctx));
   const DevState &h = *ctx->h_st;
@@ -1272,7 +1273,7 @@ int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *
 }
 
 int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (ctx->nrows > 0) {
     if (x_local == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null x");
     MLFF_HIP(ctx, hipMemcpyAsync(x_local, ctx->x, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
@@ -1282,7 +1283,7 @@ int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local) {
 }
 
 int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (!ctx->pcg_active || ctx->trace == nullptr) return set_error(ctx, MLFF_ERR_STATE, "no solve");
   if (trace_out == nullptr || n < 0) return set_error(ctx, MLFF_ERR_ARG, "bad output");
   MLFF_TRY(poll_state(ctx));
@@ -1294,7 +1295,7 @@ int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n) {
 }
 
 int mlff_timing_enable(mlff_ctx *ctx, int on) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   ctx->timing.on = on != 0;
   if (ctx->timing.on && ctx->timing.ev.size() < kTimingPool) ctx->timing.ev.reserve(kTimingPool);
   return MLFF_OK;
@@ -1302,7 +1303,7 @@ int mlff_timing_enable(mlff_ctx *ctx, int on) {
 
 int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double *iter_ms,
                      int64_t *iter_count) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   if (gemv_ms) *gemv_ms = ctx->timing.gemv_ms;
   if (gemv_count) *gemv_count = ctx->timing.gemv_count;
   if (iter_ms) *iter_ms = ctx->timing.iter_ms;
@@ -1311,7 +1312,7 @@ int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double
 }
 
 int mlff_timing_reset(mlff_ctx *ctx) {
-  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  MLFF_ENTER(ctx);
   ctx->timing.gemv_ms = 0.0;
   ctx->timing.gemv_count = 0;
   ctx->timing.iter_ms = 0.0;

@@ -185,6 +185,13 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
     ncclResult_t e__ = (call);                                \
     if (e__ != ncclSuccess) return mlff::nccl_check(ctx, e__, #call); \
   } while (0)
+// every ABI entry point with a context: null check, then make the context's device
+// current on the calling thread (one thread may drive contexts on several devices)
+#define MLFF_ENTER(ctx)                                                        \
+  do {                                                                         \
+    if ((ctx) == nullptr) return mlff::set_error(nullptr, MLFF_ERR_ARG, "null ctx"); \
+    (void)hipSetDevice((ctx)->device);                                         \
+  } while (0)
 #define MLFF_TRY(x)             \
   do {                          \
     int rc__ = (x);             \
