@@ -141,6 +141,15 @@ int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_de
 /* operator A = sigma_K * K + lam * I.  sGDML: sigma_K = -1 (K is negative
  * semidefinite, the solved system is (-K + lam I) x = y, iterative_solver.py:995);
  * RBF: sigma_K = +1. */
+/* Training-set energies of an sGDML model with coefficients `alphas` (N, global,
+ * contiguous): E_out[i - i0] for the training points [i0, i0 + ni) this rank's rows
+ * touch (E_out holds M entries).  This is GDMLPredict's E before the std scale and the
+ * integration constant (predict.py:172-220, 1100-1108), the quantity
+ * GDMLTrain._recov_int_const regresses on (train.py:972-1119).  Needs the
+ * matrix-free operator data (mlff_sgdml_operator or mlff_assemble_sgdml). */
+int mlff_sgdml_energies(mlff_ctx *ctx, const double *alphas, double *E_out, int64_t *i0_out,
+                        int64_t *ni_out);
+
 int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam);
 /* y_local = A v_global (v_global has N entries).  Collective over the ranks
  * when the symmetric tiled storage is in use (a reduce-scatter of the partial

@@ -913,6 +913,25 @@ int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_de
   return MLFF_OK;
 }
 
+int mlff_sgdml_energies(mlff_ctx *ctx, const double *alphas, double *E_out, int64_t *i0_out,
+                        int64_t *ni_out) {
+  MLFF_ENTER(ctx);
+  if (alphas == nullptr || E_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  if (!ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no sGDML operator set");
+  const MfData &mf = ctx->mf;
+  const int64_t MP = mf.M * mf.n_perms;
+  std::vector<double> pairs((size_t)std::max<int64_t>(mf.ni, 1) * MP);
+  MLFF_TRY(mf_energies(ctx, alphas, pairs.data()));
+  for (int64_t i = 0; i < mf.ni; ++i) {
+    double e = 0.0;
+    for (int64_t jp = 0; jp < MP; ++jp) e += pairs[(size_t)i * MP + jp];
+    E_out[i] = e;
+  }
+  if (i0_out) *i0_out = mf.i0;
+  if (ni_out) *ni_out = mf.ni;
+  return MLFF_OK;
+}
+
 int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
   MLFF_ENTER(ctx);
   if (!(lam > 0.0)) return set_error(ctx, MLFF_ERR_ARG, "lam must be > 0");

@@ -329,6 +329,8 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
                         const double *x_loc, const int *status, double sigma, double lam);
 int mf_diag(mlff_ctx *ctx, double *out);
+// training-set energy pair terms for coefficients alphas (N, contiguous): ni x M n_perms
+int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host);
 // diag(sigma K) of this rank's rows: dense rows or the matrix-free sGDML data
 int operator_diag(mlff_ctx *ctx, double *out);
 int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, int n,

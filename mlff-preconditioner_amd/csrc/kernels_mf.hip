@@ -27,6 +27,8 @@
 //   k_mf_jt    y rows of this rank = J_i^T F_i, epilogue sigma y + lam x
 #include "common.h"
 
+#include <algorithm>
+
 namespace mlff {
 
 namespace {
@@ -132,8 +134,8 @@ __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
   if (il < ni && jp < MP) part[((int64_t)blockIdx.z * ni + il) * MP + jp] = acc;
 }
 
-// MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot.  One wave per
-// output: lanes stride over the nz slices, fixed-order wave sum.
+// MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot; MODE 2 (energies):
+// w * dot.  One wave per output: lanes stride over the nz slices, fixed-order wave sum.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ part, int nz,
                                                      int64_t nout, double sig,
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
                                                      double *__restrict__ out0,
                                                      double *__restrict__ out1,
                                                      const int *__restrict__ status) {
-  if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
+  if (MODE >= 1 && status != nullptr && *status != ST_RUNNING) return;
   const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (o >= nout) return;
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
     out0[o] = 5.0 * m;
     out1[o] = (sig * sig + sig * norm) * m;
   } else {
-    out0[o] = m5[o] * s;
+    out0[o] = m5[o] * s;  // MODE 2: m5 holds w
   }
 }
 
@@ -455,6 +457,38 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                      mf.ypart, status);
   hipLaunchKernelGGL(k_mf_jt_fin, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s,
                      mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, status);
+}
+
+// Training-set energies of the model with coefficients `alphas` (contiguous global
+// vector, N), as GDMLPredict predicts them (predict.py:172-220, E_F[0] before the std
+// scale, flipped sign as in the reference): E_i = sum_jp (Rd_i - Rt[jp]) . Zt[jp] w_ijp
+// with Zt = J alphas.  Points [mf.i0, mf.i0 + mf.ni) of this rank; per-pair products in
+// E_pairs (ni x M n_perms, host), summed by the caller in pair order.
+int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host) {
+  MfData &mf = ctx->mf;
+  hipStream_t s = ctx->stream;
+  const int64_t MP = mf.M * mf.n_perms;
+  double *da = nullptr;
+  MLFF_HIP(ctx, hipMalloc(&da, sizeof(double) * ctx->N));
+  MLFF_HIP(ctx, hipMemcpyAsync(da, alphas, sizeof(double) * ctx->N, hipMemcpyHostToDevice, s));
+  const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
+                     mf.M, mf.n, mf.n_perms, mf.D, da, mf.Zt, (const int *)nullptr);
+  if (mf.ni > 0) {
+    hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)((MP + kPT - 1) / kPT),
+                       (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
+                       mf.Rd, mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part,
+                       (const int *)nullptr);
+    hipLaunchKernelGGL(k_mf_pair_fin<2>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
+                       mf.part, mf.nz, mf.ni * MP, mf.sig, mf.w, mf.c, (double *)nullptr,
+                       (const int *)nullptr);
+    MLFF_HIP(ctx, hipMemcpyAsync(E_pairs_host, mf.c, sizeof(double) * mf.ni * MP,
+                                 hipMemcpyDeviceToHost, s));
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  hipFree(da);
+  return MLFF_OK;
 }
 
 // diag(sigma K) of this rank's rows (assembly kernels on the diagonal blocks only)

@@ -154,6 +154,17 @@ class ShardedKernelSolver:
     def lev_scores(self, idx, lam):
         return self._each("lev_scores", idx, lam)[0]  # global scores on every rank
 
+    def sgdml_energies(self, alphas):
+        """(0, E) over all M training points: each point from the first rank that holds
+        rows of it (a point split across two ranks is computed by both)."""
+        alphas = np.ascontiguousarray(alphas, dtype=np.float64)
+        parts = self._each("sgdml_energies", alphas)
+        M = max(i0 + e.size for i0, e in parts)
+        E = np.full(M, np.nan)
+        for i0, e in reversed(parts):
+            E[i0:i0 + e.size] = e
+        return 0, E
+
     def timing(self, on=True):
         self._each("timing", on)
 

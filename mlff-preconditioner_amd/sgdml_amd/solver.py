@@ -133,6 +133,19 @@ class KernelSolver:
         self._call("mlff_assemble_sgdml", nat.dptr(R_desc), nat.dptr(R_d_desc), int(M),
                    int(n_atoms), nat.i32ptr(perms), int(perms.shape[0]), float(sig))
 
+    def sgdml_energies(self, alphas: np.ndarray) -> tuple[int, np.ndarray]:
+        """Training-set energies (GDMLPredict's E before std scale and constant) of the
+        model with coefficients `alphas` (global N-vector): (i0, E[i0 : i0 + ni]) for the
+        training points this rank's rows touch (all M on one rank)."""
+        alphas = np.ascontiguousarray(alphas, dtype=np.float64)
+        if alphas.shape != (self.n,):
+            raise ValueError("alphas must have N entries")
+        E = np.empty(self.n)  # >= M entries
+        i0, ni = ctypes.c_int64(), ctypes.c_int64()
+        self._call("mlff_sgdml_energies", nat.dptr(alphas), nat.dptr(E), ctypes.byref(i0),
+                   ctypes.byref(ni))
+        return i0.value, E[: ni.value].copy()
+
     def set_operator(self, sigma_K: float, lam: float):
         self._call("mlff_set_operator", float(sigma_K), float(lam))
 

@@ -37,6 +37,24 @@ def ethanol_like(M: int, seed: int = 0, scale: float = 0.08):
     return {"R": R, "z": ETHANOL_Z.copy(), "F": F, "E": E}
 
 
+def ethanol_harmonic(M: int, seed: int = 0, scale: float = 0.08, k: float = 1.0):
+    """ethanol_like geometries with CONSISTENT labels: E = k/2 sum_{a<b} (r_ab - r0_ab)^2
+    over all atom pairs (r0 = the frame), F = -grad E.  The reference's integration-
+    constant recovery (train.py:972-1119) needs energies that the forces integrate to."""
+    rng = np.random.default_rng(seed)
+    R = _ETHANOL_FRAME[None, :, :] + scale * rng.standard_normal((M, 9, 3))
+    a, b = np.triu_indices(9, k=1)
+    r0 = np.linalg.norm(_ETHANOL_FRAME[a] - _ETHANOL_FRAME[b], axis=1)
+    d = R[:, a, :] - R[:, b, :]                    # M x P x 3
+    r = np.linalg.norm(d, axis=2)
+    E = 0.5 * k * np.sum((r - r0) ** 2, axis=1)
+    g = (k * (r - r0) / r)[:, :, None] * d          # dE/dR_a for each pair
+    F = np.zeros_like(R)
+    np.add.at(F, (slice(None), a), -g)
+    np.add.at(F, (slice(None), b), g)
+    return {"R": R, "z": ETHANOL_Z.copy(), "F": F, "E": E}
+
+
 def nanotube_frame():
     ring_n, rings, radius, length = 15, 20, 6.0, 30.0
     pts = []

@@ -117,3 +117,27 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
         np.add.at(yi, s_at, -contrib)
         y[i] = yi
     return y.reshape(-1)
+
+
+def energies_matrix_free(R_desc, R_d_desc, perms, sig, alphas):
+    """Training-set energies of the model with coefficients alphas, E_F[0] of
+    GDMLPredict's _predict_wkr (predict.py:172-220) before the std scale and the
+    integration constant: E_i = sum_jp a_ijp (sig + norm) exp(-norm/sig) 5/(3 sig^3),
+    a_ijp = (Rd_i - Rd_j[P_p]) . (J_j alpha_j)[P_p], norm = sqrt5 |Rd_i - Rd_j[P_p]|."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    perms = np.atleast_2d(perms)
+    P = np.array([desc_perm(p) for p in perms])
+    s_at, t_at = np.tril_indices(n, k=-1)
+    A = np.asarray(alphas, dtype=np.float64).reshape(M, n, 3)
+    z = np.einsum("mdc,mdc->md", R_d_desc, A[:, t_at, :] - A[:, s_at, :])
+    Rt, Zt = R_desc[:, P], z[:, P]
+    E = np.empty(M)
+    for i in range(M):
+        diff = R_desc[i][None, None, :] - Rt
+        norm = np.sqrt(5.0) * np.linalg.norm(diff, axis=2)
+        base = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 3) * (norm + sig)
+        a = np.einsum("jpd,jpd->jp", diff, Zt)
+        E[i] = np.sum(a * base)
+    return E

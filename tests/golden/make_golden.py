@@ -414,7 +414,47 @@ def fx_lev_scores():
          lam=np.float64(1e-10))
 
 
+def fx_model():
+    """GDMLTrain.train end to end for solver 'cg' (train.py:707-970: label normalisation,
+    lam = 1e-10, Iterative.solve, create_model :597-702, model.update(info),
+    _recov_int_const :972-1119) on harmonic-labelled ethanol geometries (energies the
+    forces integrate to), plus the reference's training-set energy prediction with c = 0
+    (GDMLPredict.predict, predict.py:997-1110) that the constant is regressed on."""
+    from sgdml.predict import GDMLPredict
+
+    M = 23
+    ds = synthetic.ethanol_harmonic(M, seed=13)
+    task = make_task(ds)
+    desc, tpl, R_desc, R_d_desc, y, y_std = prepare(task)
+    n = y.size
+    m, kmin, _ = plot_data.get_params("ethanol")
+    k_rot = int(plot_data.rule_of_thumb(n=n, k_min=kmin, m=m))
+    np.random.seed(2024)
+    model = gdml_train().train(task, callback=noop, break_percentage=k_rot / n,
+                               str_preconditioner="cholesky")
+    gdml = GDMLPredict(dict(model, c=0.0), max_processes=1)
+    E_pred, F_pred = gdml.predict(task["R_train"].reshape(M, -1), R_desc=R_desc, R_d_desc=R_d_desc)
+    out = {"R": ds["R"], "F": ds["F"], "E": ds["E"], "z": ds["z"], "perms": task["perms"],
+           "k_rot": np.int64(k_rot), "E_pred_c0": np.asarray(E_pred), "F_pred_c0": np.asarray(F_pred),
+           "model_keys": np.array(sorted(model.keys()))}
+    for key, val in model.items():
+        if isinstance(val, dict) or val is None:
+            continue
+        if isinstance(val, (str, np.str_)):
+            out[f"model__{key}"] = np.array(str(val))
+        elif isinstance(val, tuple):
+            out[f"model__{key}"] = np.asarray(val)
+        else:
+            a = np.asarray(val)
+            if a.dtype == object:
+                continue
+            out[f"model__{key}"] = a
+    print(f"  model: use_E={model['use_E']} c={model.get('c')} iters={model['solver_iters']}", flush=True)
+    save("sgdml_model_ethanol_n621", **out)
+
+
 FIXTURES = {
+    "model": fx_model,
     "descriptors": fx_descriptors,
     "rule_of_thumb": fx_rule_of_thumb,
     "rbf": fx_rbf,

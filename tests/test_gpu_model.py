@@ -1,0 +1,74 @@
+"""GPU training entry point (sgdml_amd.model.train = GDMLTrain.train for solver 'cg')
+against the reference's own model (tests/golden/sgdml_model_ethanol_n621: its
+GDMLTrain.train on harmonic-labelled ethanol, cholesky preconditioner, rule-of-thumb
+rank).  This system (forces that integrate exactly, lambda = 1e-10, tol 1e-4) leaves
+large, prediction-neutral freedom in the coefficients: the CPU oracle's own solve (same
+pivots, 260 vs 262 iterations) differs from the reference's by 4.2e-4 in alphas and
+1.3e-5 in the integration constant.  Criteria, at ~5-10x that noise floor: iterations
+within 10 %, ||d alpha|| / ||alpha|| <= 5e-3, constant within 1e-4 relative, identical
+keys / flags / pivots; energies for given coefficients to 1e-12 relative."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fx(golden_dir):
+    return np.load(golden_dir / "sgdml_model_ethanol_n621.npz", allow_pickle=False)
+
+
+def task_of(f):
+    M = f["R"].shape[0]
+    return {"type": "t", "dataset_name": f["model__dataset_name"],
+            "dataset_theory": f["model__dataset_theory"], "z": f["z"], "R_train": f["R"],
+            "F_train": f["F"], "E_train": f["E"], "idxs_train": np.arange(M), "md5_train": "0",
+            "idxs_valid": np.arange(0), "md5_valid": "0", "sig": 10, "lam": 1e-15,
+            "use_E": True, "use_E_cstr": False, "use_sym": False, "use_cprsn": False,
+            "solver_name": "cg", "solver_tol": 1e-4, "n_inducing_pts_init": 25,
+            "interact_cut_off": None, "perms": f["perms"], "truncated_cholesky": 1500}
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0, 0]])
+def test_gpu_energies(fx, devices):
+    import sgdml_amd
+
+    R_desc, R_d_desc = sgdml_amd.sgdml_descriptors(fx["R"])
+    n = fx["model__alphas_F"].size
+    s = (sgdml_amd.KernelSolver(n, device=0) if devices is None
+         else sgdml_amd.ShardedKernelSolver(n, devices))
+    try:
+        s.sgdml_operator(R_desc, R_d_desc, fx["perms"], 10.0)
+        i0, E = s.sgdml_energies(fx["model__alphas_F"])
+    finally:
+        s.close()
+    assert i0 == 0 and E.size == fx["R"].shape[0]
+    np.testing.assert_allclose(E * float(fx["model__std"]), fx["E_pred_c0"], rtol=1e-12)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_train_matches_reference_model(fx, devices, tmp_path):
+    from sgdml_amd import model as mdl
+
+    f = fx
+    n = f["model__alphas_F"].size
+    bp = int(f["k_rot"]) / n
+    m = mdl.train(task_of(f), break_percentage=bp, str_preconditioner="cholesky",
+                  devices=devices)
+    assert set(f["model_keys"]) <= set(m)
+    assert m["use_E"] == bool(f["model__use_E"])
+    np.testing.assert_array_equal(m["index_columns"], f["model__index_columns"])
+    # the model keeps no residual curve: iteration count and coefficients
+    ni, ni_ref = int(m["solver_iters"]), int(f["model__solver_iters"])
+    assert abs(ni - ni_ref) <= max(3, 0.1 * ni_ref), (ni, ni_ref)
+    a, a_ref = m["alphas_F"], f["model__alphas_F"]
+    assert np.linalg.norm(a - a_ref) <= 5e-3 * np.linalg.norm(a_ref)
+    np.testing.assert_allclose(m["R_d_desc_alpha"], f["model__R_d_desc_alpha"], rtol=0,
+                               atol=5e-3 * np.abs(f["model__R_d_desc_alpha"]).max())
+    assert abs(m["c"] - float(f["model__c"])) <= 1e-4 * abs(float(f["model__c"]))
+    assert m["std"] == float(f["model__std"])
+    np.testing.assert_array_equal(m["tril_perms_lin"], f["model__tril_perms_lin"])
+    m.update(hardware="mi355x", n_datapoints=int(f["R"].shape[0]), str_preconditioner="cholesky")
+    out = mdl.store_model(m, tmp_path)
+    back = np.load(out, allow_pickle=True)
+    np.testing.assert_array_equal(back["alphas_F"], m["alphas_F"])
