@@ -131,6 +131,12 @@ def recov_int_const(E_pred: np.ndarray, E_ref: np.ndarray):
     return np.sum(E_ref - E_pred) / E_ref.shape[0]
 
 
+class _ModelFactory:
+    """Stands in for GDMLTrain where the solver's checkpoint needs create_model."""
+
+    create_model = staticmethod(create_model)
+
+
 def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
           break_percentage=0.1, n_columns=None, str_preconditioner="", flag_eigvals=False,
           device=None, devices=None, gdml_train=None):
@@ -156,7 +162,9 @@ def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
         break_percentage = n_columns / len(y)
     assert 0 <= break_percentage <= 1, "break_percentage is too large"
     task["lam"] = 1e-10                                   # train.py:866
-    it = Iterative(gdml_train, None, callback=callback, device=device, devices=devices)
+    # the 2-minute progress checkpoint of the solver builds its model with create_model
+    it = Iterative(gdml_train or _ModelFactory(), None, callback=callback, device=device,
+                   devices=devices)
     alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info = it.solve(
         task, R_desc, R_d_desc, tpl, y, y_std, save_progr_callback=save_progr_callback,
         break_percentage=break_percentage, str_preconditioner=str_preconditioner,
@@ -173,6 +181,37 @@ def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
         else:
             model["c"] = c
     it.solver.close()
+    return model
+
+
+def train_model(task, name_dataset: str, n_datapoints: int, preconditioner: str,
+                hardware: str = "mi355x", devices=None) -> dict:
+    """The solve part of src/train_models.py:train_model (:68-124) for a task the caller
+    built (dataset download and GDMLTrain.create_task stay with the reference):
+    rule-of-thumb preconditioner size (:95-97), train, and the bookkeeping keys
+    store_model and the analysis scripts read (:104-113)."""
+    import timeit
+
+    from .rule_of_thumb import get_params, rule_of_thumb
+
+    task = dict(task)
+    task["truncated_cholesky"] = 1500
+    task["str_preconditioner"] = preconditioner
+    n = task["F_train"].size
+    m, k_min, _ = get_params(name_dataset)
+    k_rot = int(rule_of_thumb(n=n, k_min=k_min, m=m))
+    strength = k_rot / n
+    t0 = timeit.default_timer()
+    model = train(task, break_percentage=strength, str_preconditioner=preconditioner,
+                  devices=devices)
+    model["solver_runtime_s"] = timeit.default_timer() - t0
+    model["truncated_cholesky"] = 1500
+    model["str_preconditioner"] = preconditioner
+    model["n_datapoints"] = n_datapoints
+    model["kernel_size"] = n
+    model["preconditioner_strength"] = strength
+    model["task"] = task
+    model["hardware"] = hardware
     return model
 
 

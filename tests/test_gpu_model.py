@@ -72,3 +72,18 @@ def test_train_matches_reference_model(fx, devices, tmp_path):
     out = mdl.store_model(m, tmp_path)
     back = np.load(out, allow_pickle=True)
     np.testing.assert_array_equal(back["alphas_F"], m["alphas_F"])
+
+
+def test_train_model_entry_point(fx, tmp_path):
+    """train_models.train_model's solve part + store_model: the file lands where the
+    reference's analysis scripts look for it."""
+    from sgdml_amd import model as mdl
+    from sgdml_amd.rule_of_thumb import get_params, rule_of_thumb
+
+    m = mdl.train_model(task_of(fx), "ethanol", 23, "cholesky")
+    n = fx["model__alphas_F"].size
+    mm, kmin, _ = get_params("ethanol")
+    assert m["preconditioner_strength"] == int(rule_of_thumb(n=n, k_min=kmin, m=mm)) / n
+    assert m["kernel_size"] == n and m["hardware"] == "mi355x" and m["use_E"]
+    out = mdl.store_model(m, tmp_path)
+    assert out.parent == tmp_path / "data_new/models/mi355x/ethanol/cholesky/n=23/k=132"
