@@ -120,3 +120,24 @@ def test_symtile_sgdml_assembly(sg):
     assert np.array_equal(K, K.T)
     ref = -(K @ v) + 1e-10 * v
     assert np.max(np.abs(y - ref)) <= 1e-13 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("n", [16384, 23040])
+def test_symtile_quarter_tail_matches_dense(sg, n):
+    """Tile counts past one round of 512 workgroups (528 and 1035 tiles: whole tiles plus
+    quarter-tile workgroups for the remainder) against the dense row GEMV."""
+    from sgdml_amd import synthetic
+
+    X, _ = synthetic.rbf_points(n, 3, 11)
+    v = np.random.default_rng(n).standard_normal(n)
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, 0.2)
+        s.set_operator(1.0, 1e-3)
+        s.set_storage("dense")
+        yd = s.matvec(v)
+        s.set_storage("sym")
+        assert s.storage_info()[0] == "sym"
+        ys = s.matvec(v)
+        ys2 = s.matvec(v)
+    np.testing.assert_array_equal(ys, ys2)  # deterministic
+    assert np.max(np.abs(ys - yd)) <= 1e-13 * np.abs(yd).max()
