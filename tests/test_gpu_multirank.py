@@ -86,7 +86,7 @@ def gather(outs, key):
 @pytest.mark.parametrize("world,precon,storage", [
     (2, "none", "auto"), (3, "none", "auto"), (2, "nystrom", "auto"), (3, "nystrom", "auto"),
     (2, "pivchol", "auto"), (3, "pivchol", "auto"), (2, "none", "dense"),
-    (3, "pivchol", "dense")])
+    (3, "pivchol", "dense"), (8, "nystrom", "auto"), (8, "none", "dense")])
 def test_sharded_solve_matches_single_rank(world, precon, storage):
     """auto = symmetric tiles (reduce-scatter of the partial products), dense = row GEMV."""
     n = 1003
@@ -138,3 +138,42 @@ def test_sharded_sgdml_assembly_rows():
     for world in (2, 4):
         rows = np.concatenate(run_ranks(world, body))
         np.testing.assert_array_equal(rows, ref)
+
+
+@pytest.mark.timeout(900)
+def test_bench_config_eight_ranks():
+    """The bench's 8-GPU configuration (N = 65536 RBF, rank-256 Nystrom, symmetric tiles,
+    8 row blocks of 8192, ~1032 tiles per rank) rehearsed as 8 ranks on one GPU, against
+    the one-rank run.  This system is chaotic under summation order: the one-rank DENSE vs
+    SYMTILE storages themselves drift apart ~10x per 3 iterations (1e-12 at 12, 3e-9 at
+    21, 6e-6 at 27; scripts/dev/diag_ranks.py), and 8 ranks drift the same way.  So: 16
+    iterations, residuals within 1e-7 relative, iterates within 1e-7."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    n, k, lam, ell, iters = 65536, 256, 1e-6, 0.2, 16
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+
+    def body(rank, world, key):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world,
+                                   comm_id=key if world > 1 else None)
+        try:
+            s.gen_rbf(X, ell)
+            s.set_operator(1.0, lam)
+            s.precon_nystrom(idx, variant=0)
+            mode, _ = s.storage_info()
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(b[r0:r1]), tol=0.0, maxiter=iters)
+            return mode, res.trace, res.x
+        finally:
+            s.close()
+
+    ref = run_ranks(1, body)[0]
+    outs = run_ranks(8, body, timeout=800)
+    assert ref[0] == "sym" and all(o[0] == "sym" for o in outs)
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o[1], outs[0][1])
+    np.testing.assert_allclose(outs[0][1], ref[1], rtol=1e-7)
+    x = np.concatenate([o[2] for o in outs])
+    assert np.linalg.norm(x - ref[2]) <= 1e-7 * np.linalg.norm(ref[2])
