@@ -366,6 +366,8 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
       ps[(int64_t)a * (a - 1) / 2 + b] = a;
       pt[(int64_t)a * (a - 1) / 2 + b] = b;
     }
+  if (M * n_perms > 65535 || M > 65535)  // grid y / z extents of the pair and J^T kernels
+    return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: M * n_perms > 65535 is not supported");
   mf.M = M;
   mf.n = n;
   mf.D = D;
