@@ -98,7 +98,8 @@ def load_library(path: str | os.PathLike | None = None):
         import torch  # noqa: F401
     except Exception:
         pass
-    p = Path(path) if path is not None else LIB_PATH
+    # MLFF_LIB: an alternative build of the same library (kernel A/B experiments)
+    p = Path(path) if path is not None else Path(os.environ.get("MLFF_LIB") or LIB_PATH)
     if not p.exists():
         raise ImportError(
             f"libmlffpcg.so not found at {p}: build it with "
