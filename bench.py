@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-1e-6 legs")
     ap.add_argument("--cpu-iters", type=int, default=100,
                     help="PCG iterations of the CPU baseline (~10-20 s of host work at N=65536)")
+    ap.add_argument("--cpu-iters-sgdml", type=int, default=20,
+                    help="PCG iterations of the CPU baseline of the sGDML workloads (~0.45 s each "
+                         "at the nanotube size)")
     ap.add_argument("--cpu-iters-1t", type=int, default=3,
                     help="PCG iterations of the single-thread CPU baseline")
     ap.add_argument("--workload", choices=["rbf", "nanotube", "ethanol"], default="rbf",
@@ -139,13 +142,54 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _time_pcg(mv, psolve, b, m):
+    """Seconds per oracle PCG iteration (after one warm-up iteration) and per mat-vec."""
+    from oracle.pcg import cg_legacy
+
+    cg_legacy(mv, b, tol=0.0, maxiter=1, psolve=psolve)
+    t0 = time.perf_counter()
+    cg_legacy(mv, b, tol=0.0, maxiter=m, psolve=psolve)
+    el = time.perf_counter() - t0
+    # cg_legacy spends one extra mat-vec on the legacy ||A x0 - b|| check
+    t_mv = time.perf_counter()
+    mv(b)
+    t_mv = time.perf_counter() - t_mv
+    return max(el - t_mv, 1e-9) / m, t_mv
+
+
+def cpu_baseline_sgdml(solver, Rd, Rdd, perms, b, lam, iters):
+    """The reference's CPU iteration for the sGDML workloads, restated by the oracle: its
+    matrix-free K_op (GDMLPredict with alphas = v, predict.py:72-234) and the Woodbury
+    apply (iterative_cholesky.py:145-148).  The rank-k panel is the one the GPU built
+    (the oracle's own pivoted Cholesky would need k CPU operator applications, ~0.4 s
+    each at the nanotube size); the timed sample is the per-iteration work only."""
+    import threadpoolctl
+
+    from oracle.precon import apply_panel
+    from oracle.sgdml import kernel_matvec_matrix_free
+
+    T = solver.precon_panel()
+    info = threadpoolctl.threadpool_info()
+    threads = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+
+    def mv(v):
+        return -kernel_matvec_matrix_free(Rd, Rdd, perms, 10.0, v) + lam * v
+
+    per_it, t_mv = _time_pcg(mv, lambda r: apply_panel(T, 1.0, lam, r), b, iters)
+    return {"value": 1.0 / per_it, "unit": "CG iters/s", "cores": int(threads), "kind": "port",
+            "sample": f"{iters} PCG iterations (oracle cg_legacy + matrix-free sGDML K_op + "
+                      f"Woodbury apply of the GPU-built rank-{T.shape[0]} panel, NumPy) at "
+                      f"N={b.size}",
+            "ms_per_iter": per_it * 1e3, "matvec_ms": t_mv * 1e3, "host_cpu": _cpu_model(),
+            "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
     """Oracle PCG iterations (NumPy/SciPy port of the reference CPU path) on the same
     matrix, copied from the device; timed per iteration after one warm-up iteration,
     with all BLAS threads and (a shorter sample) with one thread."""
     import threadpoolctl
 
-    from oracle.pcg import cg_legacy
     from oracle.precon import apply_panel, nystrom_panel
 
     n = b.size
@@ -159,22 +203,12 @@ def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
         y += lam * v
         return y
 
-    def per_iter(m):
-        cg_legacy(mv, b, tol=0.0, maxiter=1, psolve=lambda r: apply_panel(B, sp, lam, r))
-        t0 = time.perf_counter()
-        cg_legacy(mv, b, tol=0.0, maxiter=m, psolve=lambda r: apply_panel(B, sp, lam, r))
-        el = time.perf_counter() - t0
-        # cg_legacy spends one extra mat-vec on the legacy ||A x0 - b|| check
-        t_mv = time.perf_counter()
-        mv(b)
-        t_mv = time.perf_counter() - t_mv
-        return max(el - t_mv, 1e-9) / m, t_mv
-
-    per_it, t_mv = per_iter(iters)
+    psolve = lambda r: apply_panel(B, sp, lam, r)  # noqa: E731
+    per_it, t_mv = _time_pcg(mv, psolve, b, iters)
     one = None
     if iters_1t > 0:
         with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
-            p1, t1 = per_iter(iters_1t)
+            p1, t1 = _time_pcg(mv, psolve, b, iters_1t)
         one = {"value": 1.0 / p1, "cores": 1, "ms_per_iter": p1 * 1e3,
                "matvec_gbs": (8.0 * n * n) / (t1 * 1e9), "sample": f"{iters_1t} PCG iterations"}
     del K
@@ -244,7 +278,8 @@ def sgdml_workload(args, rank, world, local, pg):
     _, t_chol = solver.precon_pivchol(k)
     return solver, n, k, y, {"operator_setup_s": t_asm, "pivchol_build_s": t_chol,
                              "workload": f"sgdml_{name}_n{n}_pivchol{k}", "M": M,
-                             "n_atoms": n_atoms}
+                             "n_atoms": n_atoms, "desc": (Rd, Rdd),
+                             "perms": np.arange(n_atoms)[None, :]}
 
 
 def main():
@@ -271,7 +306,6 @@ def main():
         solver, n, k, b, sg_info = sgdml_workload(args, rank, world, local, pg)
         workload, lam = sg_info["workload"], 1e-10
         t_gen, t_pre = sg_info["operator_setup_s"], sg_info["pivchol_build_s"]
-        args.no_cpu = True
     solver.set_storage(args.storage)
     t0 = time.perf_counter()
     storage, op_bytes = solver.storage_info()  # builds the symmetric tiles (setup)
@@ -314,7 +348,12 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
-                cpu = cpu_baseline(solver, X, b, idx, lam, ell, args.cpu_iters, args.cpu_iters_1t)
+                if sg_info is None:
+                    cpu = cpu_baseline(solver, X, b, idx, lam, ell, args.cpu_iters,
+                                       args.cpu_iters_1t)
+                else:
+                    cpu = cpu_baseline_sgdml(solver, *sg_info["desc"], sg_info["perms"], b, lam,
+                                             args.cpu_iters_sgdml)
             except Exception as e:  # a baseline failure must not hide the GPU number
                 cpu = {"value": None, "error": repr(e)}
         par = None

@@ -14,6 +14,12 @@
  *       src/sGDML/sgdml/solvers/iterative_solver.py:383-445          -> mlff_set_operator + mlff_matvec
  *   GDMLTrain._assemble_kernel_mat (+ worker)
  *       src/sGDML/sgdml/train.py:81-236, 1121-1308                   -> mlff_assemble_sgdml
+ *   K_op as the reference evaluates it (GDMLPredict, alphas = v)
+ *       src/sGDML/sgdml/predict.py:72-234, 400-449                   -> mlff_sgdml_operator
+ *   Desc.from_R (descriptors + compact Jacobians)
+ *       src/sGDML/sgdml/utils/desc.py:292-358                        -> mlff_sgdml_descriptors
+ *   GDMLPredict energies on the training set (for _recov_int_const)
+ *       src/sGDML/sgdml/predict.py:172-220; train.py:972-1119        -> mlff_sgdml_energies
  *   tools.utils.create_kernel_mat (synthetic RBF)
  *       src/tools/utils.py:173-187                                   -> mlff_gen_rbf
  *   set dense K from the caller (K_hat in custom_cg_solver)
