@@ -59,6 +59,8 @@ struct SymPack {
   double *Pq = nullptr;
   unsigned char *split = nullptr;  // nb x nb: tile (I, J) is split
   int64_t t_split = 0;             // smallest I of a split tile (nb if none)
+  int64_t dyn = 0;                 // > 0: k_symv_dyn with this many workgroups
+  unsigned long long *ticket = nullptr;  // its work counter (reset by the slot reduction)
   double *yg = nullptr;      // world > 1: this rank's partial y, rank blocks of ystride
   double *yr = nullptr;      // world > 1: reduce-scatter result (ystride)
   int64_t ystride = 0;       // blk + tail (p.q shares of every rank)

@@ -26,6 +26,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 namespace mlff {
 
@@ -154,6 +156,164 @@ __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ t
     tile_body<false>(A, t.x, t.y, v, P, Pc, Np, gb0, gb1, sh);
 }
 
+// Dynamic persistent schedule with cross-tile prefetch: C resident workgroups take work
+// units (whole tiles, then the quarter units of the tail) from a ticket counter; before
+// finishing a tile (LDS combine + slot stores) a workgroup already has the first batch
+// of its next unit and the next p segment in flight, so the HBM stream of a workgroup
+// slot does not stop at tile boundaries.  The counter is reset by the slot reduction.
+__device__ __forceinline__ void decode_unit(long long u, int nwhole, int &tile, int &h, int &gb0,
+                                            int &gb1) {
+  if (u < nwhole) {
+    tile = (int)u;
+    h = 0;
+    gb0 = 0;
+    gb1 = kBatches;
+  } else {
+    const long long q = u - nwhole;
+    tile = nwhole + (int)(q >> 2);
+    h = (int)(q & 3);
+    gb0 = h * (kBatches / 4);
+    gb1 = gb0 + kBatches / 4;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ tiles,
+                                                  const int2 *__restrict__ list,
+                                                  const double *__restrict__ v,
+                                                  double *__restrict__ P,
+                                                  double *__restrict__ Pq, int64_t Np,
+                                                  int nwhole, long long nunits, int nb,
+                                                  unsigned long long *__restrict__ ticket,
+                                                  const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[6 * B + 4 * kRB * 64];
+  __shared__ long long s_next;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double *vrow = sh, *rows = sh + B, *cs = sh + 2 * B;
+  double *red = sh + 6 * B + w * kRB * 64;
+  // first unit = blockIdx.x (no atomic burst at launch: one counter word serves ~90
+  // grabs per us); later grabs come from the counter, offset by the grid
+  const long long G = gridDim.x;
+  long long u = blockIdx.x;
+  if (u >= nunits) return;
+  int tile, h, gb0, gb1;
+  decode_unit(u, nwhole, tile, h, gb0, gb1);
+  int2 t = list[tile];
+  const double *A = tiles + (int64_t)tile * B * B;
+  d2 pc[4], a[kRB][4];
+  {
+    const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)t.y * B);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+    const d2 *rowp = reinterpret_cast<const d2 *>(A + (int64_t)(gb0 + w) * kRB * B) + lane;
+#pragma unroll
+    for (int rr = 0; rr < kRB; ++rr)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+  }
+  if (threadIdx.x == 0) s_next = G + (long long)atomicAdd(ticket, 1ull);
+  for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256)
+    vrow[gb0 * kRB + i] = v[(int64_t)t.x * B + gb0 * kRB + i];
+  __syncthreads();
+  while (true) {
+    const bool diag = t.x == t.y;
+    d2 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = d2{0.0, 0.0};
+#pragma unroll 1
+    for (int g = gb0 + w; g < gb1; g += 4) {
+      const int rbase = g * kRB;
+      if (g != gb0 + w) {
+        const d2 *rowp = reinterpret_cast<const d2 *>(A + (int64_t)rbase * B) + lane;
+#pragma unroll
+        for (int rr = 0; rr < kRB; ++rr)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+      }
+#pragma unroll
+      for (int rr = 0; rr < kRB; ++rr) {
+        double s0 = a[rr][0].x * pc[0].x;
+        double s1 = a[rr][0].y * pc[0].y;
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          s0 = fma(a[rr][q].x, pc[q].x, s0);
+          s1 = fma(a[rr][q].y, pc[q].y, s1);
+        }
+        red[rr * 64 + lane] = s0 + s1;
+        if (!diag) {
+          const double pr = vrow[rbase + rr];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            acc[q].x = fma(a[rr][q].x, pr, acc[q].x);
+            acc[q].y = fma(a[rr][q].y, pr, acc[q].y);
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const d2 *rp = reinterpret_cast<const d2 *>(red + (lane >> 3) * 64 + (lane & 7) * 8);
+      const d2 t0 = rp[0], t1 = rp[1], t2 = rp[2], t3 = rp[3];
+      double tt = ((t0.x + t0.y) + (t1.x + t1.y)) + ((t2.x + t2.y) + (t3.x + t3.y));
+      tt += __shfl_xor(tt, 1, 64);
+      tt += __shfl_xor(tt, 2, 64);
+      tt += __shfl_xor(tt, 4, 64);
+      if ((lane & 7) == 0) rows[rbase + (lane >> 3)] = tt;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (!diag) {
+      d2 *cs2 = reinterpret_cast<d2 *>(cs);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cs2[w * (B / 2) + lane + 64 * q] = acc[q];
+    }
+    __syncthreads();  // rows / cs complete; s_next visible
+    const long long un = s_next;
+    int tile2 = 0, h2 = 0, gb02 = 0, gb12 = 0;
+    int2 t2 = t;
+    const double *A2 = A;
+    if (un < nunits) {  // next unit: p segment and first batch in flight during the stores
+      decode_unit(un, nwhole, tile2, h2, gb02, gb12);
+      t2 = list[tile2];
+      A2 = tiles + (int64_t)tile2 * B * B;
+      const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)t2.y * B);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+      const d2 *rowp = reinterpret_cast<const d2 *>(A2 + (int64_t)(gb02 + w) * kRB * B) + lane;
+#pragma unroll
+      for (int rr = 0; rr < kRB; ++rr)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
+    }
+    {
+      const int row0 = gb0 * kRB, nr = (gb1 - gb0) * kRB;
+      double *Prow = P + (int64_t)t.y * Np + (int64_t)t.x * B + row0;
+      for (int c = threadIdx.x; c < nr; c += 256) __builtin_nontemporal_store(rows[row0 + c], Prow + c);
+      if (!diag) {
+        double *Pc = h == 0 ? P : Pq + (int64_t)(h - 1) * nb * Np;
+        double *Pcol = Pc + (int64_t)t.x * Np + (int64_t)t.y * B;
+        for (int c = threadIdx.x; c < B; c += 256)
+          __builtin_nontemporal_store((cs[c] + cs[B + c]) + (cs[2 * B + c] + cs[3 * B + c]), Pcol + c);
+      }
+    }
+    __syncthreads();  // LDS consumed, s_next read by everyone
+    if (un >= nunits) break;
+    if (threadIdx.x == 0) s_next = G + (long long)atomicAdd(ticket, 1ull);
+    tile = tile2;
+    h = h2;
+    gb0 = gb02;
+    gb1 = gb12;
+    t = t2;
+    A = A2;
+    for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256)
+      vrow[gb0 * kRB + i] = v[(int64_t)t.x * B + gb0 * kRB + i];
+    __syncthreads();
+  }
+}
+
 // column partials of slot t for rows of block bi: tile (t, bi), t > bi; a split tile
 // adds its quarters 1..3 (planes Pq) to quarter 0 (P) in quarter order
 __device__ __forceinline__ double slot_val(const double *__restrict__ P,
@@ -190,8 +350,10 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
                                                     double sigma, double lam,
                                                     const double *__restrict__ vloc,
                                                     double *__restrict__ pq_part,
+                                                    unsigned long long *__restrict__ ticket,
                                                     const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   double apq = 0.0;
   const int64_t pl = (int64_t)nb * Np;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_out;
@@ -266,8 +428,10 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
                                                       const double *__restrict__ p,
                                                       double *__restrict__ pq_part,
                                                       double *__restrict__ pp_part,
+                                                      unsigned long long *__restrict__ ticket,
                                                       const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   __shared__ double sh[8];
   double apq = 0.0, app = 0.0;
   const int64_t lo = (int64_t)rank * blk, hi = lo + blk;
@@ -402,6 +566,12 @@ void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *
                  hipStream_t s) {
   if (sp.ntiles == 0) return;
   const int64_t grid = sp.nwhole + 4 * (sp.ntiles - sp.nwhole);
+  if (sp.dyn > 0) {
+    hipLaunchKernelGGL(k_symv_dyn, dim3((unsigned)std::min<int64_t>(sp.dyn, grid)), dim3(256), 0, s,
+                       sp.tiles, sp.list, v_full, P, sp.Pq, sp.Np, (int)sp.nwhole, (long long)grid,
+                       (int)sp.nb, sp.ticket, status);
+    return;
+  }
   hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)grid), dim3(256), 0, s, sp.tiles, sp.list, v_full,
                      P, sp.Pq, sp.Np, (int)sp.nwhole, (int)sp.nb, status);
 }
@@ -413,18 +583,18 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
   if (epilogue)
     hipLaunchKernelGGL((k_sym_reduce<true, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
                        (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
-                       (double *)nullptr, status);
+                       (double *)nullptr, sp.ticket, status);
   else
     hipLaunchKernelGGL((k_sym_reduce<false, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
                        (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
-                       (double *)nullptr, status);
+                       (double *)nullptr, sp.ticket, status);
 }
 
 void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
                           const double *p, double *pq_part, const int *status, hipStream_t s) {
   hipLaunchKernelGGL((k_sym_reduce<true, true>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
                      sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, p, pq_part,
-                     status);
+                     sp.ticket, status);
 }
 
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
@@ -436,13 +606,13 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (int)sp.nb, rank,
                        (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
-                       status);
+                       sp.ticket, status);
     return;
   }
   hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                      (int)sp.nb, rank,
                      (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
-                     status);
+                     sp.ticket, status);
   hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
                      rank, world, blk, sp.ystride, sp.yg, status);
 }
@@ -488,6 +658,14 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     cus = 256;
   const int64_t C = 2 * (int64_t)cus;
   const int64_t nwhole = (nt / C) * C;
+  // launch schedule: k_symv_dyn (C resident workgroups taking units from a counter, next
+  // unit prefetched across tile boundaries) -- measured on one MI355X: 2.51 ms at 8256
+  // tiles where one-workgroup-per-unit launches took 2.51-2.61 ms (bimodal across runs),
+  // equal at 528 / 1035 tiles.  MLFF_SYM_SCHED=static selects the one-workgroup-per-unit
+  // launch (k_symv_tiles).
+  int64_t dyn = C;
+  if (const char *e = std::getenv("MLFF_SYM_SCHED"))
+    if (std::strcmp(e, "static") == 0) dyn = 0;
   // (A persistent schedule -- exactly C workgroups streaming equal batch ranges, tiles
   // cut at range boundaries -- measured slower at every size on one MI355X: 2.67 vs
   // 2.61 ms at 8256 tiles, 0.366 vs 0.338 ms at 1035: the hardware dispatcher's dynamic
@@ -503,6 +681,8 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     MLFF_HIP(ctx, hipMalloc(&sp.Pq, sizeof(double) * 3 * (int64_t)nb * Np));
     MLFF_HIP(ctx, hipMemsetAsync(sp.Pq, 0, sizeof(double) * 3 * (int64_t)nb * Np, s));
     MLFF_HIP(ctx, hipMalloc(&sp.split, (size_t)nb * nb));
+    MLFF_HIP(ctx, hipMalloc(&sp.ticket, sizeof(unsigned long long)));
+    MLFF_HIP(ctx, hipMemsetAsync(sp.ticket, 0, sizeof(unsigned long long), s));
     if (ctx->world > 1) {
       // reduce-scatter operand: rank blocks of blk rows + a tail of p.q shares
       sp.ystride = ctx->blk + round_up(ctx->world, kPad);
@@ -518,6 +698,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   sp.nb = nb;
   sp.tiles_per_rank = tpr;
   sp.nwhole = nwhole;
+  sp.dyn = dyn;
   {
     std::vector<unsigned char> split((size_t)nb * nb, 0);
     sp.t_split = nb;
@@ -563,10 +744,11 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
 
 void sym_free(SymPack &sp) {
   for (void *p : {(void *)sp.tiles, (void *)sp.list, (void *)sp.P, (void *)sp.yg, (void *)sp.yr,
-                  (void *)sp.Pq, (void *)sp.split})
+                  (void *)sp.Pq, (void *)sp.split, (void *)sp.ticket})
     if (p) (void)hipFree(p);
   sp.Pq = nullptr;
   sp.split = nullptr;
+  sp.ticket = nullptr;
   sp.tiles = nullptr;
   sp.list = nullptr;
   sp.P = nullptr;
