@@ -386,7 +386,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": pmc_traffic(workload, storage, world),
-                         "kernel": {"sym": "k_symv_tiles + k_sym_reduce (K mat-vec, lower-triangle tiles)",
+                         "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
                                     "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
                                     "matfree": "k_mf_z + k_mf_pair + k_mf_pair_fin + k_mf_h + k_mf_jt "
                                                "(matrix-free sGDML operator)"}.get(storage, storage),
