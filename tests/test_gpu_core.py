@@ -227,3 +227,40 @@ def test_eig_preconditioner_apply(sg, mask):
     U, sv, _ = np.linalg.svd(K)
     np.testing.assert_allclose(ev, sv[:k], rtol=1e-10, atol=1e-12 * sv[0])
     np.testing.assert_allclose(lev, np.linalg.norm(U[:, :k], axis=1), rtol=1e-7, atol=1e-10)
+
+
+@pytest.mark.parametrize("case", ["warm", "early"])
+def test_pcg_x0_legacy_semantics(sg, case):
+    """Initial guess as scipy 1.7.3's cg treats it (iterative_solver.py:995-1005 passes
+    x0 = -alphas0_F): r0 = b - A x0; the legacy pre-check ||A x0 - b|| <= tol returns x0
+    untouched (no iteration, no callback)."""
+    from oracle.pcg import cg_legacy
+    from oracle.precon import apply_panel, pivoted_cholesky, woodbury_panel
+    from oracle.rbf import rbf_kernel
+
+    n, k, lam = 1500, 200, 1e-1
+    X, b = _rbf(n, seed=9)
+    K = rbf_kernel(X, 0.2)
+    A = K + lam * np.eye(n)
+    rng = np.random.default_rng(5)
+    if case == "warm":
+        x0, tol = 0.05 * rng.standard_normal(n), 1e-8
+    else:
+        x0, tol = np.linalg.solve(A, b), 1e-6
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, length_scale=0.2)
+        s.set_operator(1.0, lam)
+        s.precon_pivchol(k)
+        res = s.pcg(b, x0, tol=tol, maxiter=5 * n)
+    L, _ = pivoted_cholesky(lambda i: K[:, i], np.diag(K).copy(), k)
+    T, sp = woodbury_panel(L, lam)
+    x_ref, info, tr, it = cg_legacy(lambda v: A @ v, b, x0=x0, tol=tol, maxiter=5 * n,
+                                    psolve=lambda r: apply_panel(T, sp, lam, r))
+    assert res.info == info == 0
+    if case == "early":
+        assert res.early_exit and res.iters == it == 0 and res.callbacks == 0
+        np.testing.assert_array_equal(res.x, x0)
+        return
+    assert not res.early_exit and res.iters > 0
+    np.testing.assert_allclose(res.trace[0], tr[0], rtol=1e-12)
+    assert_pcg_parity(res.iters, res.trace[1:], res.x, it, tr[1:], x_ref, mode="stable")

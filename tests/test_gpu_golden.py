@@ -289,3 +289,24 @@ def test_dropin_info_dict_schema(sg, golden_dir, tmp_path):
     np.testing.assert_array_equal(back["alphas_F"], alphas)
     np.testing.assert_array_equal(back["index_columns"], info["index_columns"])
     assert tuple(back["L.shape"]) == (n, k)
+
+
+def test_dropin_warm_start(sg, golden_dir):
+    """task['alphas0_F'] / task['solver_iters'] (iterative_solver.py:650-660, 995-1005): the
+    solve restarts from -alphas0_F and the iteration count continues the previous one."""
+    from sgdml_amd.solvers import Iterative
+
+    name = "sgdml_ethanol_n270"
+    f = load(golden_dir, name)
+    n = f["y"].size
+    a_ref = f["cholesky__alphas"]
+    task = dict(task_of(f), alphas0_F=a_ref * (1 + 1e-3 * np.random.default_rng(0).standard_normal(n)),
+                solver_iters=1000)
+    it = Iterative(None, None, device=0)
+    alphas, num_iters, resid, rmse, idxs, is_conv, info = it.solve(
+        task, f["R_desc"], f["R_d_desc"], f["tril_perms_lin"], f["y"], float(f["y_std"]),
+        break_percentage=int(f["k_rot"]) / n, str_preconditioner="cholesky")
+    assert is_conv
+    assert num_iters == 1000 + max(info["cg_iterations"], 1)
+    assert resid <= float(f["solver_tol"]) * np.linalg.norm(f["y"])
+    assert np.linalg.norm(alphas - a_ref) <= 1e-3 * np.linalg.norm(a_ref)

@@ -177,3 +177,36 @@ def test_bench_config_eight_ranks():
     np.testing.assert_allclose(outs[0][1], ref[1], rtol=1e-7)
     x = np.concatenate([o[2] for o in outs])
     assert np.linalg.norm(x - ref[2]) <= 1e-7 * np.linalg.norm(ref[2])
+
+
+@pytest.mark.timeout(300)
+def test_sharded_x0_matches_single_rank():
+    """A warm start sliced over 3 ranks (padded blocks) equals the one-rank solve."""
+    import sgdml_amd
+
+    n = 1003
+    X, b = problem(n)
+    x0 = 0.05 * np.random.default_rng(8).standard_normal(n)
+
+    def body(rank, world, key):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world,
+                                   comm_id=key if world > 1 else None)
+        try:
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, 1e-1)
+            s.precon_pivchol(150)
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(b[r0:r1]), np.ascontiguousarray(x0[r0:r1]), tol=1e-8,
+                        maxiter=5 * n)
+            return res.x, res.iters, res.trace
+        finally:
+            s.close()
+
+    ref = run_ranks(1, body)[0]
+    outs = run_ranks(3, body)
+    assert all(o[1] == outs[0][1] for o in outs)
+    # ||b - A x0|| over the sharded operator (the warm-start residual itself)
+    np.testing.assert_allclose(outs[0][2][0], ref[2][0], rtol=1e-12)
+    x = np.concatenate([o[0] for o in outs])
+    assert_pcg_parity(outs[0][1], outs[0][2][1:], x, ref[1], ref[2][1:], ref[0], mode="chaotic",
+                      x_tol=1e-7)
