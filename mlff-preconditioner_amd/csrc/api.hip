@@ -252,6 +252,7 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
 int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
   double *tmp = nullptr;
   MLFF_HIP(ctx, hipMallocAsync(&tmp, sizeof(double) * k * k, ctx->stream));
+  ScratchFree scratch{ctx->stream, {tmp}};
   MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
   launch_add_diag(tmp, k, -1e-15, ctx->stream);
   int rc = potrf_lower(ctx, tmp, k);
@@ -262,7 +263,6 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
   }
   if (rc == MLFF_OK)
     MLFF_HIP(ctx, hipMemcpyAsync(A, tmp, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
-  MLFF_HIP(ctx, hipFreeAsync(tmp, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return rc;
 }
@@ -272,12 +272,12 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
 int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
   double *G = nullptr;
   MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, ctx->stream));
+  ScratchFree scratch{ctx->stream, {G}};
   MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
   launch_add_diag(G, k, ctx->lam, ctx->stream);
   MLFF_TRY(potrf_lower(ctx, G, k));
   MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));
-  MLFF_HIP(ctx, hipFreeAsync(G, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
 }
@@ -325,6 +325,7 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
   MLFF_HIP(ctx, hipMallocAsync(&didx, sizeof(int64_t) * k, s));
   MLFF_HIP(ctx, hipMallocAsync(&Smm, sizeof(double) * k * k, s));
   MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, s));
+  ScratchFree scratch{s, {didx, Smm, G}};
   MLFF_HIP(ctx, hipMemcpyAsync(didx, idx_host, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
   // K_nm^T (sign convention S = sigma_K K; sign flips cancel in B^T B)
   MLFF_TRY(fetch_cols(ctx, didx, k, W, ctx->blk));
@@ -348,9 +349,6 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
     rc = potrf_lower(ctx, G, k);
   if (rc != MLFF_OK) return rc;
   MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));     // B = V^-T C^T
-  MLFF_HIP(ctx, hipFreeAsync(didx, s));
-  MLFF_HIP(ctx, hipFreeAsync(Smm, s));
-  MLFF_HIP(ctx, hipFreeAsync(G, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
 }

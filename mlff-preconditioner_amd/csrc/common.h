@@ -200,6 +200,16 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
     if (rc__ != MLFF_OK) return rc__; \
   } while (0)
 
+// stream-ordered frees of scratch buffers on every exit path of a build function
+struct ScratchFree {
+  hipStream_t s;
+  std::vector<void *> p;
+  ~ScratchFree() {
+    for (void *q : p)
+      if (q != nullptr) (void)hipFreeAsync(q, s);
+  }
+};
+
 // ---- collectives (api.hip): RCCL, or the in-process transport ---------------
 // sum-allreduce of n doubles in place (no-op on one rank)
 int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n);

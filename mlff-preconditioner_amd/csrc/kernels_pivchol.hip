@@ -193,6 +193,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   MLFF_HIP(ctx, hipMallocAsync(&pv, sizeof(double) * np, s));
   MLFF_HIP(ctx, hipMallocAsync(&pp, sizeof(long long) * np, s));
   MLFF_HIP(ctx, hipMallocAsync(&wins, sizeof(double) * 2 * ctx->world, s));
+  ScratchFree scratch{s, {pv, pp, wins}};
   // init: perm = arange(N), dwork = diag(S), pivflag = 0, Lt = 0
   std::vector<int64_t> hperm(N);
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
@@ -202,12 +203,14 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   if (mfcols) {
     MLFF_TRY(operator_diag(ctx, ctx->dwork));
     MLFF_HIP(ctx, hipMallocAsync(&colbuf, sizeof(double) * blk, s));
+    scratch.p.push_back(colbuf);
     MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
   } else {
     launch_diag_of(ctx->K, ctx->ld, nrows, ctx->row0, ctx->rows_per, blk, ctx->sigma_K, ctx->dwork, s);
   }
   const int kmax_split = choose_ksplit(k, blk);
   MLFF_HIP(ctx, hipMallocAsync(&part, sizeof(double) * kmax_split * blk, s));
+  scratch.p.push_back(part);
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
@@ -242,11 +245,6 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   if (index_columns_out != nullptr)
     MLFF_HIP(ctx, hipMemcpyAsync(index_columns_out, ctx->perm, sizeof(int64_t) * N,
                                  hipMemcpyDeviceToHost, s));
-  MLFF_HIP(ctx, hipFreeAsync(pv, s));
-  MLFF_HIP(ctx, hipFreeAsync(pp, s));
-  MLFF_HIP(ctx, hipFreeAsync(part, s));
-  if (colbuf) MLFF_HIP(ctx, hipFreeAsync(colbuf, s));
-  MLFF_HIP(ctx, hipFreeAsync(wins, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   if (perr)
     return set_error(ctx, MLFF_ERR_NOT_PSD,
