@@ -332,6 +332,28 @@ def main():
     achieved = gemv_bytes / (gemv_ms * 1e-3) / 1e9
     dense_equiv = (8.0 * nloc * n + 16.0 * nloc) / (gemv_ms * 1e-3) / 1e9
     per_iter_bytes = op_bytes + 16.0 * k * nloc + 80.0 * nloc
+    roof_op = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBS,
+               "traffic": pmc_traffic(workload, storage, world),
+               "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
+                          "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
+                          "matfree": "k_mf_z + k_mf_pair + k_mf_pair_fin + k_mf_h + k_mf_jt "
+                                     "(matrix-free sGDML operator)"}.get(storage, storage),
+               "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
+    # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials
+    roof_pre = None
+    if tm.get("precon_count"):
+        pre_ms = tm["precon_ms"] / tm["precon_count"]
+        pre_bytes = 16.0 * k * nloc + 24.0 * nloc
+        pre_gbs = pre_bytes / (pre_ms * 1e-3) / 1e9
+        roof_pre = {"bound": "hbm", "achieved": pre_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": pre_gbs / HBM_PEAK_GBS,
+                    "traffic": pmc_traffic(workload + "/precon", storage, world),
+                    "kernel": "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)",
+                    "bytes_per_launch": pre_bytes, "mean_launch_ms": pre_ms}
+    # the roofline entry is the kernel group with the larger share of the iteration
+    roof_dominant = roof_pre if roof_pre is not None and roof_pre["mean_launch_ms"] > gemv_ms \
+        else roof_op
 
     solve = None
     if not args.no_solve:
@@ -383,14 +405,9 @@ def main():
                        "storage": storage,
                        "parallelism": f"row-shard x{world} (RCCL allgather/allreduce"
                        + ("/reduce-scatter)" if storage == "sym" else ")")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": pmc_traffic(workload, storage, world),
-                         "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
-                                    "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
-                                    "matfree": "k_mf_z + k_mf_pair + k_mf_pair_fin + k_mf_h + k_mf_jt "
-                                               "(matrix-free sGDML operator)"}.get(storage, storage),
-                         "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms},
+            "roofline": roof_dominant,
+            "operator_roofline": roof_op,
+            "precon_roofline": roof_pre,
             "matvec_gbs": achieved,
             # with half storage also report against the dense 8 N^2 bytes
             "matvec_gbs_dense_equivalent": dense_equiv,

@@ -238,6 +238,9 @@ int mlff_timing_enable(mlff_ctx *ctx, int on);
  * whole PCG iteration since the last reset */
 int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double *iter_ms,
                      int64_t *iter_count);
+/* summed HIP-event time of the low-rank preconditioner apply (T r, T^T t, z) inside
+ * mlff_pcg_run while timing is on (one rank) */
+int mlff_timing_read_precon(mlff_ctx *ctx, double *ms, int64_t *count);
 int mlff_timing_reset(mlff_ctx *ctx);
 
 #ifdef __cplusplus

@@ -506,30 +506,34 @@ hipEvent_t timing_event(mlff_ctx *ctx) {
   return t.ev[t.used++];
 }
 
+// a timed segment of one iteration: events ev0 -> ev1 of the pool; kind 0 = operator,
+// 1 = low-rank preconditioner apply
 struct GemvMark {
-  size_t ev0;
+  size_t ev0, ev1;
   long long it;
+  int kind;
 };
 
-void mark_begin(mlff_ctx *ctx, std::vector<GemvMark> *marks, hipEvent_t *e0) {
-  *e0 = nullptr;
-  if (ctx->timing.on && marks != nullptr) {
-    *e0 = timing_event(ctx);
-    if (*e0) hipEventRecord(*e0, ctx->stream);
-  }
+constexpr size_t kNoMark = (size_t)-1;
+
+size_t mark_begin(mlff_ctx *ctx, std::vector<GemvMark> *marks) {
+  if (!ctx->timing.on || marks == nullptr) return kNoMark;
+  hipEvent_t e0 = timing_event(ctx);
+  if (e0 == nullptr) return kNoMark;
+  hipEventRecord(e0, ctx->stream);
+  return ctx->timing.used - 1;
 }
 
-void mark_end(mlff_ctx *ctx, std::vector<GemvMark> *marks, hipEvent_t e0, long long it) {
-  if (e0 == nullptr) return;
+void mark_end(mlff_ctx *ctx, std::vector<GemvMark> *marks, size_t i0, long long it, int kind = 0) {
+  if (i0 == kNoMark) return;
   hipEvent_t e1 = timing_event(ctx);
   if (e1) {
     hipEventRecord(e1, ctx->stream);
-    marks->push_back({ctx->timing.used - 2, it});
+    marks->push_back({i0, ctx->timing.used - 1, it, kind});
   }
 }
 
-// One PCG iteration on several ranks: three collectives (two for the dense / matrix-free
-// operators without a preconditioner, ... ) instead of five:
+// One PCG iteration on several ranks: three collectives instead of five:
 //   allgather(z_g | rho partials)  -> rho and the whole p on every rank
 //   [symmetric tiles] reduce-scatter(K p partial rows | p.q shares) -> q rows and p.q
 //   [other storages]  allreduce(p.q partials)
@@ -562,8 +566,7 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   MLFF_TRY(comm_allgather(ctx, zg, ctx->gb, (size_t)ctx->gstride));
   launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
                            status, s);
-  hipEvent_t e0;
-  mark_begin(ctx, marks, &e0);
+  const size_t e0 = mark_begin(ctx, marks);
   if (ctx->use_sym) {
     SymPack &sp = ctx->sym;
     launch_symv(sp, ctx->p_full, sp.P, status, s);
@@ -607,18 +610,19 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
   if (fold_in) fold = StopFold{rr_part(ctx), ctx->st, ctx->trace, it - 1};
   const double *zsrc;
   if (lowrank) {
+    const size_t pm = mark_begin(ctx, marks);
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s,
                       fold);
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
                     ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
+    mark_end(ctx, marks, pm, it, 1);
     zsrc = ctx->z;
   } else {
     launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s, fold);
     zsrc = ctx->r;
   }
   launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
-  hipEvent_t e0;
-  mark_begin(ctx, marks, &e0);
+  const size_t e0 = mark_begin(ctx, marks);
   if (ctx->use_sym) {
     // q = sigma K p + lam p and the p.q partials from the slot reduction (no dot launch)
     launch_symv(ctx->sym, ctx->p_full, ctx->sym.P, status, s);
@@ -1254,9 +1258,14 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
       for (const GemvMark &mk : marks) {
         if (mk.it > done_now) continue;  // gated launches after convergence
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, ctx->timing.ev[mk.ev0], ctx->timing.ev[mk.ev0 + 1]) == hipSuccess) {
-          ctx->timing.gemv_ms += ms;
-          ctx->timing.gemv_count += 1;
+        if (hipEventElapsedTime(&ms, ctx->timing.ev[mk.ev0], ctx->timing.ev[mk.ev1]) == hipSuccess) {
+          if (mk.kind == 0) {
+            ctx->timing.gemv_ms += ms;
+            ctx->timing.gemv_count += 1;
+          } else {
+            ctx->timing.pre_ms += ms;
+            ctx->timing.pre_count += 1;
+          }
         }
       }
       float ms = 0.f;
@@ -1328,10 +1337,19 @@ int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double
   return MLFF_OK;
 }
 
+int mlff_timing_read_precon(mlff_ctx *ctx, double *ms, int64_t *count) {
+  MLFF_ENTER(ctx);
+  if (ms) *ms = ctx->timing.pre_ms;
+  if (count) *count = ctx->timing.pre_count;
+  return MLFF_OK;
+}
+
 int mlff_timing_reset(mlff_ctx *ctx) {
   MLFF_ENTER(ctx);
   ctx->timing.gemv_ms = 0.0;
   ctx->timing.gemv_count = 0;
+  ctx->timing.pre_ms = 0.0;
+  ctx->timing.pre_count = 0;
   ctx->timing.iter_ms = 0.0;
   ctx->timing.iter_count = 0;
   return MLFF_OK;

@@ -101,6 +101,8 @@ struct Timing {
   size_t used = 0;             // events used in the current chunk
   double gemv_ms = 0.0;
   int64_t gemv_count = 0;
+  double pre_ms = 0.0;     // low-rank preconditioner apply (one rank)
+  int64_t pre_count = 0;
   double iter_ms = 0.0;
   int64_t iter_count = 0;
 };

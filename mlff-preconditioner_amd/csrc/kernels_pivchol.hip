@@ -167,8 +167,16 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
        i += (int64_t)gridDim.x * 256) {
     if (pivflag[i]) continue;
     const double col = colvec != nullptr ? colvec[i] : sigma * K[i * ld + pos];
-    double s0 = 0.0;
-    for (int ks = 0; ks < ksplit; ++ks) s0 += part[(int64_t)ks * ldp + i];
+    double s0 = 0.0;  // slice partials in slice order, 8 loads in flight
+    int ks = 0;
+    for (; ks + 7 < ksplit; ks += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)(ks + u) * ldp + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s0 += t[u];
+    }
+    for (; ks < ksplit; ++ks) s0 += part[(int64_t)ks * ldp + i];
     const double v = (col - s0) / sq;
     Lt[m * ldl + i] = v;
     dwork[i] -= v * v;

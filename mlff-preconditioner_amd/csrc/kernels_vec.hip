@@ -267,8 +267,17 @@ __global__ __launch_bounds__(256) void k_precon_fin(const double *__restrict__ p
   double rho_acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
+    // the ksplit slice partials in slice order, 8 loads in flight
     double sv = 0.0;
-    for (int ks = 0; ks < ksplit; ++ks) sv += part[(int64_t)ks * ldp + i];
+    int ks = 0;
+    for (; ks + 7 < ksplit; ks += 8) {
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)(ks + u) * ldp + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sv += t[u];
+    }
+    for (; ks < ksplit; ++ks) sv += part[(int64_t)ks * ldp + i];
     const double rv = r[i];
     const double zv = sigma_p * (lam_inv * (rv - sv));
     z[i] = zv;

@@ -83,6 +83,7 @@ SIGNATURES = {
     "mlff_timing_enable": (_int, [_c_ctx, _int]),
     "mlff_timing_read": (_int, [_c_ctx, _p_dbl, _p_i64, _p_dbl, _p_i64]),
     "mlff_timing_reset": (_int, [_c_ctx]),
+    "mlff_timing_read_precon": (_int, [_c_ctx, _p_dbl, _p_i64]),
 }
 
 _lib = None

@@ -316,8 +316,10 @@ class KernelSolver:
         gm, gc, im, ic = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double(), ctypes.c_int64()
         self._call("mlff_timing_read", ctypes.byref(gm), ctypes.byref(gc), ctypes.byref(im),
                    ctypes.byref(ic))
+        pm, pc = ctypes.c_double(), ctypes.c_int64()
+        self._call("mlff_timing_read_precon", ctypes.byref(pm), ctypes.byref(pc))
         return {"gemv_ms": gm.value, "gemv_count": gc.value, "iter_ms": im.value,
-                "iter_count": ic.value}
+                "iter_count": ic.value, "precon_ms": pm.value, "precon_count": pc.value}
 
 
 def sgdml_descriptors(R: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
