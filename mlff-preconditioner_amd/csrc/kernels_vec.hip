@@ -171,6 +171,10 @@ int choose_tsplit(int64_t k, int64_t ncols) {
   return (int)splits;
 }
 
+// panels above this size do not share the 256 MB MALL with the operator's tables
+constexpr double kPanelMallBytes = 192.0e6;
+bool panel_streams(int64_t k, int64_t ldt) { return 8.0 * (double)k * (double)ldt > kPanelMallBytes; }
+
 void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
                        const double *r, double *tpart, const int *status, hipStream_t s,
                        StopFold fold) {
@@ -178,11 +182,16 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
   const int64_t n2 = ncols / 2;  // ncols is the padded local length (even)
   const int64_t cs2 = (n2 + splits - 1) / splits;
   dim3 grid((unsigned)((k + R - 1) / R), (unsigned)splits);
-  // default-policy loads: the panel (k x N, 134 MB at k = 256, N = 65536) can stay in
-  // the 256 MB MALL between this pass, the T^T t pass and the next iteration, since the
-  // operator streams K with non-temporal loads
-  hipLaunchKernelGGL((k_gemv<R, U, 0, false>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
-                     k, 1.0, 0.0, (const double *)nullptr, status, fold);
+  // A panel that fits the 256 MB MALL with room to spare (134 MB at k = 256, N = 65536)
+  // is read with default-policy loads, so the T^T t pass finds it there; a larger one
+  // (the nanotube's 336 MB at k = 2701) is streamed non-temporally so it does not evict
+  // the operator's tables (panel_streams)
+  if (panel_streams(k, ldt))
+    hipLaunchKernelGGL((k_gemv<R, U, 0, true>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
+                       k, 1.0, 0.0, (const double *)nullptr, status, fold);
+  else
+    hipLaunchKernelGGL((k_gemv<R, U, 0, false>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
+                       k, 1.0, 0.0, (const double *)nullptr, status, fold);
 }
 
 // ---------------------------------------------------------------------------
@@ -190,6 +199,7 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
 // t_j = sum_{sp < tsplits} tsrc[sp * tstride + j].  Workgroup = 512 columns (one
 // double2 per thread, the 4 waves read 4 KB of every row) x one slice of rows, so
 // a k x N panel is spread over ~1024 workgroups whatever its shape.
+template <bool NT>
 __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__ W, int64_t ldw,
                                                       int64_t k, const double *__restrict__ tsrc,
                                                       int tsplits, int64_t tstride,
@@ -216,7 +226,8 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
   for (; j + 7 < j1; j += 8) {  // 8 rows (128 B per lane) in flight
     d2 a[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) a[u] = w2[(j + u) * ld2];
+    for (int u = 0; u < 8; ++u)
+      a[u] = NT ? __builtin_nontemporal_load(w2 + (j + u) * ld2) : w2[(j + u) * ld2];
 #pragma unroll
     for (int u = 0; u < 8; u += 2) {
       const double t0 = t_sh[j + u - j0], t1 = t_sh[j + u + 1 - j0];
@@ -251,8 +262,12 @@ void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *
   const int64_t kslice = (k + ksplit - 1) / ksplit;
   const dim3 grid((unsigned)((ldw / 2 + 255) / 256), (unsigned)ksplit);
   const size_t shm = sizeof(double) * (kslice + 1 > 8 ? kslice + 1 : 8);
-  hipLaunchKernelGGL(k_colgemv_part, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits, tstride,
-                     kslice, part, status, fold);
+  if (panel_streams(k, ldw))
+    hipLaunchKernelGGL(k_colgemv_part<true>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
+                       tstride, kslice, part, status, fold);
+  else
+    hipLaunchKernelGGL(k_colgemv_part<false>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
+                       tstride, kslice, part, status, fold);
 }
 
 // z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
