@@ -264,3 +264,33 @@ def test_pcg_x0_legacy_semantics(sg, case):
     assert not res.early_exit and res.iters > 0
     np.testing.assert_allclose(res.trace[0], tr[0], rtol=1e-12)
     assert_pcg_parity(res.iters, res.trace[1:], res.x, it, tr[1:], x_ref, mode="stable")
+
+
+def test_call_order_and_argument_errors(sg):
+    """State / argument errors surface as the reference's exception types
+    (RuntimeError for call-order errors, ValueError for bad arguments) and leave the
+    context usable."""
+    from sgdml_amd import synthetic
+
+    n = 300
+    X, b = synthetic.rbf_points(n, 3, 1)
+    with sg.KernelSolver(n) as s:
+        with pytest.raises(RuntimeError):
+            s.pcg(b, tol=1e-6)                      # no operator yet
+        s.gen_rbf(X, 0.2)
+        with pytest.raises(RuntimeError):
+            s.precon_pivchol(10)                    # mlff_set_operator not called
+        s.set_operator(1.0, 1e-2)
+        with pytest.raises(ValueError):
+            s.precon_nystrom(np.array([5, 3, 9]))   # unsorted (train.py:1197-1201)
+        with pytest.raises(ValueError):
+            s.precon_nystrom(np.array([1, 1, 2]))   # duplicate
+        with pytest.raises(ValueError):
+            s.precon_nystrom(np.array([0, n]))      # out of range
+        with pytest.raises(ValueError):
+            s.precon_pivchol(n + 1)
+        with pytest.raises(ValueError):
+            s.matvec(np.zeros(n + 1))
+        s.precon_pivchol(20)                        # still usable
+        res = s.pcg(b, tol=1e-8, maxiter=5 * n)
+        assert res.info == 0
