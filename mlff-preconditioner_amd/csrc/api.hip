@@ -15,6 +15,8 @@
 // so the iteration count is exact without a per-iteration host sync.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>

@@ -7,6 +7,8 @@
 // iterative_cholesky.py:145-148, iterative_solver.py:315-318 and :376-379.
 #include "common.h"
 
+#include <algorithm>
+
 namespace mlff {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -161,9 +163,14 @@ void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v
                      (int64_t)0, sigma, lam, vloc, status, StopFold{});
 }
 
+// Split factors of the two panel passes, from split-factor sweeps on MI355X (round 1;
+// per-kernel times on one box): T r with ~512 workgroups (RBF k = 256: ts 16 -> 8, same
+// 24 us; nanotube k = 2701: ts 2 -> 1, 55 -> 54 us); T^T t with ~96 panel rows per
+// workgroup (RBF: 32 rows 24.8 us, 128 rows 21.5 us; nanotube: 80 rows 57.8 us, 300 rows
+// 66.7 us).
 int choose_tsplit(int64_t k, int64_t ncols) {
   const int64_t row_groups = (k + 3) / 4;
-  int64_t splits = (1024 + row_groups - 1) / row_groups;
+  int64_t splits = (512 + row_groups - 1) / row_groups;
   const int64_t max_by_cols = (ncols / 2 + 255) / 256;  // at least 256 double2 per split
   if (splits > max_by_cols) splits = max_by_cols;
   if (splits < 1) splits = 1;
@@ -248,7 +255,8 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
 
 int choose_ksplit(int64_t k, int64_t ncols) {
   const int64_t slabs = (ncols + 511) / 512;
-  int64_t sk = (1024 + slabs - 1) / slabs;
+  // ~96 panel rows per workgroup (32 or 300 were slower), and at least ~256 workgroups
+  int64_t sk = std::max<int64_t>((k + 95) / 96, (256 + slabs - 1) / slabs);
   const int64_t cap = (k + 15) / 16;  // at least 16 rows per slice
   if (sk > cap) sk = cap;
   if (sk < 1) sk = 1;
