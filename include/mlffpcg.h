@@ -107,6 +107,12 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
 int mlff_ctx_destroy(mlff_ctx *ctx);
 const char *mlff_last_error(mlff_ctx *ctx); /* ctx may be NULL (thread-local last error) */
 int mlff_shard_range(mlff_ctx *ctx, int64_t *row0_out, int64_t *nrows_out);
+/* Abort this rank's communicator (ncclCommAbort; for an in-process "LOCAL:" group, the
+ * whole group): peers blocked in, or later entering, a collective return MLFF_ERR_COMM,
+ * and every later call on this context fails with MLFF_ERR_COMM (destroy still works).
+ * The bindings call it when an entry point fails on a sharded context with anything
+ * but MLFF_ERR_NOT_PSD / MLFF_ERR_LINALG, which every rank reaches together. */
+int mlff_comm_abort(mlff_ctx *ctx);
 /* leading dimension (doubles) of the device copy of K; rows are padded to 64 */
 int mlff_matrix_ld(mlff_ctx *ctx, int64_t *ld_out);
 int mlff_synchronize(mlff_ctx *ctx);

@@ -37,8 +37,13 @@ int set_error(mlff_ctx *ctx, int code, const std::string &msg) {
   return code;
 }
 
+void local_abort(mlff_ctx *ctx);
+
+// A device failure on one rank of an in-process group aborts the group, so its peers
+// return MLFF_ERR_COMM from their next collective instead of waiting forever.
 int hip_check(mlff_ctx *ctx, hipError_t e, const char *what) {
   const int code = (e == hipErrorOutOfMemory) ? MLFF_ERR_NOMEM : MLFF_ERR_HIP;
+  local_abort(ctx);
   return set_error(ctx, code, std::string(what) + ": " + hipGetErrorString(e));
 }
 
@@ -57,19 +62,38 @@ struct LocalGroup {
   std::condition_variable cv;
   int arrived = 0;
   long long gen = 0;
+  bool aborted = false;
   std::vector<double> buf;  // world * count staging
-  void barrier() {
+  // false once any member has aborted the group
+  bool barrier() {
     std::unique_lock<std::mutex> lk(m);
+    if (aborted) return false;
     const long long g = gen;
     if (++arrived == world) {
       arrived = 0;
       ++gen;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || aborted; });
     }
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m);
+    aborted = true;
+    cv.notify_all();
   }
 };
+
+void local_abort(mlff_ctx *ctx) {
+  if (ctx != nullptr && ctx->local) ctx->local->abort();
+}
+
+#define LOCAL_BARRIER(ctx, g)                                                        \
+  do {                                                                               \
+    if (!(g).barrier())                                                              \
+      return set_error((ctx), MLFF_ERR_COMM, "in-process group aborted by a peer rank"); \
+  } while (0)
 
 static std::mutex g_groups_m;
 static std::map<std::string, std::weak_ptr<LocalGroup>> g_groups;
@@ -96,14 +120,14 @@ int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n) {
   std::vector<double> mine(n), sum(n, 0.0);
   MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), buf, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  g.barrier();  // previous users of g.buf are done
+  LOCAL_BARRIER(ctx, g);  // previous users of g.buf are done
   if (ctx->rank == 0) g.buf.assign((size_t)g.world * n, 0.0);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   std::memcpy(g.buf.data() + (size_t)ctx->rank * n, mine.data(), sizeof(double) * n);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   for (int r = 0; r < g.world; ++r)
     for (size_t i = 0; i < n; ++i) sum[i] += g.buf[(size_t)r * n + i];
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   MLFF_HIP(ctx, hipMemcpyAsync(buf, sum.data(), sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
@@ -123,13 +147,13 @@ int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count
   std::vector<double> mine(count);
   MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   if (ctx->rank == 0) g.buf.assign((size_t)g.world * count, 0.0);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   std::memcpy(g.buf.data() + (size_t)ctx->rank * count, mine.data(), sizeof(double) * count);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   std::vector<double> all(g.buf);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   MLFF_HIP(ctx, hipMemcpyAsync(recv, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
@@ -150,14 +174,14 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
   std::vector<double> mine(n), out(count, 0.0);
   MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), send, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   if (ctx->rank == 0) g.buf.assign((size_t)g.world * n, 0.0);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   std::memcpy(g.buf.data() + (size_t)ctx->rank * n, mine.data(), sizeof(double) * n);
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   for (int r = 0; r < g.world; ++r)
     for (size_t i = 0; i < count; ++i) out[i] += g.buf[(size_t)r * n + (size_t)ctx->rank * count + i];
-  g.barrier();
+  LOCAL_BARRIER(ctx, g);
   MLFF_HIP(ctx, hipMemcpyAsync(recv, out.data(), sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
@@ -786,6 +810,18 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   ctx->local.reset();
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
+  return MLFF_OK;
+}
+
+int mlff_comm_abort(mlff_ctx *ctx) {
+  if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
+  ctx->aborted = true;
+  if (ctx->local) ctx->local->abort();
+  if (ctx->comm != nullptr) {
+    (void)hipSetDevice(ctx->device);
+    ncclCommAbort(ctx->comm);
+    ctx->comm = nullptr;
+  }
   return MLFF_OK;
 }
 

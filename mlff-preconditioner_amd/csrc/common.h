@@ -170,6 +170,7 @@ struct mlff_ctx {
 
   mlff::Timing timing;
   std::string err;
+  bool aborted = false;  // mlff_comm_abort was called: every entry point fails
 };
 
 namespace mlff {
@@ -194,6 +195,8 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
 #define MLFF_ENTER(ctx)                                                        \
   do {                                                                         \
     if ((ctx) == nullptr) return mlff::set_error(nullptr, MLFF_ERR_ARG, "null ctx"); \
+    if ((ctx)->aborted)                                                        \
+      return mlff::set_error((ctx), MLFF_ERR_COMM, "communicator aborted (mlff_comm_abort)"); \
     (void)hipSetDevice((ctx)->device);                                         \
   } while (0)
 #define MLFF_TRY(x)             \

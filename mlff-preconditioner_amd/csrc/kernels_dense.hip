@@ -314,6 +314,7 @@ __global__ __launch_bounds__(256) void k_colsumsq(const double *__restrict__ W, 
 
 void launch_colsumsq(const double *W, int64_t k, int64_t ncols, int64_t ldw, double *out,
                      hipStream_t s) {
+  if (ncols <= 0) return;
   hipLaunchKernelGGL(k_colsumsq, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, s, W, k,
                      ncols, ldw, out);
 }

@@ -53,6 +53,7 @@ __global__ __launch_bounds__(256) void k_gen_rbf(double *__restrict__ K, int64_t
 void launch_gen_rbf(double *K, int64_t ld, int64_t nrows, int64_t row0, int64_t rows_per,
                     int64_t blk, int64_t N, const double *Xs, int d, double jitter,
                     hipStream_t s) {
+  if (nrows <= 0) return;
   const unsigned gx = (unsigned)std::min<int64_t>((ld + 255) / 256, 16);
   hipLaunchKernelGGL(k_gen_rbf, dim3(gx, (unsigned)nrows), dim3(256), 0, s, K, ld, nrows, row0,
                      rows_per, blk, N, Xs, d, jitter);
@@ -67,6 +68,7 @@ __global__ void k_diag_of(const double *__restrict__ K, int64_t ld, int64_t nrow
 
 void launch_diag_of(const double *K, int64_t ld, int64_t nrows, int64_t row0, int64_t rows_per,
                     int64_t blk, double sigma, double *out, hipStream_t s) {
+  if (nrows <= 0) return;
   hipLaunchKernelGGL(k_diag_of, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, s, K, ld,
                      nrows, row0, rows_per, blk, sigma, out);
 }
@@ -88,6 +90,7 @@ __global__ __launch_bounds__(256) void k_gather_cols(const double *__restrict__ 
 void launch_gather_cols(const double *K, int64_t ld, int64_t nrows, const int64_t *idx,
                         int64_t k, int64_t rows_per, int64_t blk, double sigma, double *W,
                         int64_t ldw, hipStream_t s) {
+  if (nrows <= 0) return;
   const unsigned gx = (unsigned)std::min<int64_t>((nrows + 255) / 256, 64);
   hipLaunchKernelGGL(k_gather_cols, dim3(gx, (unsigned)k), dim3(256), 0, s, K, ld, nrows, idx, k,
                      rows_per, blk, sigma, W, ldw);

@@ -457,6 +457,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, kJS),
                      dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
                      mf.ypart, status);
+  if (ctx->nrows <= 0) return;
   hipLaunchKernelGGL(k_mf_jt_fin, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s,
                      mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, status);
 }

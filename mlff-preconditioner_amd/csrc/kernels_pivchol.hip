@@ -242,7 +242,8 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
     if (ks > 0)
       launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s);
-    hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
+    if (gcol > 0)
+      hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
                        (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
                        ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());

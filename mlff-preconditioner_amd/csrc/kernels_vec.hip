@@ -157,6 +157,7 @@ void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v
                       double sigma, double lam, const double *vloc, const int *status,
                       hipStream_t s) {
   constexpr int R = 4, U = 4;
+  if (rows <= 0) return;
   const int64_t n2 = ld / 2;
   dim3 grid((unsigned)((rows + R - 1) / R), 1);
   hipLaunchKernelGGL((k_gemv<R, U, 1>), grid, dim3(256), 0, s, M, ld, rows, n2, n2, v, y,

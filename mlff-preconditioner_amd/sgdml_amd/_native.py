@@ -51,6 +51,7 @@ SIGNATURES = {
     "mlff_ctx_destroy": (_int, [_c_ctx]),
     "mlff_last_error": (ctypes.c_char_p, [_c_ctx]),
     "mlff_shard_range": (_int, [_c_ctx, _p_i64, _p_i64]),
+    "mlff_comm_abort": (_int, [_c_ctx]),
     "mlff_matrix_ld": (_int, [_c_ctx, _p_i64]),
     "mlff_synchronize": (_int, [_c_ctx]),
     "mlff_stream": (_int, [_c_ctx, ctypes.POINTER(ctypes.c_void_p)]),

@@ -73,8 +73,15 @@ class ShardedKernelSolver:
             w.q.put((lambda r=r: fn(r), box, done))
             boxes.append(box)
             events.append(done)
-        for e in events:
-            e.wait()
+        aborted = False
+        while not all(e.wait(0.05) for e in events):
+            if not aborted and any("error" in b for b in boxes) and self.ranks[0] is not None:
+                # a failed rank leaves its peers blocked in a collective: abort their
+                # communicators too (the RCCL-documented way to release them)
+                aborted = True
+                for s in self.ranks:
+                    if s is not None and s._ctx is not None:
+                        s._lib.mlff_comm_abort(s._ctx)
         for b in boxes:
             if "error" in b:
                 raise b["error"]

@@ -58,6 +58,14 @@ class KernelSolver:
     # ------------------------------------------------------------------ basics
     def _call(self, name, *args):
         rc = getattr(self._lib, name)(self._ctx, *args)
+        if rc != nat.MLFF_OK and self.world > 1 and rc not in (nat.MLFF_ERR_NOT_PSD,
+                                                                nat.MLFF_ERR_LINALG):
+            # a failure on one rank would leave its peers waiting in the next collective
+            # (mlff_comm_abort); NOT_PSD / LINALG are reached by every rank together
+            try:
+                nat.check(rc, self._ctx, name)
+            finally:
+                self._lib.mlff_comm_abort(self._ctx)
         nat.check(rc, self._ctx, name)
 
     def close(self):

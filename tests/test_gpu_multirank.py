@@ -210,3 +210,67 @@ def test_sharded_x0_matches_single_rank():
     x = np.concatenate([o[0] for o in outs])
     assert_pcg_parity(outs[0][1], outs[0][2][1:], x, ref[1], ref[2][1:], ref[0], mode="chaotic",
                       x_tol=1e-7)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 513, 1100, 2049])
+@pytest.mark.parametrize("world", [2, 5, 8])
+def test_sharded_ragged_sizes(n, world):
+    """Ragged shards (N not a multiple of W, ranks with no rows, one-tile problems) through
+    the three-collective iteration, both operator storages: the sharded mat-vec equals the
+    one-rank one, and the solve agrees with the one-rank solve."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    X, b = synthetic.rbf_points(n, 3, n)
+    v = np.random.default_rng(n).standard_normal(n)
+    k = max(1, min(40, n // 3))
+
+    def body(rank, w, key, storage):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=w, comm_id=key if w > 1 else None)
+        try:
+            s.gen_rbf(X, 0.3)
+            s.set_operator(1.0, 0.5)
+            s.set_storage(storage)
+            y = s.matvec(v)
+            s.precon_pivchol(k)
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(b[r0:r1]), tol=1e-10, maxiter=5 * n + 5)
+            return y, res.x, res.iters, res.info
+        finally:
+            s.close()
+
+    for storage in ("sym", "dense"):
+        ref = run_ranks(1, lambda r, w, key: body(r, w, key, storage))[0]
+        outs = run_ranks(world, lambda r, w, key: body(r, w, key, storage))
+        y = np.concatenate([o[0] for o in outs])
+        np.testing.assert_allclose(y, ref[0], rtol=1e-13, atol=1e-13 * np.abs(ref[0]).max())
+        x = np.concatenate([o[1] for o in outs])
+        assert all(o[3] == 0 for o in outs) and ref[3] == 0
+        assert all(o[2] == outs[0][2] for o in outs)
+        assert abs(outs[0][2] - ref[2]) <= 2
+        assert np.linalg.norm(x - ref[1]) <= 1e-8 * max(np.linalg.norm(ref[1]), 1e-300)
+
+
+def test_rank_failure_aborts_group():
+    """A failure on one rank (here: an argument error only rank 1 makes) aborts the
+    in-process group: its peer returns from the collective with an error instead of
+    waiting forever, and the aborted contexts refuse further calls."""
+    import sgdml_amd
+
+    n = 300
+    X, b = problem(n)
+
+    def body(rank, world, key):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world, comm_id=key)
+        try:
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, 0.1)
+            with pytest.raises((ValueError, RuntimeError)):
+                s.precon_pivchol(10 if rank == 0 else n + 5)
+            with pytest.raises(RuntimeError, match="aborted"):
+                s.matvec(np.ones(n))
+            return True
+        finally:
+            s.close()
+
+    assert run_ranks(2, body, timeout=60) == [True, True]
