@@ -209,3 +209,44 @@ def test_matfree_sharded_builds_and_solve(sg, golden_dir, world):
     assert r.info == 0
     np.testing.assert_allclose(outs[0][1].trace[:8], r.trace[:8], rtol=1e-6)
     assert np.linalg.norm(x - r.x) <= 1e-5 * np.linalg.norm(r.x)
+
+
+@pytest.mark.parametrize("m,world", [(1, 8), (1, 5), (2, 8), (3, 7)])
+def test_matfree_ragged_shards(sg, golden_dir, m, world):
+    """Matrix-free operator on shards that split molecules mid-way and on ranks with no
+    rows (N = 27 m < W * ceil(N / W)): mat-vec, operator-column pivoted Cholesky and the
+    solve match the one-rank run."""
+    f = load_golden(golden_dir, "sgdml_ethanol_n270")
+    Rd, Rdd = f["R_desc"][:m], f["R_d_desc"][:m]
+    n, sig = 27 * m, float(f["sig"])
+    # rotations and translations leave K (27 m) singular: a ridge of 1e-3 of its diagonal
+    # keeps the solve well posed, where lam = 1e-10 makes the iteration count a lottery
+    lam = 1e-3 * float(np.abs(f["diag_K"][:n]).mean())
+    y = np.ascontiguousarray(f["y"][:n])
+    v = np.random.default_rng(m).standard_normal(n)
+    k = min(6, n)
+
+    def body(rank, w, key):
+        with sg.KernelSolver(n, device=0, rank=rank, world=w,
+                             comm_id=key if w > 1 else None) as s:
+            s.sgdml_operator(Rd, Rdd, f["perms"], sig)
+            s.set_operator(-1.0, lam)
+            mv = s.matvec(v)
+            piv, _ = s.precon_pivchol(k)
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(y[r0:r1]), tol=1e-8, maxiter=10 * n)
+            return mv, piv, res
+
+    from tests.test_gpu_multirank import run_ranks
+
+    ref = run_ranks(1, body, timeout=120)[0]
+    outs = run_ranks(world, body, timeout=120)
+    mv = np.concatenate([o[0] for o in outs])
+    np.testing.assert_allclose(mv, ref[0], rtol=0, atol=1e-13 * np.abs(ref[0]).max())
+    for _, piv, res in outs:
+        np.testing.assert_array_equal(piv[:k], ref[1][:k])
+        assert res.info == 0 and res.iters == outs[0][2].iters
+    assert ref[2].info == 0
+    x = np.concatenate([o[2].x for o in outs])
+    assert abs(outs[0][2].iters - ref[2].iters) <= 2
+    assert np.linalg.norm(x - ref[2].x) <= 1e-6 * np.linalg.norm(ref[2].x)
