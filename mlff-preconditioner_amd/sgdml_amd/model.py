@@ -236,3 +236,69 @@ def store_model(model: dict, path_to_script: str | os.PathLike, now: datetime | 
     out = path.with_suffix(".npz")
     np.savez_compressed(out, **model)
     return out
+
+
+CG_STEPS_INFO_KEYS = ("dataset_name", "sig", "lam", "solver_tol")  # create_data.py:20
+
+
+def cg_steps_record(task: dict, model: dict, n_datapoints: int, preconditioner_strength: float,
+                    preconditioner: str, flag_eigvals: bool = False) -> dict:
+    """The measurement dict of tools/create_data.cg_steps (create_data.py:100-155) from a
+    trained model: Cholesky step timings and their begin/end medians (:123-131), the
+    preconditioner size actually used (:116-120), CG step count and the solver's timings
+    (:142-149), the task and its info keys (:150-152)."""
+    if flag_eigvals:
+        raise NotImplementedError("flag_eigvals: eigenvalue spectra are not computed here")
+    n = len(model["alphas_F"])
+    actual = len(model["inducing_pts_idxs"]) / n
+    k = int(actual * n)
+    rec: dict = {}
+    if preconditioner == "cholesky":
+        t = np.asarray(model["time_cholesky"])
+        t_begin, t_end = np.median(t[:20]), np.median(t[20:])
+        rec["t_cholesky"] = t
+        rec["time_cg_step"] = model["total_time_cg"] / model["solver_iters"]
+        rec["chol_t_begin"] = t_begin
+        rec["chol_t_end"] = t_end
+        rec["chol_t_correction"] = t_end / t_begin - 1
+    if model["is_conv"] is False:
+        raise RuntimeError("Solver is not converged.")
+    rec[f"{preconditioner}_percentage"] = actual
+    rec[f"{preconditioner}_cgsteps"] = model["solver_iters"]
+    rec["K.shape"] = (n, n)
+    rec["n_kernel"] = n
+    rec["k"] = k
+    for key in ("total_time_preconditioner", "total_time_solve", "total_time_cg"):
+        rec[key] = model[key]
+    rec["task"] = task
+    for label in CG_STEPS_INFO_KEYS:
+        rec[label] = task[label]
+    rec["platform"] = platform.uname()
+    rec["n_datapoints"] = n_datapoints
+    return rec
+
+
+def cg_steps(task: dict, n_datapoints: int, preconditioner_strength: float, preconditioner: str,
+             flag_eigvals: bool = False, path_to_script: str | os.PathLike = "",
+             devices=None, now: datetime | None = None) -> Path:
+    """tools/create_data.cg_steps (create_data.py:100-168) with the solve on the MI355X:
+    trains with `truncated_cholesky` = 1500, then pickles the record to
+    data_new/<dataset>/<precon>/n = <n>/<date>_<HHMM>_k = <k>.pickle, the file
+    scripts/main_plot.py reads."""
+    import pickle
+
+    task = dict(task)
+    task["truncated_cholesky"] = 1500
+    task["str_preconditioner"] = preconditioner
+    model = train(task, break_percentage=preconditioner_strength, callback=lambda *a, **kw: None,
+                  str_preconditioner=preconditioner, flag_eigvals=flag_eigvals, devices=devices)
+    rec = cg_steps_record(task, model, n_datapoints, preconditioner_strength, preconditioner,
+                          flag_eigvals)
+    now = now or datetime.now()
+    folder = (Path(os.path.abspath(path_to_script)) / "data_new" / str(task["dataset_name"])
+              / preconditioner / f"n = {n_datapoints}")
+    folder.mkdir(exist_ok=True, parents=True)
+    path = folder / f"{now.date()}_{now.strftime('%H%M')}_k = {rec['k']}.pickle"
+    with open(path, "wb") as fh:
+        pickle.dump(rec, fh)
+    return path

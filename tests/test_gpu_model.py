@@ -87,3 +87,24 @@ def test_train_model_entry_point(fx, tmp_path):
     assert m["kernel_size"] == n and m["hardware"] == "mi355x" and m["use_E"]
     out = mdl.store_model(m, tmp_path)
     assert out.parent == tmp_path / "data_new/models/mi355x/ethanol/cholesky/n=23/k=132"
+
+
+def test_cg_steps_writes_record(fx, tmp_path):
+    """tools/create_data.cg_steps on the GPU: the pickle lands where main_plot.py looks and
+    carries the reference's keys (create_data.py:123-155)."""
+    import pickle
+
+    from sgdml_amd import model as mdl
+
+    n = fx["model__alphas_F"].size
+    bp = int(fx["k_rot"]) / n
+    path = mdl.cg_steps(task_of(fx), 23, bp, "cholesky", path_to_script=tmp_path)
+    assert path.parent == tmp_path / "data_new" / str(fx["model__dataset_name"]) / "cholesky" / "n = 23"
+    with open(path, "rb") as fh:  # written by this test
+        rec = pickle.load(fh)
+    assert rec["k"] == int(fx["k_rot"]) and rec["n_kernel"] == n
+    assert abs(rec["cholesky_cgsteps"] - int(fx["model__solver_iters"])) <= 0.1 * int(fx["model__solver_iters"])
+    assert path.name.endswith(f"_k = {rec['k']}.pickle")
+    for key in ("t_cholesky", "time_cg_step", "chol_t_correction", "total_time_cg", "task",
+                "dataset_name", "sig", "lam", "solver_tol", "platform"):
+        assert key in rec, key

@@ -72,3 +72,26 @@ def test_store_model_layout(golden_dir, tmp_path):
     np.testing.assert_array_equal(back["alphas_F"], f["model__alphas_F"])
     assert float(back["c"]) == float(f["model__c"])
     assert back["f_err"].item()["mae"] != back["f_err"].item()["mae"]  # nan
+
+
+def test_cg_steps_record_schema():
+    """create_data.cg_steps' record (create_data.py:116-155) from a model dict."""
+    n, k = 120, 30
+    model = {"alphas_F": np.zeros(n), "inducing_pts_idxs": np.arange(k), "solver_iters": 40,
+             "time_cholesky": np.linspace(1.0, 2.0, k), "total_time_cg": 2.0, "is_conv": True,
+             "total_time_preconditioner": 0.5, "total_time_solve": 2.6}
+    task = {"dataset_name": "ethanol", "sig": 10, "lam": 1e-10, "solver_tol": 1e-4}
+    rec = mdl.cg_steps_record(task, model, 5, k / n, "cholesky")
+    t = model["time_cholesky"]
+    assert rec["k"] == k and rec["n_kernel"] == n and rec["K.shape"] == (n, n)
+    assert rec["cholesky_percentage"] == k / n and rec["cholesky_cgsteps"] == 40
+    assert rec["time_cg_step"] == 2.0 / 40
+    assert rec["chol_t_correction"] == np.median(t[20:]) / np.median(t[:20]) - 1
+    assert rec["lam"] == 1e-10 and rec["n_datapoints"] == 5 and rec["task"] is task
+    rec2 = mdl.cg_steps_record(task, model, 5, k / n, "random_scores")
+    assert "t_cholesky" not in rec2 and rec2["random_scores_cgsteps"] == 40
+    model["is_conv"] = False
+    import pytest
+
+    with pytest.raises(RuntimeError):
+        mdl.cg_steps_record(task, model, 5, k / n, "cholesky")
