@@ -474,19 +474,23 @@ int resolve_storage(mlff_ctx *ctx) {
   return MLFF_OK;
 }
 
-// y_loc = sigma_K K v_full + lam v_loc over this rank's rows (status gated)
+// y_loc = sigma_K K v_full + lam v_loc over this rank's rows (status gated).
+// pq_part: also the v_loc . y_loc partials of the CG step (kVecGrid, k_dot_part's layout;
+// fused into the last operator kernel where it can be)
 int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const double *v_loc,
-                    const int *status) {
+                    const int *status, double *pq_part = nullptr) {
   hipStream_t s = ctx->stream;
   if (ctx->use_mf) {
-    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam);
+    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part);
     return MLFF_OK;
   }
   if (!ctx->use_sym) {
     launch_gemv_rows(ctx->K, ctx->ld, ctx->nrows, v_full, y_loc, ctx->sigma_K, ctx->lam, v_loc,
                      status, s);
+    if (pq_part != nullptr) launch_dot_part(v_loc, y_loc, ctx->nrows, pq_part, status, s);
     return MLFF_OK;
   }
+  if (pq_part != nullptr) return set_error(ctx, MLFF_ERR_STATE, "launch_operator: pq with tiles");
   SymPack &sp = ctx->sym;
   launch_symv(sp, v_full, sp.P, status, s);
   if (ctx->world == 1) {
@@ -604,9 +608,8 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
                             ctx->sigma_K, ctx->lam, lowrank ? ctx->tpart_base : rr_part(ctx),
                             ctx->st, status, s);
   } else {
-    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
+    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx)));
     mark_end(ctx, marks, e0, it);
-    launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
     MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
     launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx),
                      lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
@@ -656,9 +659,8 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
                          pq_part(ctx), status, s);
     mark_end(ctx, marks, e0, it);
   } else {
-    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status));
+    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx)));
     mark_end(ctx, marks, e0, it);
-    launch_dot_part(p_loc, ctx->q, ctx->nrows, pq_part(ctx), status, s);
   }
   launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
                    status, s);

@@ -107,6 +107,26 @@ struct Timing {
   int64_t iter_count = 0;
 };
 
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+// Sum over a 256-thread block; result valid in thread 0.  Fixed order, so every
+// workgroup that reduces the same values obtains the same bits.
+__device__ __forceinline__ double block_sum256(double v, double *sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0) t = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  return t;
+}
+
 }  // namespace mlff
 
 namespace mlff {
@@ -343,8 +363,10 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
 // ---- matrix-free sGDML operator (kernels_mf.hip) ---------------------------
 int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
              const int32_t *perms, int n_perms, double sig);
+// pq_part != nullptr: also the x_loc . y_loc partials (kVecGrid, as launch_dot_part)
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
-                        const double *x_loc, const int *status, double sigma, double lam);
+                        const double *x_loc, const int *status, double sigma, double lam,
+                        double *pq_part = nullptr);
 int mf_diag(mlff_ctx *ctx, double *out);
 // training-set energy pair terms for coefficients alphas (N, contiguous): ni x M n_perms
 int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host);

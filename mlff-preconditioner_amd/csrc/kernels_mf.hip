@@ -60,6 +60,30 @@ __global__ __launch_bounds__(256) void k_mf_contig(const double *__restrict__ x,
 
 // Zt[jp, d] = sum_c Rdd_j[e, c] (x_j[t_e, c] - x_j[s_e, c]),  e = P_p[d], pair e = (s_e > t_e)
 // (x contiguous in the global index)
+struct ZSrc {
+  const double *Rdd;
+  const int32_t *Pt, *ps, *pt;
+  int n, n_perms;
+  const double *x;
+  double *Zt;  // written by the workgroups of the first point tile
+};
+
+__device__ __forceinline__ double z_entry(const ZSrc &zs, int64_t D, int64_t jp, int64_t d) {
+  const int64_t j = jp / zs.n_perms, p = jp % zs.n_perms;
+  const int64_t g0 = j * 3 * zs.n;
+  const int64_t e = zs.Pt[p * D + d];
+  const int s = zs.ps[e], t = zs.pt[e];
+  const double *r = zs.Rdd + (j * D + e) * 3;
+  double z = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double xt = zs.x[g0 + 3 * t + c];
+    const double xs = zs.x[g0 + 3 * s + c];
+    z = fma(r[c], xt - xs, z);
+  }
+  return z;
+}
+
 __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               const int32_t *__restrict__ Pt,
                                               const int32_t *__restrict__ ps,
@@ -70,21 +94,9 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   const int64_t jp = blockIdx.y;
-  const int64_t j = jp / n_perms, p = jp % n_perms;
-  const int64_t g0 = j * 3 * n;
-  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
-    const int64_t e = Pt[p * D + d];
-    const int s = ps[e], t = pt[e];
-    const double *r = Rdd + (j * D + e) * 3;
-    double z = 0.0;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const double xt = x[g0 + 3 * t + c];
-      const double xs = x[g0 + 3 * s + c];
-      z = fma(r[c], xt - xs, z);
-    }
-    Zt[jp * D + d] = z;
-  }
+  const ZSrc zs{Rdd, Pt, ps, pt, n, n_perms, x, Zt};
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)
+    Zt[jp * D + d] = z_entry(zs, D, jp, d);
 }
 
 // Partial pair sums over the descriptor slice z of this workgroup for a tile of
@@ -93,15 +105,17 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
 //   MODE 0: |Rd_i - Rt[jp]|^2                (setup)
 //   MODE 1: (Rd_i - Rt[jp]) . Zt[jp]
 // part[(z * ni + il) * MP + jp]; k_mf_pair_fin sums the slices in a fixed order.
+// FZ: the Zt entries of the tile are computed here (as k_mf_z, same bits) and stored by
+// the workgroups of point tile 0, one launch less per mat-vec.
 constexpr int kPT = 16;  // tile edge (points and pairs)
 constexpr int kDC = 64;  // descriptor chunk staged in LDS
-template <int MODE>
+template <int MODE, bool FZ = false>
 __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
                                                  const double *__restrict__ Rt,
                                                  const double *__restrict__ Zt, int64_t D,
                                                  int64_t dslice, int64_t i0, int64_t ni,
                                                  int64_t MP, double *__restrict__ part,
-                                                 const int *__restrict__ status) {
+                                                 const int *__restrict__ status, ZSrc zs = {}) {
   if (MODE == 1 && status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sR[kPT][kDC + 1];
   __shared__ double sT[kPT][kDC + 1];
@@ -121,7 +135,15 @@ __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
       const int64_t il = ic0 + r, jp = jp0 + r;
       sR[r][cc] = (okd && il < ni) ? Rd[(i0 + il) * D + d] : 0.0;
       sT[r][cc] = (okd && jp < MP) ? Rt[jp * D + d] : 0.0;
-      if (MODE == 1) sZ[r][cc] = (okd && jp < MP) ? Zt[jp * D + d] : 0.0;
+      if (MODE == 1 && !FZ) sZ[r][cc] = (okd && jp < MP) ? Zt[jp * D + d] : 0.0;
+      if (MODE == 1 && FZ) {
+        double z = 0.0;
+        if (okd && jp < MP) {
+          z = z_entry(zs, D, jp, d);
+          if (blockIdx.y == 0) zs.Zt[jp * D + d] = z;
+        }
+        sZ[r][cc] = z;
+      }
     }
     __syncthreads();
 #pragma unroll 8
@@ -331,21 +353,33 @@ __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
   }
 }
 
-// y = sigma * sum_z part[z] + lam * x (fixed slice order)
+// y = sigma * sum_z part[z] + lam * x (fixed slice order).  PQ: also the x . y partials
+// of the CG step, on the kVecGrid grid-stride layout of k_dot_part (same terms, same
+// order: the separate dot launch it replaces gives the same bits)
+template <bool PQ>
 __global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ part, int64_t nrows,
                                                    double sigma, double lam,
                                                    const double *__restrict__ xloc,
                                                    double *__restrict__ y,
+                                                   double *__restrict__ pq_part,
                                                    const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= nrows) return;
-  double s = 0.0;
+  __shared__ double sh[8];
+  double acc = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows;
+       r += (int64_t)gridDim.x * 256) {
+    double s = 0.0;
 #pragma unroll
-  for (int z = 0; z < kJS; ++z) s += part[(int64_t)z * nrows + r];
-  double yv = sigma * s;
-  if (xloc != nullptr) yv += lam * xloc[r];
-  y[r] = yv;
+    for (int z = 0; z < kJS; ++z) s += part[(int64_t)z * nrows + r];
+    double yv = sigma * s;
+    if (xloc != nullptr) yv += lam * xloc[r];
+    y[r] = yv;
+    if (PQ) acc = fma(xloc[r], yv, acc);
+  }
+  if (PQ) {
+    const double t = block_sum256(acc, sh);
+    if (threadIdx.x == 0) pq_part[blockIdx.x] = t;
+  }
 }
 
 }  // namespace
@@ -425,11 +459,11 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
 }
 
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
-                        const double *x_loc, const int *status, double sigma, double lam) {
+                        const double *x_loc, const int *status, double sigma, double lam,
+                        double *pq_part) {
   const MfData &mf = ctx->mf;
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
-  const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
   // on one rank the padded layout is the global index itself (rows_per = N)
   const double *xc = x_full;
   if (ctx->world > 1) {
@@ -437,13 +471,18 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                        ctx->N, ctx->rows_per, ctx->blk, mf.xc, status);
     xc = mf.xc;
   }
-  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
-                     mf.M, mf.n, mf.n_perms, mf.D, xc, mf.Zt, status);
-  if (mf.ni == 0) return;
+  if (mf.ni == 0) {  // no points here: Zt is not needed either
+    if (pq_part != nullptr)  // zero partials of an empty shard
+      hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart,
+                         (int64_t)0, sigma, lam, x_loc, y_loc, pq_part, status);
+    return;
+  }
   const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
-  hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)((MP + kPT - 1) / kPT),
+  const ZSrc zs{mf.Rdd, mf.Pt, mf.ps, mf.pt, (int)mf.n, (int)mf.n_perms, xc, mf.Zt};
+  hipLaunchKernelGGL((k_mf_pair<1, true>), dim3((unsigned)((MP + kPT - 1) / kPT),
                      (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
-                     mf.Rd, mf.Rt, mf.Zt, mf.D, mf.dslice, mf.i0, mf.ni, MP, mf.part, status);
+                     mf.Rd, mf.Rt, (const double *)nullptr, mf.D, mf.dslice, mf.i0, mf.ni, MP,
+                     mf.part, status, zs);
   hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
                      mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
   const int64_t dblk = (mf.D + 63) / 64;
@@ -457,9 +496,14 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, kJS),
                      dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
                      mf.ypart, status);
+  if (pq_part != nullptr) {
+    hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, ctx->nrows,
+                       sigma, lam, x_loc, y_loc, pq_part, status);
+    return;
+  }
   if (ctx->nrows <= 0) return;
-  hipLaunchKernelGGL(k_mf_jt_fin, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0, s,
-                     mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, status);
+  hipLaunchKernelGGL(k_mf_jt_fin<false>, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0,
+                     s, mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, (double *)nullptr, status);
 }
 
 // Training-set energies of the model with coefficients `alphas` (contiguous global

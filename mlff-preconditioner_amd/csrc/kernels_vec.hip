@@ -13,25 +13,6 @@ namespace mlff {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-  return v;
-}
-
-// Sum over a 256-thread block; result valid in thread 0.  Fixed order, so every
-// workgroup that reduces the same values obtains the same bits.
-__device__ __forceinline__ double block_sum256(double v, double *sh) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sh[w] = v;
-  __syncthreads();
-  double t = 0.0;
-  if (threadIdx.x == 0) t = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-  return t;
-}
-
 // Deterministic sum of np partials, broadcast to every thread of the block.
 __device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ part, int np,
                                                      double *sh) {
