@@ -258,6 +258,7 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   MLFF_HIP(ctx, hipMalloc(&ctx->T, sizeof(double) * round_up(k, 8) * ctx->blk));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * ctx->blk, ctx->stream));
   ctx->tsplit = choose_tsplit(k, ctx->blk);
+  if (const char *e = std::getenv("MLFF_TSPLIT")) ctx->tsplit = std::max(1, std::atoi(e));  // sweeps
   // [rr partials (kVecGrid) | tpart (k x tsplit)]: on several ranks the end-of-iteration
   // ||r||^2 reduction and the next iteration's T r reduction share one all-reduce
   MLFF_HIP(ctx, hipMalloc(&ctx->tpart_base, sizeof(double) * (kVecGrid + k * ctx->tsplit)));
@@ -266,7 +267,9 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
     (void)hipFree(ctx->zpart);
     ctx->zpart = nullptr;
   }
-  ctx->zsplit = choose_ksplit(k, ctx->blk);
+  ctx->zsplit = choose_zsplit(k, ctx->blk);
+  if (const char *e = std::getenv("MLFF_ZSPLIT"))  // sweeps
+    ctx->zsplit = (int)std::min<int64_t>(std::max(1, std::atoi(e)), (k + 15) / 16);
   MLFF_HIP(ctx, hipMalloc(&ctx->zpart, sizeof(double) * ctx->zsplit * ctx->blk));
   return MLFF_OK;
 }

@@ -251,6 +251,8 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
                        const double *r, double *tpart, const int *status, hipStream_t s,
                        StopFold fold = StopFold{});
 int choose_tsplit(int64_t k, int64_t ncols);
+// split factor of the apply's T^T t pass (choose_ksplit adjusted to fill whole waves)
+int choose_zsplit(int64_t k, int64_t ncols);
 // z = sigma_p/lam * (r - T^T t), t = sum_sp tpart; rho partials (r . z)
 // (split-K over the k rows of T: zpart holds zsplit x ldt partial sums)
 void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const double *tpart,

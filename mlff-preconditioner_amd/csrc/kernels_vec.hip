@@ -146,18 +146,43 @@ void launch_gemv_rows(const double *M, int64_t ld, int64_t rows, const double *v
 }
 
 // Split factors of the two panel passes, from split-factor sweeps on MI355X (round 1;
-// per-kernel times on one box): T r with ~512 workgroups (RBF k = 256: ts 16 -> 8, same
-// 24 us; nanotube k = 2701: ts 2 -> 1, 55 -> 54 us); T^T t with ~96 panel rows per
-// workgroup (RBF: 32 rows 24.8 us, 128 rows 21.5 us; nanotube: 80 rows 57.8 us, 300 rows
-// 66.7 us).
+// per-kernel times on one box): T r with ~512 workgroups or more (RBF k = 256: ts 16 -> 8,
+// same 24 us); T^T t with ~96 panel rows per workgroup (RBF: 32 rows 24.8 us, 128 rows
+// 21.5 us; nanotube: 80 rows 57.8 us, 300 rows 66.7 us).  Both passes are resident all
+// at once, so a grid that leaves some CUs one workgroup more than others runs at the
+// pace of the busier ones: among splits a little above the minimum, take the one whose
+// grid best fills whole multiples of 256 workgroups (nanotube k = 2701: T r 676 -> 2028
+// workgroups, T^T t 899 -> 1023; apply 5.73 -> 5.93 TB/s, same box).
+static double wave_fill(int64_t wgs) {
+  const int64_t full = (wgs + 255) / 256 * 256;
+  return (double)wgs / (double)full;
+}
+
 int choose_tsplit(int64_t k, int64_t ncols) {
   const int64_t row_groups = (k + 3) / 4;
-  int64_t splits = (512 + row_groups - 1) / row_groups;
+  int64_t lo = (512 + row_groups - 1) / row_groups;
+  int64_t hi = 2 * lo + 1;
   const int64_t max_by_cols = (ncols / 2 + 255) / 256;  // at least 256 double2 per split
-  if (splits > max_by_cols) splits = max_by_cols;
-  if (splits < 1) splits = 1;
-  if (splits > 64) splits = 64;
-  return (int)splits;
+  if (hi > max_by_cols) hi = max_by_cols;
+  if (hi > 64) hi = 64;
+  if (lo > hi) lo = hi;
+  if (lo < 1) lo = 1;
+  int64_t best = lo;
+  for (int64_t sp = lo; sp <= hi; ++sp)
+    if (wave_fill(row_groups * sp) > wave_fill(row_groups * best) + 1e-9) best = sp;
+  return (int)best;
+}
+
+int choose_zsplit(int64_t k, int64_t ncols) {
+  const int64_t slabs = (ncols / 2 + 255) / 256;  // 512-column workgroups
+  const int64_t lo = choose_ksplit(k, ncols);
+  int64_t hi = lo + (lo + 3) / 4 + 1;
+  const int64_t cap = std::min<int64_t>((k + 15) / 16, 256);
+  if (hi > cap) hi = cap;
+  int64_t best = lo;
+  for (int64_t zs = lo; zs <= hi; ++zs)
+    if (wave_fill(slabs * zs) > wave_fill(slabs * best) + 1e-9) best = zs;
+  return (int)best;
 }
 
 // panels above this size do not share the 256 MB MALL with the operator's tables
