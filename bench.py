@@ -337,7 +337,7 @@ def main():
                "traffic": pmc_traffic(workload, storage, world),
                "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
                           "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
-                          "matfree": "k_mf_z + k_mf_pair + k_mf_pair_fin + k_mf_h + k_mf_jt "
+                          "matfree": "k_mf_pair (+Zt) + k_mf_pair_fin + k_mf_h + k_mf_jt + k_mf_jt_fin "
                                      "(matrix-free sGDML operator)"}.get(storage, storage),
                "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
     # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials

@@ -28,6 +28,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mlff {
 
@@ -263,7 +264,7 @@ __device__ __forceinline__ int64_t pair_of(int a, int b) {
 // block's loads are issued before the current one is consumed).  8 threads per
 // atom sum 4 partners each; slices are summed in order by k_mf_jt_fin.
 constexpr int kAB = 32;
-constexpr int kJS = 4;  // partner-block slices
+constexpr int kJSMax = 16;  // partner-block slices (gridDim.z of k_mf_jt, at most)
 
 __device__ __forceinline__ void jt_load(const double *__restrict__ Fi,
                                         const double *__restrict__ Ri, int n, int A0, int B0,
@@ -290,6 +291,14 @@ __device__ __forceinline__ void jt_load(const double *__restrict__ Fi,
   }
 }
 
+// partner-block slices of k_mf_jt (MLFF_MF_JS overrides, sweeps)
+int mf_jt_slices(int n) {
+  const int nblk = (n + kAB - 1) / kAB;
+  int js = 4;
+  if (const char *e = std::getenv("MLFF_MF_JS")) js = std::atoi(e);
+  return std::max(1, std::min({js, nblk, kJSMax}));
+}
+
 __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
                                                const double *__restrict__ F, int64_t D, int n,
                                                int64_t i0, int64_t row0, int64_t nrows,
@@ -309,8 +318,8 @@ __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
   const int al = threadIdx.x >> 3, pt = threadIdx.x & 7;
   const int a = A0 + al;
   const int nblk = (n + kAB - 1) / kAB;
-  const int bz0 = (int)(((int64_t)nblk * blockIdx.z) / kJS);
-  const int bz1 = (int)(((int64_t)nblk * (blockIdx.z + 1)) / kJS);
+  const int bz0 = (int)(((int64_t)nblk * blockIdx.z) / gridDim.z);
+  const int bz1 = (int)(((int64_t)nblk * (blockIdx.z + 1)) / gridDim.z);
   double acc[3] = {0.0, 0.0, 0.0};
   double f[4], r[4][3];
   int la[4], lb[4];
@@ -357,7 +366,8 @@ __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
 // of the CG step, on the kVecGrid grid-stride layout of k_dot_part (same terms, same
 // order: the separate dot launch it replaces gives the same bits)
 template <bool PQ>
-__global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ part, int64_t nrows,
+__global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ part, int js,
+                                                   int64_t nrows,
                                                    double sigma, double lam,
                                                    const double *__restrict__ xloc,
                                                    double *__restrict__ y,
@@ -369,8 +379,7 @@ __global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ pa
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows;
        r += (int64_t)gridDim.x * 256) {
     double s = 0.0;
-#pragma unroll
-    for (int z = 0; z < kJS; ++z) s += part[(int64_t)z * nrows + r];
+    for (int z = 0; z < js; ++z) s += part[(int64_t)z * nrows + r];
     double yv = sigma * s;
     if (xloc != nullptr) yv += lam * xloc[r];
     y[r] = yv;
@@ -424,7 +433,7 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   MLFF_HIP(ctx, hipMalloc(&mf.c, sizeof(double) * nic * MP));
   MLFF_HIP(ctx, hipMalloc(&mf.F, sizeof(double) * nic * D));
   if (ctx->world > 1) MLFF_HIP(ctx, hipMalloc(&mf.xc, sizeof(double) * ctx->N));
-  MLFF_HIP(ctx, hipMalloc(&mf.ypart, sizeof(double) * kJS * std::max<int64_t>(ctx->nrows, 1)));
+  MLFF_HIP(ctx, hipMalloc(&mf.ypart, sizeof(double) * kJSMax * std::max<int64_t>(ctx->nrows, 1)));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Rd, R_desc, sizeof(double) * M * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Rdd, R_d_desc, sizeof(double) * M * D * 3, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.Pt, Pt.data(), sizeof(int32_t) * n_perms * D, hipMemcpyHostToDevice, s));
@@ -464,6 +473,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   const MfData &mf = ctx->mf;
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
+  const int js = mf_jt_slices(mf.n);
   // on one rank the padded layout is the global index itself (rows_per = N)
   const double *xc = x_full;
   if (ctx->world > 1) {
@@ -473,7 +483,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   }
   if (mf.ni == 0) {  // no points here: Zt is not needed either
     if (pq_part != nullptr)  // zero partials of an empty shard
-      hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart,
+      hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js,
                          (int64_t)0, sigma, lam, x_loc, y_loc, pq_part, status);
     return;
   }
@@ -493,17 +503,17 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     hipLaunchKernelGGL(k_mf_h<4>, dim3((unsigned)dblk, (unsigned)((mf.ni + 3) / 4)), dim3(64), 0, s,
                        mf.Rd, mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   }
-  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, kJS),
+  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, (unsigned)js),
                      dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
                      mf.ypart, status);
   if (pq_part != nullptr) {
-    hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, ctx->nrows,
+    hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js, ctx->nrows,
                        sigma, lam, x_loc, y_loc, pq_part, status);
     return;
   }
   if (ctx->nrows <= 0) return;
   hipLaunchKernelGGL(k_mf_jt_fin<false>, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0,
-                     s, mf.ypart, ctx->nrows, sigma, lam, x_loc, y_loc, (double *)nullptr, status);
+                     s, mf.ypart, js, ctx->nrows, sigma, lam, x_loc, y_loc, (double *)nullptr, status);
 }
 
 // Training-set energies of the model with coefficients `alphas` (contiguous global
