@@ -464,6 +464,11 @@ FIXTURES = {
         ["cholesky", "random_scores", "lev_scores", "inverse_lev", "lev_random",
          "truncated_cholesky", "truncated_cholesky_custom", "rank_k_lev_scores",
          "rank_k_lev_scores_custom", "eigvec_precon"], seed=3, none_tol=(1e-4, 1e-6)),
+    # the two masked eigen preconditioners (iterative_solver.py:1238-1268) on the n270 geometry
+    "sgdml_n270_eigmask": lambda: fx_sgdml(
+        10, "sgdml_ethanol_n270_eigmask",
+        ["eigvec_precon_block_diagonal", "eigvec_precon_atomic_interactions"], seed=3,
+        with_K=False, none_tol=()),
     # a permutation GROUP (rotations of the methyl hydrogens), as sGDML's find_perms returns
     "sgdml_n270_perms": lambda: fx_sgdml(
         10, "sgdml_ethanol_n270_perms", ["cholesky", "random_scores", "truncated_cholesky_custom"],
