@@ -189,6 +189,9 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
 // One wave per (64 descriptor entries, IC query points); the coefficients of the
 // IC points are staged in LDS 64 pairs at a time.  IC = 4 when 16 would leave the
 // chip with too few waves (few query points: latency bound).
+// 1-D grid, XCD-aware: workgroups L and L + 8 share an XCD (round-robin dispatch), so the
+// point groups of one descriptor block get consecutive slots of one XCD and read its
+// Rt / Zt columns from that XCD's L2 instead of the fabric once per group.
 template <int IC>
 __global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
                                              const double *__restrict__ Rt,
@@ -201,8 +204,12 @@ __global__ __launch_bounds__(64) void k_mf_h(const double *__restrict__ Rd,
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sc[IC][64];
   __shared__ double sw[IC][64];
-  const int64_t d = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t ic0 = (int64_t)blockIdx.y * IC;
+  const int64_t gi = (ni + IC - 1) / IC;
+  const int64_t slot = blockIdx.x / 8, grp = slot % gi;
+  const int64_t dblock = (slot / gi) * 8 + blockIdx.x % 8;
+  if (dblock * 64 >= D) return;
+  const int64_t d = dblock * 64 + threadIdx.x;
+  const int64_t ic0 = grp * IC;
   const int nk = (int)((ni - ic0) < IC ? (ni - ic0) : IC);
   const bool act = d < D;
   double rdi[IC], h[IC];
@@ -299,27 +306,35 @@ int mf_jt_slices(int n) {
   return std::max(1, std::min({js, nblk, kJSMax}));
 }
 
+// 1-D grid of nblk x ni x js workgroups in molecule-major order, dealt to the XCDs in
+// contiguous eighths (workgroup L runs on XCD L mod 8): the 12 x js workgroups of one
+// point, which read each of its (F, Rdd) pairs twice, mostly share one XCD's L2.
 __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
                                                const double *__restrict__ F, int64_t D, int n,
-                                               int64_t i0, int64_t row0, int64_t nrows,
-                                               double *__restrict__ part,
+                                               int64_t i0, int64_t ni, int js, int64_t row0,
+                                               int64_t nrows, double *__restrict__ part,
                                                const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sF[kAB][kAB + 1];
   __shared__ double sR[3][kAB][kAB + 1];
-  const int A0 = blockIdx.x * kAB;
-  const int64_t i = i0 + blockIdx.y;
+  const int nblk = (n + kAB - 1) / kAB;
+  const int64_t total = (int64_t)nblk * ni * js, per = (total + 7) / 8;
+  const int64_t v = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (v >= total) return;
+  const int64_t il = v / ((int64_t)nblk * js);
+  const int zz = (int)((v / nblk) % js);
+  const int A0 = (int)(v % nblk) * kAB;
+  const int64_t i = i0 + il;
   const int64_t n3 = 3 * (int64_t)n;
   const int64_t gfirst = i * n3 + 3 * (int64_t)A0;
   const int64_t glast = i * n3 + 3 * (int64_t)(A0 + kAB < n ? A0 + kAB : n) - 1;
   if (glast < row0 || gfirst >= row0 + nrows) return;
-  const double *Fi = F + (int64_t)blockIdx.y * D;
+  const double *Fi = F + il * D;
   const double *Ri = Rdd + i * D * 3;
   const int al = threadIdx.x >> 3, pt = threadIdx.x & 7;
   const int a = A0 + al;
-  const int nblk = (n + kAB - 1) / kAB;
-  const int bz0 = (int)(((int64_t)nblk * blockIdx.z) / gridDim.z);
-  const int bz1 = (int)(((int64_t)nblk * (blockIdx.z + 1)) / gridDim.z);
+  const int bz0 = (int)(((int64_t)nblk * zz) / js);
+  const int bz1 = (int)(((int64_t)nblk * (zz + 1)) / js);
   double acc[3] = {0.0, 0.0, 0.0};
   double f[4], r[4][3];
   int la[4], lb[4];
@@ -357,7 +372,7 @@ __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
     for (int c = 0; c < 3; ++c) {
       const int64_t rr = i * n3 + 3 * (int64_t)a + c - row0;
       if (rr < 0 || rr >= nrows) continue;
-      part[(int64_t)blockIdx.z * nrows + rr] = acc[c];
+      part[(int64_t)zz * nrows + rr] = acc[c];
     }
   }
 }
@@ -495,17 +510,20 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                      mf.part, status, zs);
   hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
                      mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
-  const int64_t dblk = (mf.D + 63) / 64;
+  const int64_t dblk = (mf.D + 63) / 64, dblk8 = (dblk + 7) / 8 * 8;
   if (dblk * (int64_t)gi >= 4096) {
-    hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)dblk, gi), dim3(64), 0, s, mf.Rd, mf.Rt, mf.Zt,
-                       mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+    hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)(dblk8 * gi)), dim3(64), 0, s, mf.Rd, mf.Rt,
+                       mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   } else {
-    hipLaunchKernelGGL(k_mf_h<4>, dim3((unsigned)dblk, (unsigned)((mf.ni + 3) / 4)), dim3(64), 0, s,
+    hipLaunchKernelGGL(k_mf_h<4>, dim3((unsigned)(dblk8 * ((mf.ni + 3) / 4))), dim3(64), 0, s,
                        mf.Rd, mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   }
-  hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((mf.n + kAB - 1) / kAB), (unsigned)mf.ni, (unsigned)js),
-                     dim3(256), 0, s, mf.Rdd, mf.F, mf.D, mf.n, mf.i0, ctx->row0, ctx->nrows,
-                     mf.ypart, status);
+  {
+    const int64_t total = (int64_t)((mf.n + kAB - 1) / kAB) * mf.ni * js;
+    hipLaunchKernelGGL(k_mf_jt, dim3((unsigned)((total + 7) / 8 * 8)), dim3(256), 0, s, mf.Rdd,
+                       mf.F, mf.D, (int)mf.n, mf.i0, mf.ni, js, ctx->row0, ctx->nrows, mf.ypart,
+                       status);
+  }
   if (pq_part != nullptr) {
     hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js, ctx->nrows,
                        sigma, lam, x_loc, y_loc, pq_part, status);
