@@ -262,7 +262,8 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
 // part[ks * ldw + c] = sum_{j in slice ks} W[j, c] * (sum_sp tsrc[sp * tstride + j])
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
-                         const int *status, hipStream_t s, StopFold fold = StopFold{});
+                         const int *status, hipStream_t s, StopFold fold = StopFold{},
+                         int64_t cached_rows = 0);
 int choose_ksplit(int64_t k, int64_t ncols);
 // rho partials of r . r (no preconditioner)
 void launch_dot_part(const double *a, const double *b, int64_t n, double *part,

@@ -8,6 +8,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mlff {
 
@@ -54,34 +55,10 @@ __device__ __forceinline__ bool stop_prologue(const StopFold &f, double *sh) {
 }
 
 // ---------------------------------------------------------------------------
-// Dense row GEMV: y[row] = sigma * sum_c M[row, c] v[c] + lam * vloc[row]   (EPI=1)
-//                 part[split * out_stride + row] = sum_{c in split} M[row,c] v[c] (EPI=0)
-// R rows per workgroup share every 16-B load of v (v is L2 resident); M is
-// streamed once with non-temporal 16-B loads, U loads in flight per row.
-// `rows` of M must be allocated up to a multiple of R (padding rows are zero).
-template <int R, int U, int EPI, bool NT = true>
-__global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int64_t ld,
-                                              int64_t rows, int64_t n2, int64_t cs2,
-                                              const double *__restrict__ v,
-                                              double *__restrict__ out, int64_t out_stride,
-                                              double sigma, double lam,
-                                              const double *__restrict__ vloc,
-                                              const int *__restrict__ status, StopFold fold) {
-  if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sh[4 * R > 8 ? 4 * R : 8];
-  if (!stop_prologue(fold, sh)) return;
-  const int64_t r0 = (int64_t)blockIdx.x * R;
-  const int64_t c_begin = (int64_t)blockIdx.y * cs2;
-  int64_t c_end = c_begin + cs2;
-  if (c_end > n2) c_end = n2;
-  const d2 *__restrict__ v2 = reinterpret_cast<const d2 *>(v);
-  const d2 *rowp[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) rowp[r] = reinterpret_cast<const d2 *>(M + (r0 + r) * ld);
-  double acc[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.0;
-
+// the column range [c_begin, c_end) of R rows, dot v; NT: non-temporal loads of M
+template <int R, int U, bool NT>
+__device__ __forceinline__ void gemv_rows_body(const d2 *const (&rowp)[R], const d2 *__restrict__ v2,
+                                               int64_t c_begin, int64_t c_end, double (&acc)[R]) {
   int64_t c = c_begin + threadIdx.x;
   // main body: U full strides without bounds checks
   for (; c + (int64_t)(U - 1) * 256 < c_end; c += (int64_t)256 * U) {
@@ -111,6 +88,42 @@ __global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int6
       acc[r] = fma(kv.y, xv.y, acc[r]);
     }
   }
+}
+
+// Dense row GEMV: y[row] = sigma * sum_c M[row, c] v[c] + lam * vloc[row]   (EPI=1)
+//                 part[split * out_stride + row] = sum_{c in split} M[row,c] v[c] (EPI=0)
+// R rows per workgroup share every 16-B load of v (v is L2 resident); M is
+// streamed once with non-temporal 16-B loads, U loads in flight per row; rows below
+// `cached_rows` are read with default-policy loads even when NT (a panel's leading rows
+// stay in the MALL for the next pass, panel_cached_rows).
+// `rows` of M must be allocated up to a multiple of R (padding rows are zero).
+template <int R, int U, int EPI, bool NT = true>
+__global__ __launch_bounds__(256) void k_gemv(const double *__restrict__ M, int64_t ld,
+                                              int64_t rows, int64_t n2, int64_t cs2,
+                                              const double *__restrict__ v,
+                                              double *__restrict__ out, int64_t out_stride,
+                                              double sigma, double lam,
+                                              const double *__restrict__ vloc,
+                                              const int *__restrict__ status, StopFold fold,
+                                              int64_t cached_rows = 0) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[4 * R > 8 ? 4 * R : 8];
+  if (!stop_prologue(fold, sh)) return;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int64_t c_begin = (int64_t)blockIdx.y * cs2;
+  int64_t c_end = c_begin + cs2;
+  if (c_end > n2) c_end = n2;
+  const d2 *__restrict__ v2 = reinterpret_cast<const d2 *>(v);
+  const d2 *rowp[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) rowp[r] = reinterpret_cast<const d2 *>(M + (r0 + r) * ld);
+  double acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.0;
+  if (NT && r0 + R > cached_rows)
+    gemv_rows_body<R, U, true>(rowp, v2, c_begin, c_end, acc);
+  else
+    gemv_rows_body<R, U, false>(rowp, v2, c_begin, c_end, acc);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -189,6 +202,23 @@ int choose_zsplit(int64_t k, int64_t ncols) {
 constexpr double kPanelMallBytes = 192.0e6;
 bool panel_streams(int64_t k, int64_t ldt) { return 8.0 * (double)k * (double)ldt > kPanelMallBytes; }
 
+// A streamed panel's leading rows, up to kPanelCachedBytes, are still read with
+// default-policy loads by both passes (T r, T^T t): they stay in the MALL from one pass to
+// the next and from one iteration to the next, the rest streams (MLFF_PANEL_CACHE_MB
+// overrides the budget for sweeps).  Nanotube k = 2701 (336 MB), same box, interleaved:
+// 0 / 64 / 128 / 176 / 224 MB -> apply 5.93 / 6.03 / 6.11 / 6.11 / 6.17 TB/s, operator
+// unchanged up to 176 MB and 9 % slower at 224 MB (its tables lose the MALL)
+constexpr double kPanelCachedBytes = 128.0e6;
+int64_t panel_cached_rows(int64_t k, int64_t ldt) {
+  if (!panel_streams(k, ldt)) return k;
+  static const double budget = [] {
+    const char *e = std::getenv("MLFF_PANEL_CACHE_MB");
+    return e ? 1.0e6 * std::atof(e) : kPanelCachedBytes;
+  }();
+  const int64_t rows = (int64_t)(budget / (8.0 * (double)ldt));
+  return rows < k ? rows : k;
+}
+
 void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
                        const double *r, double *tpart, const int *status, hipStream_t s,
                        StopFold fold) {
@@ -202,7 +232,8 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
   // the operator's tables (panel_streams)
   if (panel_streams(k, ldt))
     hipLaunchKernelGGL((k_gemv<R, U, 0, true>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
-                       k, 1.0, 0.0, (const double *)nullptr, status, fold);
+                       k, 1.0, 0.0, (const double *)nullptr, status, fold,
+                       panel_cached_rows(k, ldt));
   else
     hipLaunchKernelGGL((k_gemv<R, U, 0, false>), grid, dim3(256), 0, s, T, ldt, k, n2, cs2, r, tpart,
                        k, 1.0, 0.0, (const double *)nullptr, status, fold);
@@ -214,27 +245,8 @@ void launch_gemv_split(const double *T, int64_t ldt, int64_t k, int64_t ncols, i
 // double2 per thread, the 4 waves read 4 KB of every row) x one slice of rows, so
 // a k x N panel is spread over ~1024 workgroups whatever its shape.
 template <bool NT>
-__global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__ W, int64_t ldw,
-                                                      int64_t k, const double *__restrict__ tsrc,
-                                                      int tsplits, int64_t tstride,
-                                                      int64_t kslice, double *__restrict__ part,
-                                                      const int *__restrict__ status,
-                                                      StopFold fold) {
-  if (status != nullptr && *status != ST_RUNNING) return;
-  extern __shared__ double t_sh[];
-  if (!stop_prologue(fold, t_sh)) return;
-  const int64_t j0 = (int64_t)blockIdx.y * kslice;
-  const int64_t j1 = (j0 + kslice) < k ? (j0 + kslice) : k;
-  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
-    double a = 0.0;
-    for (int sp = 0; sp < tsplits; ++sp) a += tsrc[(int64_t)sp * tstride + j];
-    t_sh[j - j0] = a;
-  }
-  __syncthreads();
-  const int64_t c2 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (2 * c2 >= ldw) return;
-  const d2 *w2 = reinterpret_cast<const d2 *>(W) + c2;
-  const int64_t ld2 = ldw / 2;
+__device__ __forceinline__ d2 colgemv_slice(const d2 *__restrict__ w2, int64_t ld2, int64_t j0,
+                                            int64_t j1, const double *t_sh) {
   d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
   int64_t j = j0;
   for (; j + 7 < j1; j += 8) {  // 8 rows (128 B per lane) in flight
@@ -257,7 +269,34 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
     acc0.x = fma(a0.x, t0, acc0.x);
     acc0.y = fma(a0.y, t0, acc0.y);
   }
-  reinterpret_cast<d2 *>(part + (int64_t)blockIdx.y * ldw)[c2] = acc0 + acc1;
+  return acc0 + acc1;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__ W, int64_t ldw,
+                                                      int64_t k, const double *__restrict__ tsrc,
+                                                      int tsplits, int64_t tstride,
+                                                      int64_t kslice, double *__restrict__ part,
+                                                      const int *__restrict__ status,
+                                                      StopFold fold, int64_t cached_rows) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  extern __shared__ double t_sh[];
+  if (!stop_prologue(fold, t_sh)) return;
+  const int64_t j0 = (int64_t)blockIdx.y * kslice;
+  const int64_t j1 = (j0 + kslice) < k ? (j0 + kslice) : k;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) {
+    double a = 0.0;
+    for (int sp = 0; sp < tsplits; ++sp) a += tsrc[(int64_t)sp * tstride + j];
+    t_sh[j - j0] = a;
+  }
+  __syncthreads();
+  const int64_t c2 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (2 * c2 >= ldw) return;
+  const d2 *w2 = reinterpret_cast<const d2 *>(W) + c2;
+  const int64_t ld2 = ldw / 2;
+  const d2 acc = (NT && j1 > cached_rows) ? colgemv_slice<true>(w2, ld2, j0, j1, t_sh)
+                                           : colgemv_slice<false>(w2, ld2, j0, j1, t_sh);
+  reinterpret_cast<d2 *>(part + (int64_t)blockIdx.y * ldw)[c2] = acc;
 }
 
 int choose_ksplit(int64_t k, int64_t ncols) {
@@ -273,16 +312,16 @@ int choose_ksplit(int64_t k, int64_t ncols) {
 
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
-                         const int *status, hipStream_t s, StopFold fold) {
+                         const int *status, hipStream_t s, StopFold fold, int64_t cached_rows) {
   const int64_t kslice = (k + ksplit - 1) / ksplit;
   const dim3 grid((unsigned)((ldw / 2 + 255) / 256), (unsigned)ksplit);
   const size_t shm = sizeof(double) * (kslice + 1 > 8 ? kslice + 1 : 8);
   if (panel_streams(k, ldw))
     hipLaunchKernelGGL(k_colgemv_part<true>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
-                       tstride, kslice, part, status, fold);
+                       tstride, kslice, part, status, fold, cached_rows);
   else
     hipLaunchKernelGGL(k_colgemv_part<false>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
-                       tstride, kslice, part, status, fold);
+                       tstride, kslice, part, status, fold, cached_rows);
 }
 
 // z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
@@ -321,7 +360,8 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
                      double *rho_part, const int *status, hipStream_t s, double *zpart,
                      int zsplit, StopFold fold) {
-  launch_colgemv_part(T, ldt, k, tpart, splits, k, zsplit, zpart, status, s, fold);
+  launch_colgemv_part(T, ldt, k, tpart, splits, k, zsplit, zpart, status, s, fold,
+                      panel_cached_rows(k, ldt));
   hipLaunchKernelGGL(k_precon_fin, dim3(kVecGrid), dim3(256), 0, s, zpart, zsplit, ldt, r, z, n,
                      sigma_p, lam_inv, rho_part, status);
 }
