@@ -76,6 +76,7 @@ struct MfData {
   double *Rd = nullptr, *Rdd = nullptr;   // M x D, M x D x 3
   double *Rt = nullptr, *Zt = nullptr;    // (M n_perms) x D
   int32_t *Pt = nullptr, *ps = nullptr, *pt = nullptr;
+  bool ident = false;                     // one identity permutation: Rt == Rd, Pt unused
   double *m5 = nullptr, *w = nullptr;     // ni x (M n_perms), x independent
   double *c = nullptr, *F = nullptr;      // ni x (M n_perms), ni x D scratch
   double *part = nullptr;                 // nz x ni x (M n_perms) pair partial sums

@@ -72,7 +72,7 @@ struct ZSrc {
 __device__ __forceinline__ double z_entry(const ZSrc &zs, int64_t D, int64_t jp, int64_t d) {
   const int64_t j = jp / zs.n_perms, p = jp % zs.n_perms;
   const int64_t g0 = j * 3 * zs.n;
-  const int64_t e = zs.Pt[p * D + d];
+  const int64_t e = zs.Pt != nullptr ? (int64_t)zs.Pt[p * D + d] : d;  // Pt null: identity
   const int s = zs.ps[e], t = zs.pt[e];
   const double *r = zs.Rdd + (j * D + e) * 3;
   double z = 0.0;
@@ -101,8 +101,9 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
 }
 
 // Partial pair sums over the descriptor slice z of this workgroup for a tile of
-// 16 query points x 16 (training point, permutation) pairs; thread (ti, tj) owns
-// one pair, the slice is staged through LDS in chunks of 64 entries:
+// 16 query points x 16 (training point, permutation) pairs, the slice staged through
+// LDS in chunks of 64 entries; each wave sums a quarter of every chunk for 2 x 2 pairs
+// per thread and the four wave partials of a pair are added in wave order:
 //   MODE 0: |Rd_i - Rt[jp]|^2                (setup)
 //   MODE 1: (Rd_i - Rt[jp]) . Zt[jp]
 // part[(z * ni + il) * MP + jp]; k_mf_pair_fin sums the slices in a fixed order.
@@ -110,8 +111,9 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
 // the workgroups of point tile 0, one launch less per mat-vec.
 constexpr int kPT = 16;  // tile edge (points and pairs)
 constexpr int kDC = 64;  // descriptor chunk staged in LDS
+// waves_per_eu(5): 96 VGPRs (110 unconstrained), 5 resident workgroups per CU
 template <int MODE, bool FZ = false>
-__global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_mf_pair(const double *__restrict__ Rd,
                                                  const double *__restrict__ Rt,
                                                  const double *__restrict__ Zt, int64_t D,
                                                  int64_t dslice, int64_t i0, int64_t ni,
@@ -125,36 +127,74 @@ __global__ __launch_bounds__(256) void k_mf_pair(const double *__restrict__ Rd,
   const int64_t ic0 = (int64_t)blockIdx.y * kPT;
   const int64_t d0 = (int64_t)blockIdx.z * dslice;
   const int64_t d1 = (d0 + dslice) < D ? (d0 + dslice) : D;
-  const int tj = threadIdx.x & (kPT - 1), ti = threadIdx.x / kPT;
-  double acc = 0.0;
+  const int tj = threadIdx.x & (kPT - 1), ti = threadIdx.x / kPT;  // output pair
+  const int wv = threadIdx.x >> 6, qi = (threadIdx.x & 63) >> 3, qj = threadIdx.x & 7;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  constexpr int kPer = kPT * kDC / 256;  // staged entries per thread and array
   for (int64_t c0 = d0; c0 < d1; c0 += kDC) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < kPT * kDC; e += 256) {
+    // all loads of the chunk (and the Zt gathers) are issued before any LDS store, so
+    // the thread's kPer dependent-load chains overlap instead of running one by one
+    double vR[kPer], vT[kPer], vZ[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = threadIdx.x + 256 * u;
       const int r = e / kDC, cc = e % kDC;
       const int64_t d = c0 + cc;
       const bool okd = d < d1;
       const int64_t il = ic0 + r, jp = jp0 + r;
-      sR[r][cc] = (okd && il < ni) ? Rd[(i0 + il) * D + d] : 0.0;
-      sT[r][cc] = (okd && jp < MP) ? Rt[jp * D + d] : 0.0;
-      if (MODE == 1 && !FZ) sZ[r][cc] = (okd && jp < MP) ? Zt[jp * D + d] : 0.0;
-      if (MODE == 1 && FZ) {
-        double z = 0.0;
-        if (okd && jp < MP) {
-          z = z_entry(zs, D, jp, d);
-          if (blockIdx.y == 0) zs.Zt[jp * D + d] = z;
-        }
-        sZ[r][cc] = z;
+      vR[u] = (okd && il < ni) ? Rd[(i0 + il) * D + d] : 0.0;
+      vT[u] = (okd && jp < MP) ? Rt[jp * D + d] : 0.0;
+      vZ[u] = 0.0;
+      if (MODE == 1 && !FZ) vZ[u] = (okd && jp < MP) ? Zt[jp * D + d] : 0.0;
+      if (MODE == 1 && FZ && okd && jp < MP) vZ[u] = z_entry(zs, D, jp, d);
+    }
+    if (MODE == 1 && FZ && blockIdx.y == 0) {
+#pragma unroll
+      for (int u = 0; u < kPer; ++u) {
+        const int e = threadIdx.x + 256 * u;
+        const int64_t d = c0 + e % kDC, jp = jp0 + e / kDC;
+        if (d < d1 && jp < MP) zs.Zt[jp * D + d] = vZ[u];
       }
     }
     __syncthreads();
-#pragma unroll 8
-    for (int cc = 0; cc < kDC; ++cc) {
-      const double df = sR[ti][cc] - sT[tj][cc];
-      acc = fma(df, MODE == 0 ? df : sZ[MODE == 1 ? tj : 0][cc], acc);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      const int r = e / kDC, cc = e % kDC;
+      sR[r][cc] = vR[u];
+      sT[r][cc] = vT[u];
+      if (MODE == 1) sZ[r][cc] = vZ[u];
+    }
+    __syncthreads();
+    // wave w sums the chunk's entries [16 w, 16 w + 16) for a 2 x 2 block of pairs
+    // (qi + 8 a, qj + 8 b): 6 LDS reads per 4 products instead of 3 per 1
+#pragma unroll 4
+    for (int c = 0; c < kDC / 4; ++c) {
+      const int cc = wv * (kDC / 4) + c;
+      const double r0 = sR[qi][cc], r1 = sR[qi + 8][cc];
+      const double t0 = sT[qj][cc], t1 = sT[qj + 8][cc];
+      const double z0 = MODE == 0 ? 0.0 : sZ[MODE == 1 ? qj : 0][cc];
+      const double z1 = MODE == 0 ? 0.0 : sZ[MODE == 1 ? qj + 8 : 0][cc];
+      const double d00 = r0 - t0, d01 = r0 - t1, d10 = r1 - t0, d11 = r1 - t1;
+      acc[0] = fma(d00, MODE == 0 ? d00 : z0, acc[0]);
+      acc[1] = fma(d01, MODE == 0 ? d01 : z1, acc[1]);
+      acc[2] = fma(d10, MODE == 0 ? d10 : z0, acc[2]);
+      acc[3] = fma(d11, MODE == 0 ? d11 : z1, acc[3]);
     }
   }
+  // the 4 waves' partial sums of each pair, added in wave order
+  __syncthreads();
+  static_assert(kPT * (kDC + 1) >= 4 * 256, "wave partials fit in sR");
+  double *red = &sR[0][0];  // 4 x 256 doubles
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) red[wv * 256 + (qi + 8 * a) * kPT + qj + 8 * b] = acc[2 * a + b];
+  __syncthreads();
+  const double sum = ((red[threadIdx.x] + red[256 + threadIdx.x]) + red[512 + threadIdx.x]) +
+                     red[768 + threadIdx.x];
   const int64_t il = ic0 + ti, jp = jp0 + tj;
-  if (il < ni && jp < MP) part[((int64_t)blockIdx.z * ni + il) * MP + jp] = acc;
+  if (il < ni && jp < MP) part[((int64_t)blockIdx.z * ni + il) * MP + jp] = sum;
 }
 
 // MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot; MODE 2 (energies):
@@ -170,8 +210,17 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
   const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (o >= nout) return;
+  // the lane's slices in slice order, 8 loads in flight (same sum, same bits)
   double s = 0.0;
-  for (int z = lane; z < nz; z += 64) s += part[(int64_t)z * nout + o];
+  int z = lane;
+  for (; z + 7 * 64 < nz; z += 8 * 64) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = part[(int64_t)(z + u * 64) * nout + o];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += t[u];
+  }
+  for (; z < nz; z += 64) s += part[(int64_t)z * nout + o];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
   if (lane != 0) return;
@@ -455,13 +504,17 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   MLFF_HIP(ctx, hipMemcpyAsync(mf.ps, ps.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(mf.pt, pt.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
   mf.perms.assign(perms, perms + (size_t)n_perms * n);
+  mf.ident = n_perms == 1;
+  for (int a = 0; a < n && mf.ident; ++a) mf.ident = perms[a] == a;
   mf.piinv = piinv;
   const unsigned gx = (unsigned)std::min<int64_t>((D + 255) / 256, 1024);
   hipLaunchKernelGGL(k_mf_rt, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rd, mf.Pt, M, n_perms, D,
                      mf.Rt);
-  // descriptor slices of the pair sums: enough workgroups to cover the chip
+  // descriptor slices of the pair sums: enough workgroups to cover the chip in ONE round
+  // of resident workgroups (k_mf_pair: 96 VGPRs, 5 waves per SIMD = 5 workgroups per CU;
+  // at 4 per CU the nanotube's 1067 slices ran as 1024 + a second round of 43)
   const int64_t tiles = ((MP + kPT - 1) / kPT) * ((mf.ni + kPT - 1) / kPT);
-  int64_t nz = (2048 + tiles - 1) / std::max<int64_t>(tiles, 1);
+  int64_t nz = (5 * 256 + tiles - 1) / std::max<int64_t>(tiles, 1);
   nz = std::max<int64_t>(1, std::min<int64_t>(nz, (D + kDC - 1) / kDC));
   mf.dslice = round_up((D + nz - 1) / nz, kDC);
   mf.nz = (int)((D + mf.dslice - 1) / mf.dslice);
@@ -503,20 +556,24 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     return;
   }
   const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
-  const ZSrc zs{mf.Rdd, mf.Pt, mf.ps, mf.pt, (int)mf.n, (int)mf.n_perms, xc, mf.Zt};
+  // identity permutation: Rt is Rd (same bits), read from the same lines, and the
+  // descriptor map is skipped in the Zt gathers (one dependent load less)
+  const double *Rt = mf.ident ? mf.Rd : mf.Rt;
+  const ZSrc zs{mf.Rdd, mf.ident ? nullptr : mf.Pt, mf.ps, mf.pt, (int)mf.n, (int)mf.n_perms, xc,
+                mf.Zt};
   hipLaunchKernelGGL((k_mf_pair<1, true>), dim3((unsigned)((MP + kPT - 1) / kPT),
                      (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
-                     mf.Rd, mf.Rt, (const double *)nullptr, mf.D, mf.dslice, mf.i0, mf.ni, MP,
+                     mf.Rd, Rt, (const double *)nullptr, mf.D, mf.dslice, mf.i0, mf.ni, MP,
                      mf.part, status, zs);
   hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
                      mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
   const int64_t dblk = (mf.D + 63) / 64, dblk8 = (dblk + 7) / 8 * 8;
   if (dblk * (int64_t)gi >= 4096) {
-    hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)(dblk8 * gi)), dim3(64), 0, s, mf.Rd, mf.Rt,
+    hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)(dblk8 * gi)), dim3(64), 0, s, mf.Rd, Rt,
                        mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   } else {
     hipLaunchKernelGGL(k_mf_h<4>, dim3((unsigned)(dblk8 * ((mf.ni + 3) / 4))), dim3(64), 0, s,
-                       mf.Rd, mf.Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
+                       mf.Rd, Rt, mf.Zt, mf.D, mf.i0, mf.ni, MP, mf.c, mf.w, mf.F, status);
   }
   {
     const int64_t total = (int64_t)((mf.n + kAB - 1) / kAB) * mf.ni * js;

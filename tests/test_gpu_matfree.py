@@ -248,5 +248,8 @@ def test_matfree_ragged_shards(sg, golden_dir, m, world):
         assert res.info == 0 and res.iters == outs[0][2].iters
     assert ref[2].info == 0
     x = np.concatenate([o[2].x for o in outs])
-    assert abs(outs[0][2].iters - ref[2].iters) <= 2
+    # iteration counts: the parity contract's 10 % (>= 3); at m = 2 the counts over
+    # W = 1, 2, 5, 7, 8 spread over 66-70 with either summation order of the pair sums
+    # (scripts/dev/diag_ragged_iters.py)
+    assert abs(outs[0][2].iters - ref[2].iters) <= max(3, 0.1 * ref[2].iters)
     assert np.linalg.norm(x - ref[2].x) <= 1e-6 * np.linalg.norm(ref[2].x)
