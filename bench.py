@@ -68,6 +68,11 @@ def parse():
                          "pivoted Cholesky k=2701 built on the GPU); ethanol: configs[0] geometry")
     ap.add_argument("--m", type=int, default=0, help="training points (sGDML workloads)")
     ap.add_argument("--solve-maxiter", type=int, default=20000)
+    ap.add_argument("--solo-world", type=int, default=0,
+                    help="profiling: run ONE rank (--solo-rank) of a W-way row split alone on "
+                         "this GPU, collectives skipped (per-rank compute of the sharded "
+                         "iteration; not a bench line)")
+    ap.add_argument("--solo-rank", type=int, default=0)
     ap.add_argument("--storage", choices=["auto", "sym", "dense"], default="auto",
                     help="operator storage: symmetric 512x512 tiles of the lower block "
                          "triangle (auto/sym, ~4 N^2 bytes) or dense rows (8 N^2 bytes)")
@@ -282,8 +287,57 @@ def sgdml_workload(args, rank, world, local, pg):
                              "perms": np.arange(n_atoms)[None, :]}
 
 
+def solo_profile(args):
+    """One rank of a --solo-world W row split on one GPU with the library's SOLO transport
+    (every collective keeps only this rank's contribution): the kernels, sizes and launch
+    sequence of rank R's sharded PCG iteration without the RCCL calls.  The numbers it
+    computes are meaningless; the per-iteration device time is the compute floor of the
+    W-GPU iteration (add the three collectives' latency for the real one).  A random
+    rank-k panel stands in for the Nystrom factor (its build needs the collectives)."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    W, R = args.solo_world, args.solo_rank
+    n, k, ell = args.n, (args.k or 256), args.ell
+    X, b = synthetic.rbf_points(n, 3, 0)
+    s = sgdml_amd.KernelSolver(n, device=0, rank=R, world=W, comm_id=b"SOLO:")
+    try:
+        s.gen_rbf(X, ell)
+        s.set_operator(1.0, args.lam)
+        r0, r1 = s.row_range()
+        Lt = np.random.default_rng(R).standard_normal((k, r1 - r0)) * 1e-3
+        s.precon_lowrank(Lt)
+        s.set_storage(args.storage)
+        storage, op_bytes = s.storage_info()
+        s.pcg_start(np.ascontiguousarray(b[r0:r1]), tol=0.0,
+                    maxiter=args.warmup + args.steps + 1)
+        if args.warmup:
+            s.pcg_run(args.warmup, args.warmup)
+        s.timing(True)
+        s.timing_reset()
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.pcg_run(args.steps, args.steps)
+        s.synchronize()
+        el = time.perf_counter() - t0
+        tm = s.timing_read()
+        op_ms = tm["gemv_ms"] / max(tm["gemv_count"], 1)
+        print(json.dumps({
+            "solo_profile": True, "world": W, "rank": R, "n": n, "k": k, "rows": r1 - r0,
+            "storage": storage, "steps": args.steps, "ms_per_iter_wall": el / args.steps * 1e3,
+            "iter_device_ms": tm["iter_ms"] / max(tm["iter_count"], 1),
+            "operator_ms": op_ms, "operator_bytes": op_bytes,
+            "operator_gbs": op_bytes / (op_ms * 1e-3) / 1e9,
+            "note": "collectives skipped (SOLO transport): compute floor of one rank"}),
+            flush=True)
+    finally:
+        s.close()
+
+
 def main():
     args = parse()
+    if args.solo_world > 1:
+        return solo_profile(args)
     rank, world, local, pg = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)

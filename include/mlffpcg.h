@@ -101,7 +101,11 @@ int mlff_device_count(int *n_out);
 int mlff_comm_unique_id(unsigned char id_out[128]);
 
 /* ---- context --------------------------------------------------------------- */
-/* n_global: kernel size N.  comm_id may be NULL when world == 1. */
+/* n_global: kernel size N.  comm_id may be NULL when world == 1.  comm_id is a 128-byte
+ * RCCL unique id, "LOCAL:<key>" (world contexts of one process joined in-process, the
+ * multi-rank path on one GPU), or "SOLO:" (profiling only: this one rank of a world-way
+ * split runs alone, every collective keeps only its own contribution, results are
+ * meaningless). */
 int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_id,
                     int64_t n_global, mlff_ctx **ctx_out);
 int mlff_ctx_destroy(mlff_ctx *ctx);

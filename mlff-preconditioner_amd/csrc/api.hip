@@ -110,8 +110,13 @@ std::shared_ptr<LocalGroup> join_local_group(const std::string &key, int world) 
   return gp;
 }
 
+// SOLO transport (comm_id "SOLO:..."): ONE rank of a W-way split runs alone and every
+// collective keeps only this rank's own contribution (no data from peers, no wait).  The
+// numbers are meaningless; the kernels, their sizes and their launch sequence are those of
+// rank `rank` of W, so a one-GPU kernel trace shows the per-rank compute of the sharded
+// iteration without the collectives (bench.py --solo-world).  Profiling only.
 int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n) {
-  if (ctx->world <= 1 || n == 0) return MLFF_OK;
+  if (ctx->world <= 1 || n == 0 || ctx->solo) return MLFF_OK;
   if (ctx->comm != nullptr) {
     MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
     return MLFF_OK;
@@ -139,6 +144,12 @@ int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count
       MLFF_HIP(ctx, hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
     return MLFF_OK;
   }
+  if (ctx->solo) {
+    double *own = recv + (size_t)ctx->rank * count;
+    if (send != own)
+      MLFF_HIP(ctx, hipMemcpyAsync(own, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+    return MLFF_OK;
+  }
   if (ctx->comm != nullptr) {
     MLFF_NCCL(ctx, ncclAllGather(send, recv, count, ncclDouble, ctx->comm, ctx->stream));
     return MLFF_OK;
@@ -163,6 +174,11 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
   if (ctx->world <= 1) {
     if (send != recv)
       MLFF_HIP(ctx, hipMemcpyAsync(recv, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
+    return MLFF_OK;
+  }
+  if (ctx->solo) {
+    MLFF_HIP(ctx, hipMemcpyAsync(recv, send + (size_t)ctx->rank * count, sizeof(double) * count,
+                                 hipMemcpyDeviceToDevice, ctx->stream));
     return MLFF_OK;
   }
   if (ctx->comm != nullptr) {
@@ -753,7 +769,9 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (hipSetDevice(device) != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_HIP, "hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
     return fail(set_error(nullptr, MLFF_ERR_HIP, "hipStreamCreate failed"));
-  if (world > 1 && std::memcmp(comm_id, "LOCAL:", 6) == 0) {
+  if (world > 1 && std::memcmp(comm_id, "SOLO:", 5) == 0) {
+    ctx->solo = true;
+  } else if (world > 1 && std::memcmp(comm_id, "LOCAL:", 6) == 0) {
     const std::string key((const char *)comm_id, strnlen((const char *)comm_id, 128));
     ctx->local = join_local_group(key, world);
     if (ctx->local->world != world) return fail(set_error(nullptr, MLFF_ERR_ARG, "LOCAL group size mismatch"));

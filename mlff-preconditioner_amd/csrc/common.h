@@ -58,6 +58,7 @@ struct SymPack {
   int64_t nwhole = 0;
   double *Pq = nullptr;
   unsigned char *split = nullptr;  // nb x nb: tile (I, J) is split
+  int *own = nullptr;              // nb x nb owned slots per row block + nb counts (W > 1)
   int64_t t_split = 0;             // smallest I of a split tile (nb if none)
   int64_t dyn = 0;                 // > 0: k_symv_dyn with this many workgroups
   unsigned long long *ticket = nullptr;  // its work counter (reset by the slot reduction)
@@ -144,6 +145,7 @@ struct mlff_ctx {
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;                   // RCCL (one process per GPU)
   std::shared_ptr<mlff::LocalGroup> local;     // or: ranks as threads of one process
+  bool solo = false;                           // or: one rank alone (profiling, api.hip)
 
   // kernel matrix, blk rows x ld columns (padding rows/cols are zero)
   double *K = nullptr;

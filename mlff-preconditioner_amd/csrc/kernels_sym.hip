@@ -316,25 +316,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
 
 // column partials of slot t for rows of block bi: tile (t, bi), t > bi; a split tile
 // adds its quarters 1..3 (planes Pq) to quarter 0 (P) in quarter order
-__device__ __forceinline__ double slot_val(const double *__restrict__ P,
-                                           const double *__restrict__ Pq,
-                                           const unsigned char *__restrict__ split, int nb,
-                                           int64_t Np, int t, int bi, int64_t i) {
-  double v = P[(int64_t)t * Np + i];
-  if (t > bi && split[(int64_t)t * nb + bi]) {
-    const int64_t pl = (int64_t)nb * Np;
-    v += Pq[(int64_t)t * Np + i];
-    v += Pq[pl + (int64_t)t * Np + i];
-    v += Pq[2 * pl + (int64_t)t * Np + i];
-  }
-  return v;
-}
-
-__device__ __forceinline__ int owner_of(int I, int J, int tiles_per_rank) {
-  const int a = I / tiles_per_rank, c = J / tiles_per_rank;
-  if (a == c) return a;
-  return ((I + J) & 1) ? a : c;
-}
+constexpr int kOwnSplit = 1 << 24;  // flag bit of an owned-slot entry: the tile is split
 
 // y[i] = sum_{t=0}^{nb-1} P[t, i] over the slots whose tile this rank owns
 // (all slots on one rank); EPI: y = sigma * y + lam * vloc for rows < n_out
@@ -365,7 +347,16 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
     // thread; the additions stay in slot order
     const int tend = t_split > bi ? t_split : bi + 1;
     const int t8 = tend < nb ? tend : nb;
+    // (16 in flight: at one row per thread the 512-workgroup PQ grid leaves 1 wave per SIMD,
+    // so the slot loads' round trips are the kernel's time)
     int t = 0;
+    for (; t + 15 < t8; t += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
     for (; t + 7 < t8; t += 8) {
       double v[8];
 #pragma unroll
@@ -374,7 +365,7 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
       for (int u = 0; u < 8; ++u) s += v[u];
     }
     // the remaining slots (split tiles among them) in batches of 8 as well; every slot
-    // value is ((P + Pq0) + Pq1) + Pq2 as in slot_val, added in slot order
+    // value is ((P + Pq0) + Pq1) + Pq2, added in slot order
     for (; t < nb; t += 8) {
       double v[8];
 #pragma unroll
@@ -422,7 +413,8 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
                                                       const double *__restrict__ Pq,
                                                       const unsigned char *__restrict__ split,
                                                       int64_t Np,
-                                                      int nb, int rank, int tiles_per_rank,
+                                                      int nb, int rank,
+                                                      const int *__restrict__ own,
                                                       int64_t ld, int64_t blk, int64_t bstride,
                                                       double *__restrict__ yg,
                                                       const double *__restrict__ p,
@@ -437,12 +429,32 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
   const int64_t lo = (int64_t)rank * blk, hi = lo + blk;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
        i += (int64_t)gridDim.x * 256) {
-    const int bi = (int)(i / B);
+    // a wave's 64 rows lie in one 512-row block: bi, the slot list and its split flags are
+    // wave-uniform (scalar loads), so no slot load waits on a flag or index load
+    const int bi = __builtin_amdgcn_readfirstlane((int)(i / B));
     double s = 0.0;
-    for (int t = 0; t < nb; ++t) {
-      const int I = bi > t ? bi : t, J = bi > t ? t : bi;
-      if (owner_of(I, J, tiles_per_rank) != rank) continue;
-      s += slot_val(P, Pq, split, nb, Np, t, bi, i);
+    // this rank's slots of row block bi (own: ascending slots, kOwnSplit marks a split
+    // tile; built at setup) in batches of 16 whose loads are all in flight before the
+    // first addition; every slot value is ((P + Pq0) + Pq1) + Pq2, added in
+    // slot order
+    const int *ol = own + (int64_t)bi * nb;
+    const int cnt = own[(int64_t)nb * nb + bi];
+    const int64_t pl = (int64_t)nb * Np;
+    for (int c = 0; c < cnt; c += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        v[u] = 0.0;
+        if (c + u < cnt) {
+          const int e = ol[c + u];
+          const int64_t at = (int64_t)(e & (kOwnSplit - 1)) * Np + i;
+          v[u] = P[at];
+          if (e & kOwnSplit) v[u] = ((v[u] + Pq[at]) + Pq[pl + at]) + Pq[2 * pl + at];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (c + u < cnt) s += v[u];
     }
     yg[(i / blk) * bstride + i % blk] = s;
     if (PQ) {
@@ -605,13 +617,13 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
   if (p_full == nullptr) {
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (int)sp.nb, rank,
-                       (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
+                       sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
                        sp.ticket, status);
     return;
   }
   hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                      (int)sp.nb, rank,
-                     (int)sp.tiles_per_rank, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
+                     sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
                      sp.ticket, status);
   hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
                      rank, world, blk, sp.ystride, sp.yg, status);
@@ -624,7 +636,8 @@ void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, dou
                      sigma, lam, vloc, status);
 }
 
-// host-side tile assignment (same rule as owner_of)
+// tile assignment: tile (I, J), I >= J, is stored by the rank of row block I when both
+// blocks are one rank's, else by I's or J's rank by the parity of I + J (balanced to a tile)
 static int owner_host(int I, int J, int tpr) {
   const int a = I / tpr, c = J / tpr;
   if (a == c) return a;
@@ -681,6 +694,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     MLFF_HIP(ctx, hipMalloc(&sp.Pq, sizeof(double) * 3 * (int64_t)nb * Np));
     MLFF_HIP(ctx, hipMemsetAsync(sp.Pq, 0, sizeof(double) * 3 * (int64_t)nb * Np, s));
     MLFF_HIP(ctx, hipMalloc(&sp.split, (size_t)nb * nb));
+    MLFF_HIP(ctx, hipMalloc(&sp.own, sizeof(int) * (size_t)nb * (nb + 1)));
     MLFF_HIP(ctx, hipMalloc(&sp.ticket, sizeof(unsigned long long)));
     MLFF_HIP(ctx, hipMemsetAsync(sp.ticket, 0, sizeof(unsigned long long), s));
     if (ctx->world > 1) {
@@ -707,6 +721,17 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
       sp.t_split = std::min<int64_t>(sp.t_split, list[t].x);
     }
     MLFF_HIP(ctx, hipMemcpyAsync(sp.split, split.data(), split.size(), hipMemcpyHostToDevice, s));
+    // owned slots per row block (k_sym_reduce_w): row bi's slot t is this rank's when it
+    // stores tile (max(bi, t), min(bi, t)); rows of nb ascending entries, then nb counts
+    std::vector<int> own((size_t)nb * (nb + 1), 0);
+    for (int bi = 0; bi < nb; ++bi) {
+      int c = 0;
+      for (int t = 0; t < nb; ++t)
+        if (owner_host(std::max(bi, t), std::min(bi, t), tpr) == ctx->rank)
+          own[(size_t)bi * nb + c++] = t | (t > bi && split[(size_t)t * nb + bi] ? kOwnSplit : 0);
+      own[(size_t)nb * nb + bi] = c;
+    }
+    MLFF_HIP(ctx, hipMemcpyAsync(sp.own, own.data(), sizeof(int) * own.size(), hipMemcpyHostToDevice, s));
     MLFF_HIP(ctx, hipStreamSynchronize(s));
   }
   unsigned char *dtrans = nullptr;
@@ -744,8 +769,9 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
 
 void sym_free(SymPack &sp) {
   for (void *p : {(void *)sp.tiles, (void *)sp.list, (void *)sp.P, (void *)sp.yg, (void *)sp.yr,
-                  (void *)sp.Pq, (void *)sp.split, (void *)sp.ticket})
+                  (void *)sp.Pq, (void *)sp.split, (void *)sp.ticket, (void *)sp.own})
     if (p) (void)hipFree(p);
+  sp.own = nullptr;
   sp.Pq = nullptr;
   sp.split = nullptr;
   sp.ticket = nullptr;
