@@ -458,9 +458,20 @@ __global__ __launch_bounds__(256) void k_update_p_gathered(const double *__restr
   if (*status != ST_RUNNING) return;
   __shared__ double sh[8];
   double v = 0.0;
+  // the thread's partials (world * kVecGrid / 256 of them) in order, 8 loads in flight
   const int np = world * kVecGrid;
-  for (int f = threadIdx.x; f < np; f += 256)
-    v += gb[(int64_t)(f / kVecGrid) * gstride + blk + (f % kVecGrid)];
+  int f = threadIdx.x;
+  for (; f + 7 * 256 < np; f += 8 * 256) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int g = f + u * 256;
+      t[u] = gb[(int64_t)(g / kVecGrid) * gstride + blk + (g % kVecGrid)];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; f < np; f += 256) v += gb[(int64_t)(f / kVecGrid) * gstride + blk + (f % kVecGrid)];
   v = block_sum256(v, sh);
   __syncthreads();
   if (threadIdx.x == 0) sh[4] = v;
