@@ -95,25 +95,59 @@ __global__ __launch_bounds__(256) void k_piv_rank_winner(const double *__restric
   }
 }
 
-// global winner over ranks; swap; pivot; owner writes Lt[m, m_pi] and the pivot row
+// global winner over ranks; swap; pivot; owner writes Lt[m, m_pi] and the pivot row.
+// Single rank (pv != nullptr): the per-workgroup winners pv/pp are reduced here, in the
+// same total order as k_piv_rank_winner, so the pivot is the same without that launch.
+// xunit != nullptr: sets e_{m_pi} in the padded global layout (matrix-free column fetch).
 __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__ wins, int world,
+                                                      const double *__restrict__ pv,
+                                                      const long long *__restrict__ pp, int np,
                                                       int64_t *__restrict__ perm, int64_t m,
                                                       int64_t row0, int64_t nrows,
                                                       double *__restrict__ Lt, int64_t ldl,
                                                       int *__restrict__ pivflag,
                                                       double *__restrict__ prow,
+                                                      double *__restrict__ xunit,
+                                                      int64_t rows_per, int64_t blk,
                                                       DevState *st) {
+  __shared__ double sv[256];
+  __shared__ long long sp[256];
   __shared__ long long s_mpi;
   __shared__ double s_sq;
+  if (pv != nullptr) {  // block-uniform branch
+    double bv = -INFINITY;
+    long long bp = LLONG_MAX;
+    for (int t = threadIdx.x; t < np; t += 256)
+      if (better(pv[t], pp[t], bv, bp)) {
+        bv = pv[t];
+        bp = pp[t];
+      }
+    sv[threadIdx.x] = bv;
+    sp[threadIdx.x] = bp;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o)
+        if (better(sv[threadIdx.x + o], sp[threadIdx.x + o], sv[threadIdx.x], sp[threadIdx.x])) {
+          sv[threadIdx.x] = sv[threadIdx.x + o];
+          sp[threadIdx.x] = sp[threadIdx.x + o];
+        }
+      __syncthreads();
+    }
+  }
   if (threadIdx.x == 0) {
     double bv = -INFINITY;
     long long bp = LLONG_MAX;
-    for (int r = 0; r < world; ++r) {
-      const double v = wins[2 * r];
-      const long long p = (long long)wins[2 * r + 1];
-      if (better(v, p, bv, bp)) {
-        bv = v;
-        bp = p;
+    if (pv != nullptr) {
+      bv = sv[0];
+      bp = sp[0];
+    } else {
+      for (int r = 0; r < world; ++r) {
+        const double v = wins[2 * r];
+        const long long p = (long long)wins[2 * r + 1];
+        if (better(v, p, bv, bp)) {
+          bv = v;
+          bp = p;
+        }
       }
     }
     long long mpi = -1;
@@ -132,6 +166,7 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
     st->sqrt_piv = sq;
     s_mpi = mpi;
     s_sq = sq;
+    if (xunit != nullptr && mpi >= 0) xunit[(mpi / rows_per) * blk + mpi % rows_per] = 1.0;
   }
   __syncthreads();
   const long long mpi = s_mpi;
@@ -158,11 +193,14 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
                                                  double *__restrict__ Lt, int64_t ldl,
                                                  const int *__restrict__ pivflag,
                                                  double *__restrict__ dwork,
-                                                 const DevState *__restrict__ st) {
+                                                 const DevState *__restrict__ st,
+                                                 double *__restrict__ xunit) {
   const long long mpi = st->m_pi;
   if (mpi < 0) return;
   const double sq = st->sqrt_piv;
   const int64_t pos = (mpi / rows_per) * blk + (mpi % rows_per);
+  // clears e_{m_pi} set by k_piv_finalize (the operator that read it ran before this kernel)
+  if (xunit != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xunit[pos] = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrows;
        i += (int64_t)gridDim.x * 256) {
     if (pivflag[i]) continue;
@@ -226,26 +264,30 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   for (int64_t m = 0; m < k; ++m) {
     hipLaunchKernelGGL(k_piv_argmax, dim3(np), dim3(256), 0, s, ctx->dwork, ctx->perm, N, m,
                        ctx->row0, nrows, pv, pp);
-    double *my = wins + 2 * ctx->rank;
-    hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
-    if (ctx->world > 1) MLFF_TRY(comm_allgather(ctx, my, wins, 2));
-    hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world, ctx->perm, m,
-                       ctx->row0, nrows, ctx->T, blk, ctx->pivflag, ctx->prow, ctx->st);
-    if (ctx->world > 1 && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
-    if (mfcols) {
-      hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
-                         ctx->st, 1.0);
-      launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
-      hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
-                         ctx->st, 0.0);
+    const bool multi = ctx->world > 1;
+    if (multi) {
+      double *my = wins + 2 * ctx->rank;
+      hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
+      MLFF_TRY(comm_allgather(ctx, my, wins, 2));
     }
+    double *xunit = mfcols ? ctx->xg : nullptr;
+    hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world,
+                       multi ? nullptr : (const double *)pv,
+                       multi ? nullptr : (const long long *)pp, np, ctx->perm, m, ctx->row0,
+                       nrows, ctx->T, blk, ctx->pivflag, ctx->prow, xunit, ctx->rows_per, blk,
+                       ctx->st);
+    if (multi && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
+    if (mfcols) launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
     const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
     if (ks > 0)
       launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s);
     if (gcol > 0)
       hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
                        (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
-                       ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st);
+                       ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st, xunit);
+    else if (mfcols)
+      hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
+                         ctx->st, 0.0);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
   }
   MLFF_HIP(ctx, hipGetLastError());
