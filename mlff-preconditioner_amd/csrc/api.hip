@@ -39,6 +39,46 @@ int set_error(mlff_ctx *ctx, int code, const std::string &msg) {
 
 void local_abort(mlff_ctx *ctx);
 
+int api_exception(mlff_ctx *ctx, int code, const char *what) {
+  try {
+    local_abort(ctx);
+    return set_error(ctx, code, std::string("C++ exception in libmlffpcg: ") + (what ? what : ""));
+  } catch (...) {
+    return code;
+  }
+}
+
+ScratchScope::ScratchScope(mlff_ctx *c) : ctx(c), chunk(c->scratch_cur), off(c->scratch_off) {}
+
+ScratchScope::~ScratchScope() {
+  ctx->scratch_cur = chunk;
+  ctx->scratch_off = off;
+}
+
+int scratch_get(mlff_ctx *ctx, size_t bytes, void **out) {
+  constexpr size_t kAlign = 256, kChunk = size_t(64) << 20;
+  bytes = (bytes + kAlign - 1) / kAlign * kAlign;
+  auto &ch = ctx->scratch_chunks;
+  while (true) {
+    if (ctx->scratch_cur < ch.size()) {
+      const auto &c = ch[ctx->scratch_cur];
+      if (ctx->scratch_off + bytes <= c.size) {
+        *out = c.p + ctx->scratch_off;
+        ctx->scratch_off += bytes;
+        return MLFF_OK;
+      }
+      ++ctx->scratch_cur;  // the rest of this chunk stays unused until the scope closes
+      ctx->scratch_off = 0;
+      continue;
+    }
+    void *p = nullptr;
+    MLFF_HIP(ctx, hipMalloc(&p, std::max(bytes, kChunk)));
+    ch.push_back({static_cast<char *>(p), std::max(bytes, kChunk)});
+    ctx->scratch_cur = ch.size() - 1;
+    ctx->scratch_off = 0;
+  }
+}
+
 // A device failure on one rank of an in-process group aborts the group, so its peers
 // return MLFF_ERR_COMM from their next collective instead of waiting forever.
 int hip_check(mlff_ctx *ctx, hipError_t e, const char *what) {
@@ -295,9 +335,9 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
 // sign test is done by attempting the factorization: a successful Cholesky of
 // M - 1e-15 I certifies lo_eig > 0 up to rounding; otherwise M + 1e-15 I is used.
 int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
+  ScratchScope scope(ctx);
   double *tmp = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&tmp, sizeof(double) * k * k, ctx->stream));
-  ScratchFree scratch{ctx->stream, {tmp}};
+  MLFF_TRY(scratch_alloc(ctx, &tmp, k * k));
   MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
   launch_add_diag(tmp, k, -1e-15, ctx->stream);
   int rc = potrf_lower(ctx, tmp, k);
@@ -315,9 +355,9 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
 // Woodbury panel from a wide factor W = L^T (k x blk) in place:
 //   G = lam I + W W^T; L2 = chol(G); W <- L2^-1 W   (iterative_cholesky.py:141-143)
 int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
+  ScratchScope scope(ctx);
   double *G = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, ctx->stream));
-  ScratchFree scratch{ctx->stream, {G}};
+  MLFF_TRY(scratch_alloc(ctx, &G, k * k));
   MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
   launch_add_diag(G, k, ctx->lam, ctx->stream);
@@ -365,12 +405,12 @@ int fetch_cols(mlff_ctx *ctx, const int64_t *didx, int64_t k, double *W, int64_t
 int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant, double lam,
                   double *W) {
   hipStream_t s = ctx->stream;
+  ScratchScope scope(ctx);
   int64_t *didx = nullptr;
   double *Smm = nullptr, *G = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&didx, sizeof(int64_t) * k, s));
-  MLFF_HIP(ctx, hipMallocAsync(&Smm, sizeof(double) * k * k, s));
-  MLFF_HIP(ctx, hipMallocAsync(&G, sizeof(double) * k * k, s));
-  ScratchFree scratch{s, {didx, Smm, G}};
+  MLFF_TRY(scratch_alloc(ctx, &didx, k));
+  MLFF_TRY(scratch_alloc(ctx, &Smm, k * k));
+  MLFF_TRY(scratch_alloc(ctx, &G, k * k));
   MLFF_HIP(ctx, hipMemcpyAsync(didx, idx_host, sizeof(int64_t) * k, hipMemcpyHostToDevice, s));
   // K_nm^T (sign convention S = sigma_K K; sign flips cancel in B^T B)
   MLFF_TRY(fetch_cols(ctx, didx, k, W, ctx->blk));
@@ -715,6 +755,7 @@ extern "C" {
 int mlff_version(void) { return 100; }
 
 int mlff_device_count(int *n_out) {
+  MLFF_API_BEGIN
   if (n_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null pointer");
   int n = 0;
   const hipError_t e = hipGetDeviceCount(&n);
@@ -724,15 +765,18 @@ int mlff_device_count(int *n_out) {
   }
   *n_out = n;
   return MLFF_OK;
+  MLFF_API_END(nullptr)
 }
 
 int mlff_comm_unique_id(unsigned char id_out[128]) {
+  MLFF_API_BEGIN
   if (id_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null pointer");
   ncclUniqueId id;
   MLFF_NCCL(nullptr, ncclGetUniqueId(&id));
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   std::memcpy(id_out, &id, 128);
   return MLFF_OK;
+  MLFF_API_END(nullptr)
 }
 
 const char *mlff_last_error(mlff_ctx *ctx) {
@@ -742,6 +786,7 @@ const char *mlff_last_error(mlff_ctx *ctx) {
 
 int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_id,
                     int64_t n_global, mlff_ctx **ctx_out) {
+  MLFF_API_BEGIN
   if (ctx_out == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx_out");
   *ctx_out = nullptr;
   if (world < 1 || rank < 0 || rank >= world) return set_error(nullptr, MLFF_ERR_ARG, "bad rank/world");
@@ -814,9 +859,11 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (hipDeviceSynchronize() != hipSuccess) return fail(set_error(nullptr, MLFF_ERR_HIP, "init sync failed"));
   *ctx_out = ctx;
   return MLFF_OK;
+  MLFF_API_END(nullptr)
 }
 
 int mlff_ctx_destroy(mlff_ctx *ctx) {
+  MLFF_API_BEGIN
   if (ctx == nullptr) return MLFF_OK;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
@@ -825,6 +872,8 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart_base,
                   (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->gb})
     dev_free(p);
+  for (const auto &c : ctx->scratch_chunks) dev_free(c.p);
+  ctx->scratch_chunks.clear();
   sym_free(ctx->sym);
   mf_free(ctx->mf);
   if (ctx->h_st) hipHostFree(ctx->h_st);
@@ -834,9 +883,11 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_comm_abort(mlff_ctx *ctx) {
+  MLFF_API_BEGIN
   if (ctx == nullptr) return set_error(nullptr, MLFF_ERR_ARG, "null ctx");
   ctx->aborted = true;
   if (ctx->local) ctx->local->abort();
@@ -846,34 +897,44 @@ int mlff_comm_abort(mlff_ctx *ctx) {
     ctx->comm = nullptr;
   }
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_shard_range(mlff_ctx *ctx, int64_t *row0_out, int64_t *nrows_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (row0_out) *row0_out = ctx->row0;
   if (nrows_out) *nrows_out = ctx->nrows;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_matrix_ld(mlff_ctx *ctx, int64_t *ld_out) {
+  MLFF_API_BEGIN
   if (ctx == nullptr || ld_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
   *ld_out = ctx->ld;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_synchronize(mlff_ctx *ctx) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_stream(mlff_ctx *ctx, void **stream_out) {
+  MLFF_API_BEGIN
   if (ctx == nullptr || stream_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
   *stream_out = (void *)ctx->stream;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (K_local == nullptr && ctx->nrows > 0) return set_error(ctx, MLFF_ERR_ARG, "null K");
   if (ld_host < ctx->N) return set_error(ctx, MLFF_ERR_ARG, "ld_host < N");
@@ -893,9 +954,11 @@ int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) 
   ctx->sym.ready = false;
   mf_free(ctx->mf);
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int64_t ld_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
   if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
@@ -912,9 +975,11 @@ int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int
   }
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, double jitter) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (X == nullptr || d < 1 || d > 8 || !(length_scale > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "gen_rbf: need X, 1 <= d <= 8, length_scale > 0");
@@ -938,10 +1003,12 @@ int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, dou
   ctx->sym.ready = false;
   mf_free(ctx->mf);
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: null input or sig <= 0");
@@ -953,10 +1020,12 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   ctx->K_symmetric = true;  // the assembly mirrors the lower block triangle
   ctx->sym.ready = false;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "sgdml_operator: null input or sig <= 0");
@@ -965,19 +1034,23 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   ctx->has_matrix = false;  // a dense K set earlier is not this operator
   ctx->sym.ready = false;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out) {
+  MLFF_API_BEGIN
   if (R == nullptr || R_desc_out == nullptr || R_d_desc_out == nullptr || M < 1 || n_atoms < 2)
     return set_error(nullptr, MLFF_ERR_ARG, "sgdml_descriptors: bad arguments");
   const int rc = sgdml_descriptors(R, M, n_atoms, R_desc_out, R_d_desc_out);
   if (rc != MLFF_OK) return set_error(nullptr, rc, "sgdml_descriptors: HIP failure");
   return MLFF_OK;
+  MLFF_API_END(nullptr)
 }
 
 int mlff_sgdml_energies(mlff_ctx *ctx, const double *alphas, double *E_out, int64_t *i0_out,
                         int64_t *ni_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (alphas == nullptr || E_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
   if (!ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no sGDML operator set");
@@ -993,9 +1066,11 @@ int mlff_sgdml_energies(mlff_ctx *ctx, const double *alphas, double *E_out, int6
   if (i0_out) *i0_out = mf.i0;
   if (ni_out) *ni_out = mf.ni;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!(lam > 0.0)) return set_error(ctx, MLFF_ERR_ARG, "lam must be > 0");
   if (sigma_K != 1.0 && sigma_K != -1.0) return set_error(ctx, MLFF_ERR_ARG, "sigma_K must be +-1");
@@ -1003,9 +1078,11 @@ int mlff_set_operator(mlff_ctx *ctx, double sigma_K, double lam) {
   ctx->lam = lam;
   ctx->has_operator = true;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_set_storage(mlff_ctx *ctx, int mode) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (mode != MLFF_STORAGE_DENSE && mode != MLFF_STORAGE_SYMTILE && mode != MLFF_STORAGE_AUTO &&
       mode != MLFF_STORAGE_MATFREE)
@@ -1017,9 +1094,11 @@ int mlff_set_storage(mlff_ctx *ctx, int mode) {
     if (mode == MLFF_STORAGE_DENSE || mode == MLFF_STORAGE_MATFREE) sym_free(ctx->sym);
   }
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   MLFF_TRY(resolve_storage(ctx));
@@ -1028,9 +1107,11 @@ int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out
                             : (ctx->use_sym ? MLFF_STORAGE_SYMTILE : MLFF_STORAGE_DENSE);
   if (bytes_per_matvec_out) *bytes_per_matvec_out = operator_bytes(ctx);
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (v_global == nullptr || (y_local == nullptr && ctx->nrows > 0)) return set_error(ctx, MLFF_ERR_ARG, "null vector");
@@ -1042,9 +1123,11 @@ int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
     MLFF_HIP(ctx, hipMemcpyAsync(y_local, ctx->q, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   MLFF_TRY(operator_diag(ctx, ctx->dwork));
@@ -1052,17 +1135,21 @@ int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
     MLFF_HIP(ctx, hipMemcpyAsync(diag_local, ctx->dwork, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_none(mlff_ctx *ctx) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   ctx->precon_kind = MLFF_PRECON_NONE;
   ctx->k = 0;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (k < 1 || k > ctx->N || k > 16384)
@@ -1084,10 +1171,12 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
   if (seconds_out)
     *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int variant,
                         double *seconds_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (variant != 0 && variant != 1) return set_error(ctx, MLFF_ERR_ARG, "variant must be 0 or 1");
@@ -1102,9 +1191,11 @@ int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int varian
   if (seconds_out)
     *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if (k < 1 || k > ctx->N || (Lt_local == nullptr && ctx->nrows > 0))
@@ -1120,10 +1211,12 @@ int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k) {
   ctx->k = k;
   ctx->sigma_p = 1.0;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
                     double *evals_out, double *rowlev_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_matrix(ctx));
   if (ctx->world != 1) return set_error(ctx, MLFF_ERR_ARG, "eigen preconditioner needs a single rank");
@@ -1140,22 +1233,27 @@ int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int 
     ctx->sigma_p = 1.0;
   }
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (kind_out) *kind_out = ctx->precon_kind;
   if (k_out) *k_out = ctx->k;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   hipStream_t s = ctx->stream;
+  ScratchScope scope(ctx);
   double *rd = nullptr, *zd = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&rd, sizeof(double) * ctx->blk, s));
-  MLFF_HIP(ctx, hipMallocAsync(&zd, sizeof(double) * ctx->blk, s));
+  MLFF_TRY(scratch_alloc(ctx, &rd, ctx->blk));
+  MLFF_TRY(scratch_alloc(ctx, &zd, ctx->blk));
   MLFF_HIP(ctx, hipMemsetAsync(rd, 0, sizeof(double) * ctx->blk, s));
   if (ctx->nrows > 0)
     MLFF_HIP(ctx, hipMemcpyAsync(rd, r_local, sizeof(double) * ctx->nrows, hipMemcpyHostToDevice, s));
@@ -1171,13 +1269,13 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
   MLFF_HIP(ctx, hipGetLastError());
   if (ctx->nrows > 0)
     MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
-  MLFF_HIP(ctx, hipFreeAsync(rd, s));
-  MLFF_HIP(ctx, hipFreeAsync(zd, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (ctx->T == nullptr || ctx->k < 1) return set_error(ctx, MLFF_ERR_STATE, "no low-rank panel");
   if (T_local == nullptr || ld_out < ctx->nrows) return set_error(ctx, MLFF_ERR_ARG, "bad output");
@@ -1186,9 +1284,11 @@ int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
                                    sizeof(double) * ctx->nrows, ctx->k, hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (!(lam > 0.0) || scores_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "lev_scores: bad args");
@@ -1215,10 +1315,12 @@ int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, do
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   hipFree(W);
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local, double tol,
                    int64_t maxiter, int *early_exit_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
   if ((b_local == nullptr && ctx->nrows > 0) || maxiter < 1 || !(tol >= 0.0))
@@ -1285,9 +1387,11 @@ int mlff_pcg_start(mlff_ctx *ctx, const double *b_local, const double *x0_local,
   ctx->pcg_active = true;
   if (early_exit_out) *early_exit_out = early;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
   if (n_iter < 0) return set_error(ctx, MLFF_ERR_ARG, "n_iter < 0");
@@ -1344,10 +1448,12 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
   }
   if (status_out) *status_out = ctx->h_st->status;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *resid_out,
                     int *info_out) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!ctx->pcg_active) return set_error(ctx, MLFF_ERR_STATE, "mlff_pcg_start not called");
   MLFF_TRY(poll_state(ctx));
@@ -1357,9 +1463,11 @@ int mlff_pcg_result(mlff_ctx *ctx, int64_t *iters_out, int *status_out, double *
   if (resid_out) *resid_out = h.resid;
   if (info_out) *info_out = (h.status == ST_CONVERGED) ? 0 : (int)h.iters;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (ctx->nrows > 0) {
     if (x_local == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null x");
@@ -1367,9 +1475,11 @@ int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local) {
   }
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (!ctx->pcg_active || ctx->trace == nullptr) return set_error(ctx, MLFF_ERR_STATE, "no solve");
   if (trace_out == nullptr || n < 0) return set_error(ctx, MLFF_ERR_ARG, "bad output");
@@ -1379,33 +1489,41 @@ int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n) {
   if (cnt > 0)
     MLFF_HIP(ctx, hipMemcpy(trace_out, ctx->trace, sizeof(double) * cnt, hipMemcpyDeviceToHost));
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_timing_enable(mlff_ctx *ctx, int on) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   ctx->timing.on = on != 0;
   if (ctx->timing.on && ctx->timing.ev.size() < kTimingPool) ctx->timing.ev.reserve(kTimingPool);
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double *iter_ms,
                      int64_t *iter_count) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (gemv_ms) *gemv_ms = ctx->timing.gemv_ms;
   if (gemv_count) *gemv_count = ctx->timing.gemv_count;
   if (iter_ms) *iter_ms = ctx->timing.iter_ms;
   if (iter_count) *iter_count = ctx->timing.iter_count;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_timing_read_precon(mlff_ctx *ctx, double *ms, int64_t *count) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (ms) *ms = ctx->timing.pre_ms;
   if (count) *count = ctx->timing.pre_count;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 int mlff_timing_reset(mlff_ctx *ctx) {
+  MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   ctx->timing.gemv_ms = 0.0;
   ctx->timing.gemv_count = 0;
@@ -1414,6 +1532,7 @@ int mlff_timing_reset(mlff_ctx *ctx) {
   ctx->timing.iter_ms = 0.0;
   ctx->timing.iter_count = 0;
   return MLFF_OK;
+  MLFF_API_END(ctx)
 }
 
 }  // extern "C"

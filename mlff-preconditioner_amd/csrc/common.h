@@ -194,6 +194,14 @@ struct mlff_ctx {
   mlff::Timing timing;
   std::string err;
   bool aborted = false;  // mlff_comm_abort was called: every entry point fails
+
+  // device scratch arena (ScratchScope / scratch_get): chunks, current chunk and offset
+  struct ScratchChunk {
+    char *p;
+    size_t size;
+  };
+  std::vector<ScratchChunk> scratch_chunks;
+  size_t scratch_cur = 0, scratch_off = 0;
 };
 
 namespace mlff {
@@ -228,15 +236,43 @@ int nccl_check(mlff_ctx *ctx, ncclResult_t e, const char *what);
     if (rc__ != MLFF_OK) return rc__; \
   } while (0)
 
-// stream-ordered frees of scratch buffers on every exit path of a build function
-struct ScratchFree {
-  hipStream_t s;
-  std::vector<void *> p;
-  ~ScratchFree() {
-    for (void *q : p)
-      if (q != nullptr) (void)hipFreeAsync(q, s);
+// No C++ exception may cross the C ABI (ctypes would see std::terminate): every
+// extern "C" body runs inside MLFF_API_BEGIN / MLFF_API_END(ctx), which maps
+// std::bad_alloc to MLFF_ERR_NOMEM and anything else to MLFF_ERR_HIP, aborting the
+// rank's in-process group so that its peers leave their collectives.
+int api_exception(mlff_ctx *ctx, int code, const char *what);
+#define MLFF_API_BEGIN try {
+#define MLFF_API_END(ctx)                                                             \
+  }                                                                                   \
+  catch (const std::bad_alloc &) {                                                    \
+    return mlff::api_exception((ctx), MLFF_ERR_NOMEM, "host allocation failed");      \
+  }                                                                                   \
+  catch (const std::exception &e__) {                                                 \
+    return mlff::api_exception((ctx), MLFF_ERR_HIP, e__.what());                      \
+  }                                                                                   \
+  catch (...) {                                                                       \
+    return mlff::api_exception((ctx), MLFF_ERR_HIP, "unknown C++ exception");         \
   }
+
+// Device scratch of a build function, from the context's arena (mlff_ctx::scratch):
+// a bump allocator over chunks obtained once with hipMalloc and kept until
+// mlff_ctx_destroy.  Every user runs on ctx->stream, so memory handed out again after a
+// ScratchScope has closed is only touched by kernels ordered after the previous user's.
+// (No stream-ordered allocator: hipMallocAsync pools outlive the contexts' streams.)
+struct ScratchScope {
+  mlff_ctx *ctx;
+  size_t chunk, off;
+  explicit ScratchScope(mlff_ctx *c);
+  ~ScratchScope();
+  ScratchScope(const ScratchScope &) = delete;
+  ScratchScope &operator=(const ScratchScope &) = delete;
 };
+// bytes (rounded up to 256) of scratch valid until the innermost open ScratchScope closes
+int scratch_get(mlff_ctx *ctx, size_t bytes, void **out);
+template <typename T>
+int scratch_alloc(mlff_ctx *ctx, T **out, size_t count) {
+  return scratch_get(ctx, sizeof(T) * (count > 0 ? count : 1), reinterpret_cast<void **>(out));
+}
 
 // ---- collectives (api.hip): RCCL, or the in-process transport ---------------
 // sum-allreduce of n doubles in place (no-op on one rank)

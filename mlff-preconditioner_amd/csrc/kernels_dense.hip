@@ -132,14 +132,14 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
     MLFF_HIP(ctx, hipGetLastError());
     return MLFF_OK;
   }
+  ScratchScope scope(ctx);
   double *slabs = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&slabs, sizeof(double) * splits * k * k, ctx->stream));
+  MLFF_TRY(scratch_alloc(ctx, &slabs, splits * k * k));
   gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, W, ldw, 0.0, slabs, k, (int)splits, k * k,
               ctx->stream);
   const int64_t n = k * k;
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)),
                      dim3(256), 0, ctx->stream, slabs, (int)splits, n, G);
-  MLFF_HIP(ctx, hipFreeAsync(slabs, ctx->stream));
   MLFF_HIP(ctx, hipGetLastError());
   return MLFF_OK;
 }

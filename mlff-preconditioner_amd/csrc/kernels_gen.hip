@@ -409,12 +409,13 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
   int32_t *dP = nullptr, *dpi = nullptr, *dpiinv = nullptr;
   const int64_t rec = 6 * n + 2;
   hipStream_t s = ctx->stream;
-  MLFF_HIP(ctx, hipMallocAsync(&dRd, sizeof(double) * M * D, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dRdd, sizeof(double) * M * D * 3, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dP, sizeof(int32_t) * n_perms * D, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dpi, sizeof(int32_t) * n_perms * n, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dpiinv, sizeof(int32_t) * n_perms * n, s));
-  MLFF_HIP(ctx, hipMallocAsync(&uv, sizeof(double) * mi * M * n_perms * rec, s));
+  ScratchScope scope(ctx);
+  MLFF_TRY(scratch_alloc(ctx, &dRd, M * D));
+  MLFF_TRY(scratch_alloc(ctx, &dRdd, M * D * 3));
+  MLFF_TRY(scratch_alloc(ctx, &dP, n_perms * D));
+  MLFF_TRY(scratch_alloc(ctx, &dpi, n_perms * n));
+  MLFF_TRY(scratch_alloc(ctx, &dpiinv, n_perms * n));
+  MLFF_TRY(scratch_alloc(ctx, &uv, mi * M * n_perms * rec));
   MLFF_HIP(ctx, hipMemcpyAsync(dRd, R_desc, sizeof(double) * M * D, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(dRdd, R_d_desc, sizeof(double) * M * D * 3, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(dP, Pt.data(), sizeof(int32_t) * n_perms * D, hipMemcpyHostToDevice, s));
@@ -428,12 +429,6 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
                      ctx->rows_per, ctx->blk, dRdd, M, n, D, i0, dpi, dpiinv, n_perms, uv, 0,
                      (double *)nullptr);
   MLFF_HIP(ctx, hipGetLastError());
-  MLFF_HIP(ctx, hipFreeAsync(dRd, s));
-  MLFF_HIP(ctx, hipFreeAsync(dRdd, s));
-  MLFF_HIP(ctx, hipFreeAsync(dP, s));
-  MLFF_HIP(ctx, hipFreeAsync(dpi, s));
-  MLFF_HIP(ctx, hipFreeAsync(dpiinv, s));
-  MLFF_HIP(ctx, hipFreeAsync(uv, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
 }
@@ -452,9 +447,10 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
   double *uv = nullptr;
   int32_t *dpi = nullptr, *dpiinv = nullptr;
   const int64_t rec = 6 * n + 2;
-  MLFF_HIP(ctx, hipMallocAsync(&uv, sizeof(double) * mi * n_perms * rec, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dpi, sizeof(int32_t) * n_perms * n, s));
-  MLFF_HIP(ctx, hipMallocAsync(&dpiinv, sizeof(int32_t) * n_perms * n, s));
+  ScratchScope scope(ctx);
+  MLFF_TRY(scratch_alloc(ctx, &uv, mi * n_perms * rec));
+  MLFF_TRY(scratch_alloc(ctx, &dpi, n_perms * n));
+  MLFF_TRY(scratch_alloc(ctx, &dpiinv, n_perms * n));
   MLFF_HIP(ctx, hipMemcpyAsync(dpi, perms_host, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(dpiinv, piinv_host, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_sgdml_uv, dim3(1, (unsigned)mi, (unsigned)n_perms), dim3(256), 0, s, dRd, dRdd,
@@ -464,9 +460,6 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
                      ctx->nrows, ctx->rows_per, ctx->blk, dRdd, (int64_t)1, n, D, i0, dpi, dpiinv,
                      n_perms, uv, 1, diag_out);
   MLFF_HIP(ctx, hipGetLastError());
-  MLFF_HIP(ctx, hipFreeAsync(uv, s));
-  MLFF_HIP(ctx, hipFreeAsync(dpi, s));
-  MLFF_HIP(ctx, hipFreeAsync(dpiinv, s));
   (void)M;
   return MLFF_OK;
 }

@@ -234,12 +234,12 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   hipStream_t s = ctx->stream;
   const int64_t N = ctx->N, nrows = ctx->nrows, blk = ctx->blk;
   const int np = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + 1023) / 1024));
+  ScratchScope scope(ctx);
   double *pv = nullptr, *wins = nullptr;
   long long *pp = nullptr;
-  MLFF_HIP(ctx, hipMallocAsync(&pv, sizeof(double) * np, s));
-  MLFF_HIP(ctx, hipMallocAsync(&pp, sizeof(long long) * np, s));
-  MLFF_HIP(ctx, hipMallocAsync(&wins, sizeof(double) * 2 * ctx->world, s));
-  ScratchFree scratch{s, {pv, pp, wins}};
+  MLFF_TRY(scratch_alloc(ctx, &pv, np));
+  MLFF_TRY(scratch_alloc(ctx, &pp, np));
+  MLFF_TRY(scratch_alloc(ctx, &wins, 2 * ctx->world));
   // init: perm = arange(N), dwork = diag(S), pivflag = 0, Lt = 0
   std::vector<int64_t> hperm(N);
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
@@ -248,15 +248,13 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   double *colbuf = nullptr, *part = nullptr;
   if (mfcols) {
     MLFF_TRY(operator_diag(ctx, ctx->dwork));
-    MLFF_HIP(ctx, hipMallocAsync(&colbuf, sizeof(double) * blk, s));
-    scratch.p.push_back(colbuf);
+    MLFF_TRY(scratch_alloc(ctx, &colbuf, blk));
     MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
   } else {
     launch_diag_of(ctx->K, ctx->ld, nrows, ctx->row0, ctx->rows_per, blk, ctx->sigma_K, ctx->dwork, s);
   }
   const int kmax_split = choose_ksplit(k, blk);
-  MLFF_HIP(ctx, hipMallocAsync(&part, sizeof(double) * kmax_split * blk, s));
-  scratch.p.push_back(part);
+  MLFF_TRY(scratch_alloc(ctx, &part, kmax_split * blk));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));

@@ -165,22 +165,22 @@ def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
     # the 2-minute progress checkpoint of the solver builds its model with create_model
     it = Iterative(gdml_train or _ModelFactory(), None, callback=callback, device=device,
                    devices=devices)
-    alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info = it.solve(
-        task, R_desc, R_d_desc, tpl, y, y_std, save_progr_callback=save_progr_callback,
-        break_percentage=break_percentage, str_preconditioner=str_preconditioner,
-        flag_eigvals=flag_eigvals)
-    model = create_model(task, "cg", R_desc, R_d_desc, tpl, y_std, alphas,
-                         solver_resid=resid, solver_iters=num_iters,
-                         norm_y_train=np.linalg.norm(y), inducing_pts_idxs=inducing_pts_idxs)
-    model.update(info)
-    if model["use_E"]:
-        _, E = it.solver.sgdml_energies(alphas)
-        c = recov_int_const(E * y_std, task["E_train"])
-        if c is None:
-            model["use_E"] = False
-        else:
-            model["c"] = c
-    it.solver.close()
+    with it:  # the device contexts are released on every exit path
+        alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info = it.solve(
+            task, R_desc, R_d_desc, tpl, y, y_std, save_progr_callback=save_progr_callback,
+            break_percentage=break_percentage, str_preconditioner=str_preconditioner,
+            flag_eigvals=flag_eigvals)
+        model = create_model(task, "cg", R_desc, R_d_desc, tpl, y_std, alphas,
+                             solver_resid=resid, solver_iters=num_iters,
+                             norm_y_train=np.linalg.norm(y), inducing_pts_idxs=inducing_pts_idxs)
+        model.update(info)
+        if model["use_E"]:
+            _, E = it.solver.sgdml_energies(alphas)
+            c = recov_int_const(E * y_std, task["E_train"])
+            if c is None:
+                model["use_E"] = False
+            else:
+                model["c"] = c
     return model
 
 

@@ -24,8 +24,8 @@ from .solver import KernelSolver, PCGResult
 
 
 class _Worker(threading.Thread):
-    def __init__(self):
-        super().__init__(daemon=True)
+    def __init__(self, name: str):
+        super().__init__(daemon=True, name=name)
         self.q: queue.Queue = queue.Queue()
         self.start()
 
@@ -40,6 +40,9 @@ class _Worker(threading.Thread):
             except BaseException as e:  # noqa: BLE001 - re-raised by the caller
                 box["error"] = e
             done.set()
+            # drop the closure while waiting for the next item: it references the
+            # ShardedKernelSolver, which must stay collectable
+            del item, fn, box, done
 
 
 class ShardedKernelSolver:
@@ -58,7 +61,7 @@ class ShardedKernelSolver:
         else:
             raise ValueError("comm must be 'rccl' or 'local'")
         self.comm = comm
-        self._workers = [_Worker() for _ in devices]
+        self._workers = [_Worker(f"mlff-rank{r}-dev{d}") for r, d in enumerate(devices)]
         self.ranks: list[KernelSolver | None] = [None] * self.world
         self._all(lambda r: KernelSolver(n, device=devices[r], rank=r, world=self.world,
                                          comm_id=comm_id), assign=True)
@@ -102,15 +105,25 @@ class ShardedKernelSolver:
 
     # --------------------------------------------------------------- lifecycle
     def close(self):
-        if getattr(self, "_workers", None) is None:
+        """Destroy every rank's context and stop the workers.  The contexts are destroyed
+        concurrently on the workers (RCCL's communicator teardown waits for the peers);
+        from __del__ on a worker thread itself, where that dispatch would wait on the
+        calling thread, they are destroyed one by one.  Idempotent."""
+        workers = getattr(self, "_workers", None)
+        if workers is None:
             return
         try:
-            if all(s is not None for s in self.ranks):
+            ranks = getattr(self, "ranks", [])
+            if threading.current_thread() in workers or any(s is None for s in ranks):
+                for s in ranks:
+                    if s is not None:
+                        s.close()
+            else:
                 self._each("close")
         finally:
-            for w in self._workers:
-                w.q.put(None)
             self._workers = None
+            for w in workers:
+                w.q.put(None)
 
     def __enter__(self):
         return self

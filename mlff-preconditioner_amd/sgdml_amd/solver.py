@@ -17,6 +17,7 @@ and passes its own row block (row_range()).
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -40,6 +41,7 @@ class KernelSolver:
     def __init__(self, n: int, device: int | None = None, rank: int = 0, world: int = 1,
                  comm_id: bytes | None = None):
         self._lib = nat.load_library()
+        self._close_lock = threading.Lock()
         self.n = int(n)
         self.rank, self.world = int(rank), int(world)
         if device is None:
@@ -69,9 +71,15 @@ class KernelSolver:
         nat.check(rc, self._ctx, name)
 
     def close(self):
-        if getattr(self, "_ctx", None) is not None and self._ctx.value is not None:
-            self._lib.mlff_ctx_destroy(self._ctx)
+        """Destroy the device context (idempotent, safe from any thread)."""
+        lock = getattr(self, "_close_lock", None)
+        if lock is None:
+            return
+        with lock:
+            ctx = getattr(self, "_ctx", None)
             self._ctx = None
+            if ctx is not None and ctx.value is not None:
+                self._lib.mlff_ctx_destroy(ctx)
 
     def __del__(self):  # pragma: no cover
         try:

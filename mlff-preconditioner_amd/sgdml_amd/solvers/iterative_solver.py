@@ -60,6 +60,24 @@ class Iterative(object):
         self.devices = None if devices is None or len(devices) < 2 else [int(d) for d in devices]
         self.solver = None  # KernelSolver of the last solve (kept for inspection)
 
+    def close(self):
+        """Release the device context(s) of the last solve (a new solve does so too)."""
+        solver, self.solver = self.solver, None
+        if solver is not None:
+            solver.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
     # ------------------------------------------------------------ helpers
     def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n, dense):
         """dense: assemble K on the device (the eigen preconditioners factor all of K);
@@ -126,6 +144,7 @@ class Iterative(object):
 
         dense = str_preconditioner in EIGVEC_KEYS or str_preconditioner in [
             "rank_k_lev_scores", "rank_k_lev_scores_custom"]
+        self.close()  # the previous solve's contexts (operator tables, panel, communicator)
         solver = self._kernel_solver(task, np.asarray(R_desc), np.asarray(R_d_desc),
                                      tril_perms_lin, n, dense)
         self.solver = solver

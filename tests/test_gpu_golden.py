@@ -96,9 +96,9 @@ def run_dropin(f, name, precon, desc=None):
     bp = int(f["k_rot"]) / n
     Rd, Rdd = desc if desc is not None else (f["R_desc"], f["R_d_desc"])
     np.random.seed(1000 + SEEDS[name])
-    it = Iterative(None, None, device=0)
-    return it.solve(task_of(f), Rd, Rdd, f["tril_perms_lin"], f["y"],
-                    float(f["y_std"]), break_percentage=bp, str_preconditioner=precon)
+    with Iterative(None, None, device=0) as it:  # contexts released when the solve returns
+        return it.solve(task_of(f), Rd, Rdd, f["tril_perms_lin"], f["y"],
+                        float(f["y_std"]), break_percentage=bp, str_preconditioner=precon)
 
 
 @pytest.fixture(scope="module")
@@ -326,10 +326,10 @@ def test_dropin_warm_start(sg, golden_dir):
     a_ref = f["cholesky__alphas"]
     task = dict(task_of(f), alphas0_F=a_ref * (1 + 1e-3 * np.random.default_rng(0).standard_normal(n)),
                 solver_iters=1000)
-    it = Iterative(None, None, device=0)
-    alphas, num_iters, resid, rmse, idxs, is_conv, info = it.solve(
-        task, f["R_desc"], f["R_d_desc"], f["tril_perms_lin"], f["y"], float(f["y_std"]),
-        break_percentage=int(f["k_rot"]) / n, str_preconditioner="cholesky")
+    with Iterative(None, None, device=0) as it:
+        alphas, num_iters, resid, rmse, idxs, is_conv, info = it.solve(
+            task, f["R_desc"], f["R_d_desc"], f["tril_perms_lin"], f["y"], float(f["y_std"]),
+            break_percentage=int(f["k_rot"]) / n, str_preconditioner="cholesky")
     assert is_conv
     assert num_iters == 1000 + max(info["cg_iterations"], 1)
     assert resid <= float(f["solver_tol"]) * np.linalg.norm(f["y"])

@@ -110,7 +110,8 @@ def test_matfree_sharded(sg, golden_dir, world):
         except BaseException as e:  # noqa: BLE001
             errs[r] = e
 
-    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    th = [threading.Thread(target=body, args=(r,), daemon=True, name=f"rank{r}of{world}")
+          for r in range(world)]
     for t in th:
         t.start()
     for t in th:
@@ -185,7 +186,8 @@ def test_matfree_sharded_builds_and_solve(sg, golden_dir, world):
             except BaseException as e:  # noqa: BLE001
                 errs[r] = e
 
-        ts = [threading.Thread(target=th, args=(r,), daemon=True) for r in range(w)]
+        ts = [threading.Thread(target=th, args=(r,), daemon=True, name=f"rank{r}of{w}")
+              for r in range(w)]
         for t in ts:
             t.start()
         for t in ts:

@@ -29,7 +29,8 @@ def run_ranks(world, fn, timeout=300):
         except BaseException as e:  # noqa: BLE001
             errors[r] = e
 
-    threads = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    threads = [threading.Thread(target=body, args=(r,), daemon=True, name=f"rank{r}of{world}")
+               for r in range(world)]
     for t in threads:
         t.start()
     for t in threads:

@@ -23,15 +23,17 @@ def sg():
 
 
 def run(f, name, precon, devices, desc=None):
+    """(solve result, type and world of the solver it used); the solver's contexts are
+    released before returning, pass or fail."""
     from sgdml_amd.solvers import Iterative
 
     n = f["y"].size
     Rd, Rdd = desc if desc is not None else (f["R_desc"], f["R_d_desc"])
     np.random.seed(1000 + SEEDS[name])
-    it = Iterative(None, None, devices=devices)
-    out = it.solve(task_of(f), Rd, Rdd, f["tril_perms_lin"], f["y"], float(f["y_std"]),
-                   break_percentage=int(f["k_rot"]) / n, str_preconditioner=precon)
-    return out, it.solver
+    with Iterative(None, None, devices=devices) as it:
+        out = it.solve(task_of(f), Rd, Rdd, f["tril_perms_lin"], f["y"], float(f["y_std"]),
+                       break_percentage=int(f["k_rot"]) / n, str_preconditioner=precon)
+        return out, (type(it.solver), getattr(it.solver, "world", 1))
 
 
 @pytest.mark.timeout(600)
@@ -42,9 +44,9 @@ def run(f, name, precon, devices, desc=None):
 def test_sharded_dropin_vs_reference(sg, golden_dir, name, precon, world):
     f = load(golden_dir, name)
     desc = sg.sgdml_descriptors(f["R"]) if "R_desc" not in f.files else None
-    (alphas, num_iters, resid, rmse, idxs, is_conv, info), solver = run(
+    (alphas, num_iters, resid, rmse, idxs, is_conv, info), (kind, w) = run(
         f, name, precon, [0] * world, desc)
-    assert isinstance(solver, sg.ShardedKernelSolver) and solver.world == world
+    assert kind is sg.ShardedKernelSolver and w == world
     assert info["n_gpus"] == world
     assert is_conv
     if precon != "lev_random":
@@ -53,7 +55,6 @@ def test_sharded_dropin_vs_reference(sg, golden_dir, name, precon, world):
         assert np.array_equal(info["index_columns"], f["cholesky__index_columns"])
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
                       f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
-    solver.close()
 
 
 @pytest.mark.timeout(300)
@@ -61,9 +62,9 @@ def test_sharded_dropin_eigen_uses_one_device(sg, golden_dir):
     """eigvec_precon factors all of K: the drop-in keeps it on the first device."""
     name = "sgdml_ethanol_n270"
     f = load(golden_dir, name)
-    (alphas, num_iters, resid, rmse, idxs, is_conv, info), solver = run(
+    (alphas, num_iters, resid, rmse, idxs, is_conv, info), (kind, _) = run(
         f, name, "eigvec_precon", [0, 0])
-    assert isinstance(solver, sg.KernelSolver) and info["n_gpus"] == 1
+    assert kind is sg.KernelSolver and info["n_gpus"] == 1
     assert is_conv
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas,
                       int(f["eigvec_precon__num_iters"]), f["eigvec_precon__trace"],
