@@ -119,6 +119,45 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
     return y.reshape(-1)
 
 
+def kernel_diag(R_desc, R_d_desc, perms, sig):
+    """diag(K) of the assembled sGDML kernel, one diagonal block K[i, i] per training point
+    (IterativeCholesky._assemble_kernel_mat_diag, iterative_cholesky.py:241-373, which
+    returns -diag for the PSD operator -K).  The block is
+        K_ii = J_i^T (5 sum_p m_p diff_p (diff_p . J_i[P_p]) - sum_p w_p J_i[P_p]),
+    diff_p = Rd_i - Rd_i[P_p].  For a single identity permutation diff = 0 and
+    diag_(a,c) = -(5 / (3 sig^2)) sum_{b != a} Rdd_i[pair(a, b), c]^2, evaluated without
+    forming the D x 3n Jacobian (the nanotube's is 68265 x 1110)."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    R_d_desc = np.asarray(R_d_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    perms = np.atleast_2d(perms)
+    s_at, t_at = np.tril_indices(n, k=-1)
+    out = np.empty((M, n, 3))
+    if perms.shape[0] == 1 and np.array_equal(perms[0], np.arange(n)):
+        for i in range(M):
+            sq = R_d_desc[i] ** 2                       # D x 3, each pair feeds both atoms
+            acc = np.zeros((n, 3))
+            np.add.at(acc, t_at, sq)
+            np.add.at(acc, s_at, sq)
+            out[i] = -(5.0 / (3.0 * sig ** 2)) * acc
+        return out.reshape(-1)
+    P = np.array([desc_perm(p) for p in perms])
+    sqrt5 = np.sqrt(5.0)
+    for i in range(M):
+        J = d_desc_from_comp(R_d_desc[i], n)            # D x 3n
+        diff = R_desc[i][None, :] - R_desc[i][P]        # n_perms x D
+        norm = sqrt5 * np.linalg.norm(diff, axis=1)
+        m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+        w = (sig ** 2 + sig * norm) * m
+        O = np.zeros((D, 3 * n))
+        for p in range(P.shape[0]):
+            Jp = J[P[p]]                                # rows permuted: J_i[P_p]
+            O += 5.0 * m[p] * np.outer(diff[p], diff[p] @ Jp) - w[p] * Jp
+        out[i] = np.einsum("dk,dk->k", J, O).reshape(n, 3)
+    return out.reshape(-1)
+
+
 def energies_matrix_free(R_desc, R_d_desc, perms, sig, alphas):
     """Training-set energies of the model with coefficients alphas, E_F[0] of
     GDMLPredict's _predict_wkr (predict.py:172-220) before the std scale and the

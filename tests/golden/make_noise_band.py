@@ -1,0 +1,170 @@
+"""Noise band of the golden PCG solves: how far the reference's own algorithm moves under a
+change of floating-point summation order alone.
+
+For every golden solve of the reference (tests/golden/sgdml_*.npz, the same list as
+tests/test_gpu_golden.py) the CPU oracle (oracle/: the reference's preconditioner build,
+operator and scipy-1.7.3 CG recurrence restated in NumPy) is re-run with several
+summation orders of the operator and of the preconditioner apply:
+
+  blas      K @ v, T.T @ (T @ r)                        (the oracle's default order)
+  blk7      7 column blocks, partial products added in block order
+  rev       columns / panel rows in reverse order
+  blk512    512-column tiles (the GPU tile width), added in tile order
+  pair      np.einsum (pairwise, unblocked)
+  ld        extended precision (np.longdouble) products, rounded once (N <= 621 only)
+
+and the spread against the reference's recorded solve is written to noise_band.json:
+iteration-count differences and the iteration at which the running-minimum residual first
+crosses every half decade.  tests/parity.py holds the GPU to this band (scaled, see there).
+
+Inputs are the committed fixtures only (the reference is not imported).  CPU only:
+    python tests/golden/make_noise_band.py            (~5 min on 8 cores)
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(REPO)]
+
+from oracle.pcg import cg_legacy  # noqa: E402
+from oracle.precon import (nystrom_panel, pivoted_cholesky, svd_panel,  # noqa: E402
+                           woodbury_panel)
+from oracle.sgdml import assemble_kernel, descriptors, kernel_matvec_matrix_free  # noqa: E402
+
+GOLDEN = REPO / "tests" / "golden"
+PRECONS_270 = ["cholesky", "random_scores", "lev_scores", "inverse_lev", "lev_random",
+               "truncated_cholesky", "truncated_cholesky_custom", "rank_k_lev_scores",
+               "rank_k_lev_scores_custom", "eigvec_precon"]
+CASES = [("sgdml_ethanol_n270", p) for p in PRECONS_270] + [
+    ("sgdml_ethanol_n270_perms", p) for p in ["cholesky", "random_scores",
+                                              "truncated_cholesky_custom"]] + [
+    ("sgdml_ethanol_n621", p) for p in ["cholesky", "random_scores", "truncated_cholesky"]] + [
+    ("sgdml_ethanol_n2997", p) for p in ["cholesky", "random_scores"]] + [
+    ("sgdml_nanotube_n3330", p) for p in ["cholesky", "random_scores"]]
+
+
+def half_decade_crossings(trace, top):
+    """Iteration (1-based) at which the running minimum first reaches each half decade
+    below `top` (log10 of the first residual)."""
+    env = np.minimum.accumulate(np.asarray(trace))
+    out = {}
+    for lvl in np.arange(np.floor(top) - 0.5, np.log10(env[-1]) - 1e-12, -0.5):
+        hit = np.nonzero(env <= 10 ** lvl)[0]
+        if hit.size:
+            out[f"{lvl:.1f}"] = int(hit[0])
+    return out
+
+
+def dense_K(f):
+    if "K" in f.files:
+        return np.array(f["K"])
+    if "R_desc" in f.files:
+        return assemble_kernel(f["R_desc"], f["R_d_desc"], f["tril_perms_lin"], float(f["sig"]))
+    # nanotube: columns of the matrix-free operator (the reference's K_op), symmetrised
+    Rd, Rdd = descriptors(f["R"])
+    n = f["y"].size
+    K = np.empty((n, n))
+    e = np.zeros(n)
+    for j in range(n):
+        e[j] = 1.0
+        K[:, j] = kernel_matvec_matrix_free(Rd, Rdd, f["perms"], float(f["sig"]), e)
+        e[j] = 0.0
+    return 0.5 * (K + K.T)
+
+
+def panel(f, precon, K, lam):
+    n = K.shape[0]
+    S = -K
+    k = int(int(f["k_rot"]) / n * n)
+    if precon == "cholesky":
+        L, piv = pivoted_cholesky(lambda i: S[:, i] + lam * (np.arange(n) == i),
+                                  np.diag(S).copy(), k)
+        return woodbury_panel(L, lam)
+    if precon.startswith("eigvec"):
+        return svd_panel(S, k, lam)
+    idx = f[f"{precon}__inducing_pts_idxs"]
+    return nystrom_panel(S[:, idx], idx, lam, 1 if precon.endswith("_custom") else 0)
+
+
+def make_gemv(A, order):
+    """v -> A @ v in a given summation order over the columns of A."""
+    n = A.shape[1]
+    if order == "blas":
+        return lambda v: A @ v
+    if order == "rev":
+        Ar = np.ascontiguousarray(A[:, ::-1])
+        return lambda v: Ar @ v[::-1]
+    if order in ("blk7", "blk512"):
+        edges = (np.linspace(0, n, 8).astype(int) if order == "blk7"
+                 else np.arange(0, n + 512, 512).clip(max=n))
+        blocks = [(a, b, np.ascontiguousarray(A[:, a:b])) for a, b in zip(edges[:-1], edges[1:])
+                  if b > a]
+
+        def f(v):
+            y = np.zeros(A.shape[0])
+            for a, b, Ab in blocks:
+                y = y + Ab @ v[a:b]
+            return y
+        return f
+    if order == "pair":
+        return lambda v: np.einsum("ij,j->i", A, v)
+    if order == "ld":
+        Al = A.astype(np.longdouble)
+        return lambda v: (Al @ v.astype(np.longdouble)).astype(np.float64)
+    raise ValueError(order)
+
+
+def run_case(name, precon, orders):
+    f = np.load(GOLDEN / f"{name}.npz", allow_pickle=False)
+    K = dense_K(f)
+    y, lam, tol = f["y"], float(f["lam"]), float(f["solver_tol"])
+    n = y.size
+    T, sp = panel(f, precon, K, lam)
+    ref_it = int(f[f"{precon}__num_iters"])
+    ref_tr = f[f"{precon}__trace"]
+    top = float(np.log10(np.minimum.accumulate(ref_tr)[0]))
+    ref_cross = half_decade_crossings(ref_tr, top)
+    out = {"n": n, "ref_iters": ref_it, "variants": {}}
+    for order in orders:
+        mvK = make_gemv(K, order)
+        mvT = make_gemv(T, order)
+        mvTt = make_gemv(np.ascontiguousarray(T.T), order)
+        x, info, tr, it = cg_legacy(lambda v: -mvK(v) + lam * v, y, tol=tol, maxiter=5 * n,
+                                    psolve=lambda r: sp * ((r - mvTt(mvT(r))) / lam))
+        cross = half_decade_crossings(tr[1:], top)
+        dc = [abs(cross[k] - ref_cross[k]) for k in ref_cross if k in cross]
+        out["variants"][order] = {
+            "iters": int(it), "info": int(info), "d_iters": int(it - ref_it),
+            "max_d_crossing": int(max(dc) if dc else 0),
+            "rel_dalpha": float(np.linalg.norm(-x - f[f"{precon}__alphas"])
+                                / np.linalg.norm(f[f"{precon}__alphas"]))}
+    v = out["variants"].values()
+    out["band_iters"] = int(max(abs(e["d_iters"]) for e in v))
+    out["band_crossing"] = int(max(e["max_d_crossing"] for e in v))
+    out["band_rel_dalpha"] = float(max(e["rel_dalpha"] for e in v))
+    return out
+
+
+def main():
+    res = {}
+    for name, precon in CASES:
+        t0 = time.time()
+        n = int(np.load(GOLDEN / f"{name}.npz", allow_pickle=False)["y"].size)
+        orders = ["blas", "blk7", "rev", "blk512", "pair"] + (["ld"] if n <= 621 else [])
+        r = run_case(name, precon, orders)
+        res[f"{name}/{precon}"] = r
+        print(f"{name:28s} {precon:26s} ref {r['ref_iters']:5d}  "
+              + " ".join(f"{o}:{e['d_iters']:+d}" for o, e in r["variants"].items())
+              + f"  band it {r['band_iters']} cross {r['band_crossing']}  ({time.time() - t0:.1f} s)",
+              flush=True)
+    (GOLDEN / "noise_band.json").write_text(json.dumps(res, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

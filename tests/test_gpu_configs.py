@@ -1,0 +1,140 @@
+"""BASELINE.json configs[0], [1] and [4] through the HIP path (size-true, -m gpu).
+
+configs[0]  ethanol N = 2997, no preconditioner: the drop-in Iterative.solve against the
+            reference's own unpreconditioned solve (tests/golden/sgdml_ethanol_n2997.npz,
+            none_1e-04__*: 5N = 14985 iterations without reaching tol 1e-4).  Contract for
+            unpreconditioned runs: same stopping outcome, the first residuals
+            pointwise, the running-minimum envelope within 0.5 decade at every iteration.
+configs[1]  nanotube N = 15540 (synthetic 370-atom geometry, M = 14), matrix-free operator:
+            the first 64 pivots and L columns of the pivoted Cholesky against the oracle's
+            (incomplete_cholesky.py:24-93 with get_col = -K_op e_i, iterative_cholesky.py:
+            152-156, on oracle.sgdml.kernel_matvec_matrix_free), then the rule-of-thumb rank
+            k = 2701 build and a solve to 1e-6 whose true residual ||b - A x|| is recomputed
+            on the host with the oracle operator.
+configs[4]  nanotube N = 15540, rank-1024 pivoted Cholesky on 8 ranks (in-process
+            transport on one GPU, the same collectives as RCCL on 8 GPUs): pivots identical
+            to the one-rank build, panels within 1e-10.
+"""
+import numpy as np
+import pytest
+
+from tests.test_gpu_golden import load, run_dropin
+from tests.test_gpu_multirank import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+N_ATOMS, M_NANO, SIG, LAM = 370, 14, 10.0, 1e-10
+
+
+@pytest.fixture(scope="module")
+def sg():
+    import sgdml_amd
+
+    if sgdml_amd.device_count() < 1:
+        pytest.fail("no GPU visible to libmlffpcg.so")
+    return sgdml_amd
+
+
+@pytest.fixture(scope="module")
+def nanotube(sg):
+    """configs[1] geometry (bench.py --workload nanotube): descriptors on the GPU."""
+    from sgdml_amd import synthetic
+
+    ds = synthetic.nanotube_like(M_NANO, seed=0)
+    Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+    y, _ = synthetic.labels(ds["F"])
+    return Rd, Rdd, np.arange(N_ATOMS)[None, :], y
+
+
+@pytest.mark.timeout(600)
+def test_config0_ethanol_n2997_unpreconditioned(sg, golden_dir):
+    name = "sgdml_ethanol_n2997"
+    f = load(golden_dir, name)
+    n = f["y"].size
+    alphas, num_iters, resid, rmse, idxs, is_conv, info = run_dropin(f, name, "none")
+    ref = f["none_1e-04__trace"]
+    # the reference stops at maxiter = 5N (iterative_solver.py:1002) without converging
+    assert int(f["none_1e-04__info"]) == 5 * n and not is_conv
+    assert num_iters == int(f["none_1e-04__callbacks"]) == 5 * n
+    tr = info["resid_trace"][1:]
+    assert tr.size == ref.size
+    assert np.max(np.abs(np.log10(tr[:8] / ref[:8]))) <= 1e-6
+    env, env_ref = np.minimum.accumulate(tr), np.minimum.accumulate(ref)
+    assert np.max(np.abs(np.log10(env / env_ref))) <= 0.5
+    assert idxs.size == 0
+
+
+def _oracle_pivots(Rd, Rdd, perms, k):
+    from oracle.precon import pivoted_cholesky
+    from oracle.sgdml import kernel_diag, kernel_matvec_matrix_free
+
+    n = Rd.shape[0] * 3 * N_ATOMS
+
+    def get_col(i):  # (-K_op) e_i = -K e_i + lam e_i (iterative_cholesky.py:152-156)
+        e = np.zeros(n)
+        e[i] = 1.0
+        return -kernel_matvec_matrix_free(Rd, Rdd, perms, SIG, e) + LAM * e
+
+    diag = -kernel_diag(Rd, Rdd, perms, SIG)  # excludes lam (iterative_cholesky.py:373)
+    return pivoted_cholesky(get_col, diag, k), diag
+
+
+@pytest.mark.timeout(900)
+def test_config1_nanotube_pivchol_and_solve(sg, nanotube):
+    from oracle.sgdml import kernel_matvec_matrix_free
+
+    Rd, Rdd, perms, y = nanotube
+    n = y.size
+    assert n == 15540
+    kk = 64
+    (L_ref, piv_ref), diag_ref = _oracle_pivots(Rd, Rdd, perms, kk)
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, perms, SIG)
+        s.set_operator(-1.0, LAM)
+        assert s.storage_info()[0] == "matfree"
+        np.testing.assert_allclose(s.diag(), diag_ref, rtol=1e-12, atol=0)
+        piv, _ = s.precon_pivchol(kk, build_woodbury=False)
+        Lt = s.precon_panel()
+        np.testing.assert_array_equal(piv[:kk], piv_ref[:kk])
+        np.testing.assert_allclose(Lt.T, L_ref, rtol=0, atol=1e-10 * np.abs(L_ref).max())
+        # the rule-of-thumb rank (plot_data.py:1254-1258: k = 2701 at N = 15540) and the solve
+        k = 2701
+        piv_full, _ = s.precon_pivchol(k)
+        np.testing.assert_array_equal(piv_full[:kk], piv_ref[:kk])
+        res = s.pcg(y, tol=1e-6, maxiter=5 * n)
+    assert res.info == 0 and 0 < res.iters < 5 * n
+    # the recheck guarantees the GPU's own ||b - A x|| <= tol ||b||; the oracle operator
+    # (another summation order) must see the same to rounding of ||A|| ||x||
+    Ax = -kernel_matvec_matrix_free(Rd, Rdd, perms, SIG, res.x) + LAM * res.x
+    relres = np.linalg.norm(y - Ax) / np.linalg.norm(y)
+    assert relres <= 1.05e-6, relres
+    assert abs(res.resid / np.linalg.norm(y) - relres) <= 1e-2 * relres
+
+
+@pytest.mark.timeout(900)
+def test_config4_nanotube_pivchol_rank1024_eight_ranks(sg, nanotube):
+    Rd, Rdd, perms, y = nanotube
+    n, k = y.size, 1024
+
+    def body(rank, world, key):
+        with sg.KernelSolver(n, device=0, rank=rank, world=world,
+                             comm_id=key if world > 1 else None) as s:
+            s.sgdml_operator(Rd, Rdd, perms, SIG)
+            s.set_operator(-1.0, LAM)
+            piv, _ = s.precon_pivchol(k, build_woodbury=False)
+            Lt = s.precon_panel()
+            s.precon_pivchol(k)  # + Woodbury: the configs[4] preconditioner
+            r0, r1 = s.row_range()
+            z = s.precon_apply(np.ascontiguousarray(y[r0:r1]))
+            return piv, Lt, z
+
+    ref = run_ranks(1, body, timeout=600)[0]
+    outs = run_ranks(8, body, timeout=800)
+    for piv, _, _ in outs:
+        np.testing.assert_array_equal(piv[:k], ref[0][:k])
+    Lt = np.concatenate([o[1] for o in outs], axis=1)
+    np.testing.assert_allclose(Lt, ref[1], rtol=0, atol=1e-10 * np.abs(ref[1]).max())
+    z = np.concatenate([o[2] for o in outs])
+    err = np.abs(z - ref[2]).max() / np.abs(ref[2]).max()
+    print(f"configs[4] Woodbury apply: max |dz| / max |z| = {err:.3e}")
+    assert err <= 1e-11
