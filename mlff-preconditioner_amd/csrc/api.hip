@@ -387,6 +387,10 @@ int fetch_cols(mlff_ctx *ctx, const int64_t *didx, int64_t k, double *W, int64_t
     return MLFF_OK;
   }
   if (!ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix / operator set");
+  if (mf_columns(ctx, didx, k, ctx->sigma_K, W, ldw)) {  // single-column path, one launch
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
   MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
   for (int64_t j = 0; j < k; ++j) {
     hipLaunchKernelGGL(k_unit_idx, dim3(1), dim3(64), 0, s, ctx->xg, didx, j, ctx->rows_per,

@@ -86,6 +86,12 @@ struct MfData {
   int nz = 1;                             // descriptor slices of the pair sums
   int64_t dslice = 0;
   std::vector<int32_t> perms, piinv;      // host copies (diagonal blocks)
+  // single-column path (kernels_gen.hip k_sgdml_col): (r = i, s = j) records of every
+  // (local point, point, permutation), ni x M x n_perms x (6 n + 2), and device atom maps;
+  // null when the table would exceed kMfColTableBytes (columns then go through the
+  // whole operator)
+  double *uvk = nullptr;
+  int32_t *pi_d = nullptr, *piinv_d = nullptr;
 };
 
 // The scipy stop test of iteration `it` (k_stoptest), done by every workgroup of the
@@ -374,6 +380,17 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
                    int n_atoms, const int32_t *perms, int n_perms, double sig);
 int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,
                       double *R_d_desc);
+// (r = i, s = j) point-pair records of the local points [i0, i0 + ni) (k_sgdml_uv, no mirror)
+void launch_sgdml_records(const double *Rd, const double *Rdd, int64_t M, int n, int64_t D,
+                          int64_t i0, int64_t ni, const int32_t *Pt, const int32_t *piinv,
+                          int n_perms, double sig, double *uvk, hipStream_t s);
+// out[jc * ldo + r] = sigma K_op[row0 + r, col_jc] for the local rows; col_jc = cols[jc]
+// (device array, ncols entries) or, with cols == nullptr and ncols == 1, st->m_pi
+void launch_sgdml_columns(const double *Rdd, int64_t M, int n, int64_t D, int64_t i0,
+                          const int32_t *pi, const int32_t *piinv, int n_perms,
+                          const double *uvk, int64_t row0, int64_t nrows, const int64_t *cols,
+                          int64_t ncols, const DevState *st, double sigma, double *out,
+                          int64_t ldo, hipStream_t s);
 
 // ---- symmetric tiled operator (kernels_sym.hip) -----------------------------
 // build the tiles this rank owns from the dense rows; check_symmetry compares
@@ -410,6 +427,9 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                         const double *x_loc, const int *status, double sigma, double lam,
                         double *pq_part = nullptr);
 int mf_diag(mlff_ctx *ctx, double *out);
+// sigma K_op columns through the single-column path (mf.uvk); false when it is not set up
+bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double sigma,
+                double *out, int64_t ldo);
 // training-set energy pair terms for coefficients alphas (N, contiguous): ni x M n_perms
 int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host);
 // diag(sigma K) of this rank's rows: dense rows or the matrix-free sGDML data

@@ -149,8 +149,11 @@ __global__ __launch_bounds__(256) void k_sgdml_uv(const double *__restrict__ Rd,
                                                   const int32_t *__restrict__ Pt,  // n_perms x D
                                                   const int32_t *__restrict__ piinv,
                                                   double sig, double *__restrict__ uv,
-                                                  int jdiag) {
+                                                  int jdiag, int mirror = 1) {
   // jdiag: only the diagonal blocks j = i (records indexed with j slot 0, M = 1)
+  // mirror = 0: the record of (r, s) = (i, j) for every j -- the block the reference's
+  // matrix-free K_op applies (the query point i, the column point j), used for single
+  // columns of the operator (launch_sgdml_columns)
   const int64_t iloc = blockIdx.y;
   const int64_t i = i0 + iloc;
   const int64_t j = jdiag ? i : (int64_t)blockIdx.x;
@@ -158,8 +161,8 @@ __global__ __launch_bounds__(256) void k_sgdml_uv(const double *__restrict__ Rd,
   const int p = blockIdx.z;
   const int n_perms = gridDim.z;
   const int n3 = 3 * n;
-  const int64_t rp = (j < i) ? i : j;
-  const int64_t sp = (j < i) ? j : i;
+  const int64_t rp = (!mirror || j < i) ? i : j;
+  const int64_t sp = (!mirror || j < i) ? j : i;
   __shared__ double sh[8];
   const double *rdr = Rd + rp * D;
   const double *rds = Rd + sp * D;
@@ -462,6 +465,123 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
   MLFF_HIP(ctx, hipGetLastError());
   (void)M;
   return MLFF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Single columns of the matrix-free operator, S[:, g] = sigma K_op e_g, from the (r = i,
+// s = j) records of the point pairs (mirror = 0 above).  e_g (g = j 3n + 3a + c) touches
+// one training point j, so K_op e_g (predict.py:72-234 with alphas = e_g; the reference's
+// get_col, iterative_cholesky.py:152-156) reduces to the j-column of every query point's
+// Hessian block:
+//   K[(i,b,c'), g] = sum_p 5 m_p u_p[(b,c')] v_p[(a,c)] - w_p G_p[(b,c'), (a,c)],
+//   G_p = J_i^T J_j[P_p]: atom b = pi_p^-1(a) sums over all partners (sgdml_gdiag), every
+//   other atom b has the single partner pi_p^-1(a).
+// O(rows x n_perms) per column instead of a full operator application (O(M^2 D)).
+// Column index: cols[blockIdx.y] (host-chosen sets), or st->m_pi (the device-side pivot
+// of the pivoted Cholesky; no host round trip).  Rows: this rank's [row0, row0 + nrows).
+// One workgroup per (query point, column): wave 0 first sums the partner series of the
+// diagonal atom (b = pi_p^-1 a) lane-parallel for every p into LDS, then the 256 threads
+// write the point's 3n rows.
+constexpr int kColMaxPerms = 64;  // LDS slots for the diagonal-atom sums (more: looped)
+__global__ __launch_bounds__(256) void k_sgdml_col(const double *__restrict__ Rdd, int64_t M,
+                                                   int n, int64_t D, int64_t i0,
+                                                   const int32_t *__restrict__ pi,
+                                                   const int32_t *__restrict__ piinv,
+                                                   int n_perms, const double *__restrict__ uvk,
+                                                   int64_t row0, int64_t nrows,
+                                                   const int64_t *__restrict__ cols,
+                                                   const DevState *__restrict__ st, double sigma,
+                                                   double *__restrict__ out, int64_t ldo) {
+  __shared__ double gd[kColMaxPerms][3];
+  const int64_t g = cols != nullptr ? cols[blockIdx.y] : (int64_t)st->m_pi;
+  if (g < 0) return;
+  const int n3 = 3 * n;
+  const int64_t i = i0 + blockIdx.x;  // query point of this workgroup
+  const int64_t r_lo = i * n3 - row0, r_hi = r_lo + n3;
+  const int64_t lo = r_lo > 0 ? r_lo : 0, hi = r_hi < nrows ? r_hi : nrows;
+  if (lo >= hi) return;
+  const int64_t j = g / n3;
+  const int a = (int)((g % n3) / 3), c = (int)(g % 3);
+  double *o = out + (int64_t)blockIdx.y * ldo;
+  const int64_t rec_stride = 6 * n + 2;
+  const double *rdds = Rdd + j * D * 3;
+  const double *rddr = Rdd + i * D * 3;
+  const double *recs = uvk + ((int64_t)blockIdx.x * M + j) * n_perms * rec_stride;
+  const int lane = threadIdx.x & 63;
+  for (int p0 = 0; p0 < n_perms; p0 += kColMaxPerms) {
+    const int np = n_perms - p0 < kColMaxPerms ? n_perms - p0 : kColMaxPerms;
+    if (threadIdx.x < 64) {
+      for (int q = 0; q < np; ++q) {
+        const int p = p0 + q;
+        const int32_t *pp = pi + (int64_t)p * n;
+        const int b = piinv[(int64_t)p * n + a];  // the row atom whose image is a
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+        for (int x = lane; x < n; x += 64) {
+          if (x == b) continue;
+          const int64_t d = pair_idx(b, x);
+          const int px = pp[x];
+          const double js = pair_sign(a, px) * rdds[pair_idx(a, px) * 3 + c];
+          const double sd = pair_sign(b, x);
+          s0 = fma(sd * rddr[d * 3 + 0], js, s0);
+          s1 = fma(sd * rddr[d * 3 + 1], js, s1);
+          s2 = fma(sd * rddr[d * 3 + 2], js, s2);
+        }
+        s0 = wave_sum(s0);
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) {
+          gd[q][0] = s0;
+          gd[q][1] = s1;
+          gd[q][2] = s2;
+        }
+      }
+    }
+    __syncthreads();
+    for (int64_t r = lo + threadIdx.x; r < hi; r += 256) {
+      const int t = (int)(r - r_lo);
+      const int b = t / 3, cr = t % 3;
+      double acc = p0 == 0 ? 0.0 : o[r];
+      for (int q = 0; q < np; ++q) {
+        const int p = p0 + q;
+        const double *rec = recs + (int64_t)p * rec_stride;
+        const double m5 = 5.0 * rec[6 * n];
+        const double w = rec[6 * n + 1];
+        const int ai = piinv[(int64_t)p * n + a];
+        const double tv = m5 * rec[3 * b + cr] * rec[n3 + 3 * a + c];
+        double gv;
+        if (ai == b) {
+          gv = gd[q][cr];
+        } else {
+          const int64_t d = pair_idx(b, ai);
+          const int pb = pi[(int64_t)p * n + b];
+          gv = pair_sign(b, ai) * rddr[d * 3 + cr] * (pair_sign(a, pb) * rdds[pair_idx(a, pb) * 3 + c]);
+        }
+        acc += tv - w * gv;
+      }
+      o[r] = (p0 + np == n_perms) ? sigma * acc : acc;
+    }
+    __syncthreads();
+  }
+}
+
+void launch_sgdml_records(const double *Rd, const double *Rdd, int64_t M, int n, int64_t D,
+                          int64_t i0, int64_t ni, const int32_t *Pt, const int32_t *piinv,
+                          int n_perms, double sig, double *uvk, hipStream_t s) {
+  if (ni <= 0) return;
+  hipLaunchKernelGGL(k_sgdml_uv, dim3((unsigned)M, (unsigned)ni, (unsigned)n_perms), dim3(256), 0,
+                     s, Rd, Rdd, M, n, D, i0, Pt, piinv, sig, uvk, 0, 0);
+}
+
+void launch_sgdml_columns(const double *Rdd, int64_t M, int n, int64_t D, int64_t i0,
+                          const int32_t *pi, const int32_t *piinv, int n_perms,
+                          const double *uvk, int64_t row0, int64_t nrows, const int64_t *cols,
+                          int64_t ncols, const DevState *st, double sigma, double *out,
+                          int64_t ldo, hipStream_t s) {
+  if (nrows <= 0 || ncols <= 0) return;
+  const int64_t n3 = 3 * (int64_t)n;
+  const int64_t ni = (row0 + nrows + n3 - 1) / n3 - i0;  // local query points
+  hipLaunchKernelGGL(k_sgdml_col, dim3((unsigned)ni, (unsigned)ncols), dim3(256), 0, s, Rdd, M, n, D,
+                     i0, pi, piinv, n_perms, uvk, row0, nrows, cols, st, sigma, out, ldo);
 }
 
 // ---------------------------------------------------------------------------

@@ -35,6 +35,9 @@ namespace mlff {
 namespace {
 
 constexpr int kIC = 16;  // training points per workgroup in the pair / F kernels
+// largest pair-record table of the single-column path (beyond it, columns run through the
+// whole operator as K_op e_i)
+constexpr double kMfColTableBytes = 2.0e9;
 
 __device__ __forceinline__ int64_t xpos(int64_t g, int64_t rows_per, int64_t blk) {
   return (g / rows_per) * blk + g % rows_per;
@@ -520,6 +523,19 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   mf.nz = (int)((D + mf.dslice - 1) / mf.dslice);
   nz = mf.nz;
   MLFF_HIP(ctx, hipMalloc(&mf.part, sizeof(double) * nz * nic * MP));
+  // single-column path: the (r = i, s = j) pair records of the local points (3.5 MB for
+  // the nanotube, M = 14; ni M n_perms (6 n + 2) doubles in general)
+  const double col_bytes = 8.0 * (double)mf.ni * (double)MP * (double)(6 * n + 2);
+  if (mf.ni > 0 && col_bytes <= kMfColTableBytes) {
+    MLFF_HIP(ctx, hipMalloc(&mf.uvk, (size_t)col_bytes));
+    MLFF_HIP(ctx, hipMalloc(&mf.pi_d, sizeof(int32_t) * n_perms * n));
+    MLFF_HIP(ctx, hipMalloc(&mf.piinv_d, sizeof(int32_t) * n_perms * n));
+    MLFF_HIP(ctx, hipMemcpyAsync(mf.pi_d, perms, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
+    MLFF_HIP(ctx, hipMemcpyAsync(mf.piinv_d, piinv.data(), sizeof(int32_t) * n_perms * n,
+                                 hipMemcpyHostToDevice, s));
+    launch_sgdml_records(mf.Rd, mf.Rdd, M, n, D, mf.i0, mf.ni, mf.Pt, mf.piinv_d, n_perms, sig,
+                         mf.uvk, s);
+  }
   if (mf.ni > 0) {
     hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)((MP + kPT - 1) / kPT),
                        (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)nz), dim3(256), 0,
@@ -633,6 +649,15 @@ int mf_diag(mlff_ctx *ctx, double *out) {
   return MLFF_OK;
 }
 
+bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double sigma,
+                double *out, int64_t ldo) {
+  const MfData &mf = ctx->mf;
+  if (mf.uvk == nullptr) return ctx->nrows == 0 && mf.ready;  // an empty shard has no rows
+  launch_sgdml_columns(mf.Rdd, mf.M, mf.n, mf.D, mf.i0, mf.pi_d, mf.piinv_d, mf.n_perms, mf.uvk,
+                       ctx->row0, ctx->nrows, cols, ncols, ctx->st, sigma, out, ldo, ctx->stream);
+  return true;
+}
+
 double mf_bytes(const mlff_ctx *ctx) {
   const MfData &mf = ctx->mf;
   const double MP = (double)(mf.M * mf.n_perms), D = (double)mf.D;
@@ -644,7 +669,8 @@ double mf_bytes(const mlff_ctx *ctx) {
 void mf_free(MfData &mf) {
   for (void *p : {(void *)mf.Rd, (void *)mf.Rdd, (void *)mf.Rt, (void *)mf.Zt, (void *)mf.Pt,
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
-                  (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc})
+                  (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc,
+                  (void *)mf.uvk, (void *)mf.pi_d, (void *)mf.piinv_d})
     if (p) (void)hipFree(p);
   mf = MfData();
 }

@@ -245,6 +245,9 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->perm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
   const bool mfcols = !ctx->has_matrix;  // columns from the matrix-free operator
+  // matrix-free columns: the single-column path (one training point's pair records,
+  // k_sgdml_col) when its table exists, else K_op e_{m_pi} through the whole operator
+  const bool colpath = mfcols && (ctx->mf.uvk != nullptr || ctx->nrows == 0);
   double *colbuf = nullptr, *part = nullptr;
   if (mfcols) {
     MLFF_TRY(operator_diag(ctx, ctx->dwork));
@@ -268,14 +271,17 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
       MLFF_TRY(comm_allgather(ctx, my, wins, 2));
     }
-    double *xunit = mfcols ? ctx->xg : nullptr;
+    double *xunit = (mfcols && !colpath) ? ctx->xg : nullptr;
     hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world,
                        multi ? nullptr : (const double *)pv,
                        multi ? nullptr : (const long long *)pp, np, ctx->perm, m, ctx->row0,
                        nrows, ctx->T, blk, ctx->pivflag, ctx->prow, xunit, ctx->rows_per, blk,
                        ctx->st);
     if (multi && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
-    if (mfcols) launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
+    if (colpath)
+      mf_columns(ctx, nullptr, 1, ctx->sigma_K, colbuf, blk);  // column st->m_pi
+    else if (mfcols)
+      launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
     const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
     if (ks > 0)
       launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s);
@@ -283,7 +289,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
                        (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
                        ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st, xunit);
-    else if (mfcols)
+    else if (mfcols && !colpath)
       hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
                          ctx->st, 0.0);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());

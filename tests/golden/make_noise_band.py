@@ -4,14 +4,18 @@ change of floating-point summation order alone.
 For every golden solve of the reference (tests/golden/sgdml_*.npz, the same list as
 tests/test_gpu_golden.py) the CPU oracle (oracle/: the reference's preconditioner build,
 operator and scipy-1.7.3 CG recurrence restated in NumPy) is re-run with several
-summation orders of the operator and of the preconditioner apply:
+summation orders.  The reference's CG operator is the MATRIX-FREE K_op
+(iterative_solver.py:383-445); a dense K @ v rounds differently (its errors scale with
+||K|| ||v|| through the cancellations of the ill-conditioned K) and measurably shifts the
+counts (+7 iterations on sgdml_ethanol_n270/cholesky for every BLAS order, 0 with
+extended-precision products), so the variants are of the matrix-free operator:
 
-  blas      K @ v, T.T @ (T @ r)                        (the oracle's default order)
-  blk7      7 column blocks, partial products added in block order
-  rev       columns / panel rows in reverse order
-  blk512    512-column tiles (the GPU tile width), added in tile order
-  pair      np.einsum (pairwise, unblocked)
-  ld        extended precision (np.longdouble) products, rounded once (N <= 621 only)
+  mf        oracle.sgdml.kernel_matvec_matrix_free, T.T @ (T @ r)   (the oracle's order)
+  mf_rev    training points summed in reverse order, panel rows reversed
+  mf_split  descriptor dot products in 4 chunks added in chunk order, 7-column-block panel
+  mf_pair   pairwise einsum contractions, 512-column tiles of the panel (the GPU's width)
+  ld        dense K with extended-precision (np.longdouble) products, rounded once
+            (N <= 621: near-exact arithmetic)
 
 and the spread against the reference's recorded solve is written to noise_band.json:
 iteration-count differences and the iteration at which the running-minimum residual first
@@ -92,6 +96,51 @@ def panel(f, precon, K, lam):
     return nystrom_panel(S[:, idx], idx, lam, 1 if precon.endswith("_custom") else 0)
 
 
+def kop_variant(Rd, Rdd, perms, sig, order):
+    """v -> K v by the reference's matrix-free formulation (predict.py:72-234, restated in
+    oracle.sgdml.kernel_matvec_matrix_free) in a given summation order."""
+    from oracle.sgdml import desc_perm
+
+    M, D = Rd.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    P = np.array([desc_perm(p) for p in np.atleast_2d(perms)])
+    s_at, t_at = np.tril_indices(n, k=-1)
+    Rt = Rd[:, P]
+    jorder = np.arange(M)[::-1] if order == "mf_rev" else np.arange(M)
+    chunks = np.array_split(np.arange(D), 4) if order == "mf_split" else [np.arange(D)]
+    sqrt5 = np.sqrt(5.0)
+
+    def dot_d(a, b):  # sum over the last (descriptor) axis in the variant's order
+        if order == "mf_pair":
+            return np.einsum("...d,...d->...", a, b, optimize=False)
+        out = 0.0
+        for c in chunks:
+            out = out + np.sum(a[..., c] * b[..., c], axis=-1)
+        return out
+
+    def mv(x):
+        X = np.asarray(x).reshape(M, n, 3)
+        z = np.einsum("mdc,mdc->md", Rdd, X[:, t_at, :] - X[:, s_at, :])
+        Zt = z[:, P]
+        y = np.empty((M, n, 3))
+        for i in range(M):
+            F = np.zeros(D)
+            for j in jorder:
+                diff = Rd[i][None, :] - Rt[j]                 # n_perms x D
+                norm = sqrt5 * np.sqrt(dot_d(diff, diff))
+                m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+                w = (sig ** 2 + sig * norm) * m
+                a = dot_d(diff, Zt[j])
+                F = F + ((5.0 * m * a)[:, None] * diff - w[:, None] * Zt[j]).sum(axis=0)
+            contrib = Rdd[i] * F[:, None]
+            yi = np.zeros((n, 3))
+            np.add.at(yi, t_at, contrib)
+            np.add.at(yi, s_at, -contrib)
+            y[i] = yi
+        return y.reshape(-1)
+    return mv
+
+
 def make_gemv(A, order):
     """v -> A @ v in a given summation order over the columns of A."""
     n = A.shape[1]
@@ -131,10 +180,14 @@ def run_case(name, precon, orders):
     top = float(np.log10(np.minimum.accumulate(ref_tr)[0]))
     ref_cross = half_decade_crossings(ref_tr, top)
     out = {"n": n, "ref_iters": ref_it, "variants": {}}
+    Rd, Rdd = (f["R_desc"], f["R_d_desc"]) if "R_desc" in f.files else descriptors(f["R"])
+    panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7", "mf_pair": "blk512",
+                   "ld": "ld"}
     for order in orders:
-        mvK = make_gemv(K, order)
-        mvT = make_gemv(T, order)
-        mvTt = make_gemv(np.ascontiguousarray(T.T), order)
+        mvK = (make_gemv(K, "ld") if order == "ld"
+               else kop_variant(Rd, Rdd, f["perms"], float(f["sig"]), order))
+        mvT = make_gemv(T, panel_order[order])
+        mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order[order])
         x, info, tr, it = cg_legacy(lambda v: -mvK(v) + lam * v, y, tol=tol, maxiter=5 * n,
                                     psolve=lambda r: sp * ((r - mvTt(mvT(r))) / lam))
         cross = half_decade_crossings(tr[1:], top)
@@ -156,7 +209,7 @@ def main():
     for name, precon in CASES:
         t0 = time.time()
         n = int(np.load(GOLDEN / f"{name}.npz", allow_pickle=False)["y"].size)
-        orders = ["blas", "blk7", "rev", "blk512", "pair"] + (["ld"] if n <= 621 else [])
+        orders = ["mf", "mf_rev", "mf_split", "mf_pair"] + (["ld"] if n <= 621 else [])
         r = run_case(name, precon, orders)
         res[f"{name}/{precon}"] = r
         print(f"{name:28s} {precon:26s} ref {r['ref_iters']:5d}  "
