@@ -308,8 +308,10 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
                          const int *status, hipStream_t s, StopFold fold = StopFold{},
-                         int64_t cached_rows = 0);
+                         int64_t cached_rows = 0, const long long *tcol = nullptr);
 int choose_ksplit(int64_t k, int64_t ncols);
+// leading rows of a k x ldt panel read with default-policy (MALL-resident) loads
+int64_t panel_cached_rows(int64_t k, int64_t ldt);
 // rho partials of r . r (no preconditioner)
 void launch_dot_part(const double *a, const double *b, int64_t n, double *part,
                      const int *status, hipStream_t s, StopFold fold = StopFold{});

@@ -479,89 +479,76 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
 // O(rows x n_perms) per column instead of a full operator application (O(M^2 D)).
 // Column index: cols[blockIdx.y] (host-chosen sets), or st->m_pi (the device-side pivot
 // of the pivoted Cholesky; no host round trip).  Rows: this rank's [row0, row0 + nrows).
-// One workgroup per (query point, column): wave 0 first sums the partner series of the
-// diagonal atom (b = pi_p^-1 a) lane-parallel for every p into LDS, then the 256 threads
-// write the point's 3n rows.
-constexpr int kColMaxPerms = 64;  // LDS slots for the diagonal-atom sums (more: looped)
-__global__ __launch_bounds__(256) void k_sgdml_col(const double *__restrict__ Rdd, int64_t M,
-                                                   int n, int64_t D, int64_t i0,
-                                                   const int32_t *__restrict__ pi,
-                                                   const int32_t *__restrict__ piinv,
-                                                   int n_perms, const double *__restrict__ uvk,
-                                                   int64_t row0, int64_t nrows,
-                                                   const int64_t *__restrict__ cols,
-                                                   const DevState *__restrict__ st, double sigma,
-                                                   double *__restrict__ out, int64_t ldo) {
-  __shared__ double gd[kColMaxPerms][3];
+// One wave per (64 rows of a query point, column): the rows of atom b = pi_p^-1 a (the
+// diagonal atom of permutation p) need its partner series, which the wave sums
+// lane-parallel first when its rows include that atom; then every lane writes one row.
+// ~250 waves for the nanotube (14 points x 18 row chunks), two dependent load rounds each.
+constexpr int kColRows = 64;
+__global__ __launch_bounds__(64) void k_sgdml_col(const double *__restrict__ Rdd, int64_t M,
+                                                  int n, int64_t D, int64_t i0,
+                                                  const int32_t *__restrict__ pi,
+                                                  const int32_t *__restrict__ piinv,
+                                                  int n_perms, const double *__restrict__ uvk,
+                                                  int64_t row0, int64_t nrows,
+                                                  const int64_t *__restrict__ cols,
+                                                  const DevState *__restrict__ st, double sigma,
+                                                  double *__restrict__ out, int64_t ldo) {
   const int64_t g = cols != nullptr ? cols[blockIdx.y] : (int64_t)st->m_pi;
   if (g < 0) return;
   const int n3 = 3 * n;
-  const int64_t i = i0 + blockIdx.x;  // query point of this workgroup
-  const int64_t r_lo = i * n3 - row0, r_hi = r_lo + n3;
-  const int64_t lo = r_lo > 0 ? r_lo : 0, hi = r_hi < nrows ? r_hi : nrows;
-  if (lo >= hi) return;
+  const int chunks = (n3 + kColRows - 1) / kColRows;
+  const int64_t il = blockIdx.x / chunks;  // local query point
+  const int t0 = (int)(blockIdx.x % chunks) * kColRows;
+  const int64_t i = i0 + il;
+  const int lane = threadIdx.x;
+  const int t = t0 + lane;                  // row of the point's 3n block
+  const int64_t r = i * n3 + t - row0;      // local row
   const int64_t j = g / n3;
   const int a = (int)((g % n3) / 3), c = (int)(g % 3);
-  double *o = out + (int64_t)blockIdx.y * ldo;
   const int64_t rec_stride = 6 * n + 2;
   const double *rdds = Rdd + j * D * 3;
   const double *rddr = Rdd + i * D * 3;
-  const double *recs = uvk + ((int64_t)blockIdx.x * M + j) * n_perms * rec_stride;
-  const int lane = threadIdx.x & 63;
-  for (int p0 = 0; p0 < n_perms; p0 += kColMaxPerms) {
-    const int np = n_perms - p0 < kColMaxPerms ? n_perms - p0 : kColMaxPerms;
-    if (threadIdx.x < 64) {
-      for (int q = 0; q < np; ++q) {
-        const int p = p0 + q;
-        const int32_t *pp = pi + (int64_t)p * n;
-        const int b = piinv[(int64_t)p * n + a];  // the row atom whose image is a
-        double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-        for (int x = lane; x < n; x += 64) {
-          if (x == b) continue;
-          const int64_t d = pair_idx(b, x);
-          const int px = pp[x];
-          const double js = pair_sign(a, px) * rdds[pair_idx(a, px) * 3 + c];
-          const double sd = pair_sign(b, x);
-          s0 = fma(sd * rddr[d * 3 + 0], js, s0);
-          s1 = fma(sd * rddr[d * 3 + 1], js, s1);
-          s2 = fma(sd * rddr[d * 3 + 2], js, s2);
-        }
-        s0 = wave_sum(s0);
-        s1 = wave_sum(s1);
-        s2 = wave_sum(s2);
-        if (lane == 0) {
-          gd[q][0] = s0;
-          gd[q][1] = s1;
-          gd[q][2] = s2;
-        }
+  const double *recs = uvk + (il * M + j) * n_perms * rec_stride;
+  const bool act = t < n3 && r >= 0 && r < nrows;
+  const int b = t / 3, cr = t % 3;
+  double acc = 0.0;
+  for (int p = 0; p < n_perms; ++p) {
+    const int32_t *pp = pi + (int64_t)p * n;
+    const int bd = piinv[(int64_t)p * n + a];  // the row atom whose image is a
+    double gdv = 0.0;
+    if (3 * bd + 2 >= t0 && 3 * bd < t0 + kColRows) {  // wave-uniform: this chunk holds bd
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+      for (int x = lane; x < n; x += 64) {
+        if (x == bd) continue;
+        const int64_t d = pair_idx(bd, x);
+        const int px = pp[x];
+        const double js = pair_sign(a, px) * rdds[pair_idx(a, px) * 3 + c];
+        const double sd = pair_sign(bd, x);
+        s0 = fma(sd * rddr[d * 3 + 0], js, s0);
+        s1 = fma(sd * rddr[d * 3 + 1], js, s1);
+        s2 = fma(sd * rddr[d * 3 + 2], js, s2);
       }
+      s0 = wave_sum(s0);
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      const double s0b = __shfl(s0, 0, 64), s1b = __shfl(s1, 0, 64), s2b = __shfl(s2, 0, 64);
+      gdv = cr == 0 ? s0b : (cr == 1 ? s1b : s2b);
     }
-    __syncthreads();
-    for (int64_t r = lo + threadIdx.x; r < hi; r += 256) {
-      const int t = (int)(r - r_lo);
-      const int b = t / 3, cr = t % 3;
-      double acc = p0 == 0 ? 0.0 : o[r];
-      for (int q = 0; q < np; ++q) {
-        const int p = p0 + q;
-        const double *rec = recs + (int64_t)p * rec_stride;
-        const double m5 = 5.0 * rec[6 * n];
-        const double w = rec[6 * n + 1];
-        const int ai = piinv[(int64_t)p * n + a];
-        const double tv = m5 * rec[3 * b + cr] * rec[n3 + 3 * a + c];
-        double gv;
-        if (ai == b) {
-          gv = gd[q][cr];
-        } else {
-          const int64_t d = pair_idx(b, ai);
-          const int pb = pi[(int64_t)p * n + b];
-          gv = pair_sign(b, ai) * rddr[d * 3 + cr] * (pair_sign(a, pb) * rdds[pair_idx(a, pb) * 3 + c]);
-        }
-        acc += tv - w * gv;
+    if (act) {
+      const double *rec = recs + (int64_t)p * rec_stride;
+      const double m5 = 5.0 * rec[6 * n];
+      const double w = rec[6 * n + 1];
+      const double tv = m5 * rec[3 * b + cr] * rec[n3 + 3 * a + c];
+      double gv = gdv;
+      if (b != bd) {
+        const int64_t d = pair_idx(b, bd);
+        const int pb = pp[b];
+        gv = pair_sign(b, bd) * rddr[d * 3 + cr] * (pair_sign(a, pb) * rdds[pair_idx(a, pb) * 3 + c]);
       }
-      o[r] = (p0 + np == n_perms) ? sigma * acc : acc;
+      acc += tv - w * gv;
     }
-    __syncthreads();
   }
+  if (act) out[(int64_t)blockIdx.y * ldo + r] = sigma * acc;
 }
 
 void launch_sgdml_records(const double *Rd, const double *Rdd, int64_t M, int n, int64_t D,
@@ -580,8 +567,9 @@ void launch_sgdml_columns(const double *Rdd, int64_t M, int n, int64_t D, int64_
   if (nrows <= 0 || ncols <= 0) return;
   const int64_t n3 = 3 * (int64_t)n;
   const int64_t ni = (row0 + nrows + n3 - 1) / n3 - i0;  // local query points
-  hipLaunchKernelGGL(k_sgdml_col, dim3((unsigned)ni, (unsigned)ncols), dim3(256), 0, s, Rdd, M, n, D,
-                     i0, pi, piinv, n_perms, uvk, row0, nrows, cols, st, sigma, out, ldo);
+  const int64_t chunks = (n3 + kColRows - 1) / kColRows;
+  hipLaunchKernelGGL(k_sgdml_col, dim3((unsigned)(ni * chunks), (unsigned)ncols), dim3(64), 0, s, Rdd,
+                     M, n, D, i0, pi, piinv, n_perms, uvk, row0, nrows, cols, st, sigma, out, ldo);
 }
 
 // ---------------------------------------------------------------------------

@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
                                                       double *__restrict__ prow,
                                                       double *__restrict__ xunit,
                                                       int64_t rows_per, int64_t blk,
-                                                      DevState *st) {
+                                                      DevState *st,
+                                                      int64_t *__restrict__ iperm) {
   __shared__ double sv[256];
   __shared__ long long sp[256];
   __shared__ long long s_mpi;
@@ -157,6 +158,8 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
       perm[m] = perm[bp];
       perm[bp] = tmp;
       mpi = perm[m];
+      iperm[mpi] = m;
+      iperm[tmp] = bp;
       if (!(bv > 0.0)) st->pivot_err = 1;
       sq = sqrt(bv);
     } else {
@@ -172,8 +175,10 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
   const long long mpi = s_mpi;
   const int64_t g = mpi - row0;
   const bool own = (mpi >= 0 && g >= 0 && g < nrows);
-  // pivot row L[m_pi, :m] = Lt[:m, m_pi] (zeros on non-owner ranks: summed by allreduce)
-  for (int64_t c = threadIdx.x; c < m; c += 256) prow[c] = own ? Lt[c * ldl + g] : 0.0;
+  // pivot row L[m_pi, :m] = Lt[:m, m_pi] (zeros on non-owner ranks: summed by allreduce);
+  // on one rank (prow == nullptr) the Schur GEMV reads it from Lt itself
+  if (prow != nullptr)
+    for (int64_t c = threadIdx.x; c < m; c += 256) prow[c] = own ? Lt[c * ldl + g] : 0.0;
   if (threadIdx.x == 0 && own) {
     Lt[m * ldl + g] = s_sq;
     pivflag[g] = 1;
@@ -194,13 +199,27 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
                                                  const int *__restrict__ pivflag,
                                                  double *__restrict__ dwork,
                                                  const DevState *__restrict__ st,
-                                                 double *__restrict__ xunit) {
+                                                 double *__restrict__ xunit,
+                                                 const int64_t *__restrict__ iperm,
+                                                 int64_t row0, int64_t N,
+                                                 double *__restrict__ pv,
+                                                 long long *__restrict__ pp) {
+  __shared__ double sv[256];
+  __shared__ long long sp[256];
   const long long mpi = st->m_pi;
-  if (mpi < 0) return;
+  if (mpi < 0) {  // no pivot (error already flagged): an empty candidate set
+    if (threadIdx.x == 0) {
+      pv[blockIdx.x] = -INFINITY;
+      pp[blockIdx.x] = (long long)N;
+    }
+    return;
+  }
   const double sq = st->sqrt_piv;
   const int64_t pos = (mpi / rows_per) * blk + (mpi % rows_per);
   // clears e_{m_pi} set by k_piv_finalize (the operator that read it ran before this kernel)
   if (xunit != nullptr && blockIdx.x == 0 && threadIdx.x == 0) xunit[pos] = 0.0;
+  double bv = -INFINITY;
+  long long bp = (long long)N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nrows;
        i += (int64_t)gridDim.x * 256) {
     if (pivflag[i]) continue;
@@ -217,7 +236,29 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
     for (; ks < ksplit; ++ks) s0 += part[(int64_t)ks * ldp + i];
     const double v = (col - s0) / sq;
     Lt[m * ldl + i] = v;
-    dwork[i] -= v * v;
+    const double dn = dwork[i] - v * v;
+    dwork[i] = dn;
+    // the next step's argmax (k_piv_argmax's order: largest value, then smallest position)
+    const long long pos_i = (long long)iperm[row0 + i];
+    if (better(dn, pos_i, bv, bp)) {
+      bv = dn;
+      bp = pos_i;
+    }
+  }
+  sv[threadIdx.x] = bv;
+  sp[threadIdx.x] = bp;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      if (better(sv[threadIdx.x + o], sp[threadIdx.x + o], sv[threadIdx.x], sp[threadIdx.x])) {
+        sv[threadIdx.x] = sv[threadIdx.x + o];
+        sp[threadIdx.x] = sp[threadIdx.x + o];
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    pv[blockIdx.x] = sv[0];
+    pp[blockIdx.x] = sp[0];
   }
 }
 
@@ -234,16 +275,21 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   hipStream_t s = ctx->stream;
   const int64_t N = ctx->N, nrows = ctx->nrows, blk = ctx->blk;
   const int np = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + 1023) / 1024));
+  const unsigned gcol = (unsigned)std::min<int64_t>((nrows + 255) / 256, 1024);
   ScratchScope scope(ctx);
   double *pv = nullptr, *wins = nullptr;
   long long *pp = nullptr;
-  MLFF_TRY(scratch_alloc(ctx, &pv, np));
-  MLFF_TRY(scratch_alloc(ctx, &pp, np));
+  int64_t *iperm = nullptr;
+  const int npart = std::max<int>(np, (int)gcol);
+  MLFF_TRY(scratch_alloc(ctx, &pv, npart));
+  MLFF_TRY(scratch_alloc(ctx, &pp, npart));
   MLFF_TRY(scratch_alloc(ctx, &wins, 2 * ctx->world));
-  // init: perm = arange(N), dwork = diag(S), pivflag = 0, Lt = 0
+  MLFF_TRY(scratch_alloc(ctx, &iperm, N));
+  // init: perm = iperm = arange(N), dwork = diag(S), pivflag = 0, Lt = 0
   std::vector<int64_t> hperm(N);
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->perm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(iperm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
   const bool mfcols = !ctx->has_matrix;  // columns from the matrix-free operator
   // matrix-free columns: the single-column path (one training point's pair records,
   // k_sgdml_col) when its table exists, else K_op e_{m_pi} through the whole operator
@@ -261,34 +307,44 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
-  const unsigned gcol = (unsigned)std::min<int64_t>((nrows + 255) / 256, 1024);
   for (int64_t m = 0; m < k; ++m) {
-    hipLaunchKernelGGL(k_piv_argmax, dim3(np), dim3(256), 0, s, ctx->dwork, ctx->perm, N, m,
-                       ctx->row0, nrows, pv, pp);
+    // candidates of step m: a scan of the positions [m, N) at m = 0 (and on a rank without
+    // rows), afterwards the per-workgroup winners k_piv_fin left from step m - 1
+    int npc = (int)gcol;
+    if (m == 0 || gcol == 0) {
+      hipLaunchKernelGGL(k_piv_argmax, dim3(np), dim3(256), 0, s, ctx->dwork, ctx->perm, N, m,
+                         ctx->row0, nrows, pv, pp);
+      npc = np;
+    }
     const bool multi = ctx->world > 1;
     if (multi) {
       double *my = wins + 2 * ctx->rank;
-      hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, np, my);
+      hipLaunchKernelGGL(k_piv_rank_winner, dim3(1), dim3(256), 0, s, pv, pp, npc, my);
       MLFF_TRY(comm_allgather(ctx, my, wins, 2));
     }
     double *xunit = (mfcols && !colpath) ? ctx->xg : nullptr;
     hipLaunchKernelGGL(k_piv_finalize, dim3(1), dim3(256), 0, s, wins, ctx->world,
                        multi ? nullptr : (const double *)pv,
-                       multi ? nullptr : (const long long *)pp, np, ctx->perm, m, ctx->row0,
-                       nrows, ctx->T, blk, ctx->pivflag, ctx->prow, xunit, ctx->rows_per, blk,
-                       ctx->st);
+                       multi ? nullptr : (const long long *)pp, npc, ctx->perm, m, ctx->row0,
+                       nrows, ctx->T, blk, ctx->pivflag, multi ? ctx->prow : nullptr, xunit,
+                       ctx->rows_per, blk, ctx->st, iperm);
     if (multi && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
     if (colpath)
       mf_columns(ctx, nullptr, 1, ctx->sigma_K, colbuf, blk);  // column st->m_pi
     else if (mfcols)
       launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
     const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
+    // Schur column GEMV over L[:, :m]; the panel's leading rows (up to 128 MB) are read
+    // with default-policy loads so they stay in the MALL from one step to the next
     if (ks > 0)
-      launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s);
+      launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s, StopFold{},
+                          panel_cached_rows(m, blk),
+                          multi ? nullptr : (const long long *)&ctx->st->m_pi);
     if (gcol > 0)
       hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
                        (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
-                       ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st, xunit);
+                       ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st, xunit, iperm, ctx->row0, N,
+                       pv, pp);
     else if (mfcols && !colpath)
       hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
                          ctx->st, 0.0);

@@ -121,17 +121,22 @@ def kop_variant(Rd, Rdd, perms, sig, order):
     def mv(x):
         X = np.asarray(x).reshape(M, n, 3)
         z = np.einsum("mdc,mdc->md", Rdd, X[:, t_at, :] - X[:, s_at, :])
-        Zt = z[:, P]
+        Zt = z[:, P][jorder]                                  # j order of the sums
+        Rtj = Rt[jorder]
         y = np.empty((M, n, 3))
         for i in range(M):
-            F = np.zeros(D)
-            for j in jorder:
-                diff = Rd[i][None, :] - Rt[j]                 # n_perms x D
-                norm = sqrt5 * np.sqrt(dot_d(diff, diff))
-                m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
-                w = (sig ** 2 + sig * norm) * m
-                a = dot_d(diff, Zt[j])
-                F = F + ((5.0 * m * a)[:, None] * diff - w[:, None] * Zt[j]).sum(axis=0)
+            diff = Rd[i][None, None, :] - Rtj                 # M x n_perms x D
+            norm = sqrt5 * np.sqrt(dot_d(diff, diff))
+            m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+            w = (sig ** 2 + sig * norm) * m
+            a = dot_d(diff, Zt)
+            if order == "mf_pair":
+                F = (np.einsum("jp,jpd->d", 5.0 * m * a, diff, optimize=False)
+                     - np.einsum("jp,jpd->d", w, Zt, optimize=False))
+            else:
+                # axis-0 sums of a C-contiguous array accumulate row after row: j order
+                terms = (5.0 * m * a)[..., None] * diff - w[..., None] * Zt
+                F = terms.reshape(-1, D).sum(axis=0)
             contrib = Rdd[i] * F[:, None]
             yi = np.zeros((n, 3))
             np.add.at(yi, t_at, contrib)
