@@ -204,12 +204,15 @@ int mlff_precon_nystrom(mlff_ctx *ctx, const int64_t *idx, int64_t k, int varian
 /* Woodbury on a caller-supplied factor L (N x k, given as Lt_local: k x nrows):
  * T = chol(lam I + L^T L)^-1 L^T, apply z = (r - T^T T r)/lam. */
 int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k);
-/* Truncated eigen-decomposition of S = sigma_K * K (single rank): the k largest
- * |eigenvalues| s and eigenvectors U (= scipy svd(K) of the reference).
+/* Truncated eigen-decomposition of S = sigma_K * K: the k largest |eigenvalues| s and
+ * eigenvectors U (= scipy svd(K) of the reference), by block subspace iteration on the
+ * operator in any storage (matrix-free included) with Rayleigh-Ritz and a device Jacobi
+ * eigensolver (kernels_eig.hip; no LAPACK).  Collective over the ranks except mask 2.
  * mask_mode 0: K as is ('eigvec_precon'); 1: all entries zeroed
  * ('eigvec_precon_block_diagonal', iterative_solver.py:1255-1261); 2: only same-atom
  * 3x3 blocks and the max-|K| entries kept ('eigvec_precon_atomic_interactions',
- * :1238-1254; dim_i = 3 * n_atoms).  build_woodbury = 1 installs the preconditioner
+ * :1238-1254; dim_i = 3 * n_atoms; needs the dense K and one rank).
+ * build_woodbury = 1 installs the preconditioner
  * L = U sqrt(s)[:, :k] + Woodbury (svd_preconditioner :1313-1329).
  * evals_out (k) and rowlev_out (N, ||U[i, :k]||, :1172-1173) are optional. */
 int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,

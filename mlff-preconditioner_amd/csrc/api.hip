@@ -569,6 +569,21 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
 
 }  // namespace
 
+// y_loc = S x = sigma_K K x (no ridge) for this rank's rows, x given as this rank's block
+// of a distributed vector (blk entries, zero padded): the block is all-gathered into the
+// operand xg first (one collective).  resolve_storage must have run.  Stream ordered.
+int mlff::operator_apply_local(mlff_ctx *ctx, const double *x_loc, double *y_loc) {
+  MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * ctx->blk, x_loc,
+                               sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, ctx->stream));
+  MLFF_TRY(allgather_blocks(ctx, ctx->xg));
+  return launch_operator(ctx, ctx->xg, y_loc, nullptr, nullptr);
+}
+
+int mlff::operator_prepare(mlff_ctx *ctx) {
+  MLFF_TRY(require_operator(ctx));
+  return resolve_storage(ctx);
+}
+
 int mlff::operator_diag(mlff_ctx *ctx, double *out) {
   if (ctx->has_matrix) {
     launch_diag_of(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->sigma_K,
@@ -1222,11 +1237,16 @@ int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int 
                     double *evals_out, double *rowlev_out) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
-  MLFF_TRY(require_matrix(ctx));
-  if (ctx->world != 1) return set_error(ctx, MLFF_ERR_ARG, "eigen preconditioner needs a single rank");
-  if (k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "eig: need 1 <= k <= N");
   if (mask_mode < 0 || mask_mode > 2 || (mask_mode == 2 && (dim_i < 3 || dim_i % 3 != 0)))
     return set_error(ctx, MLFF_ERR_ARG, "eig: bad mask_mode / dim_i");
+  if (mask_mode == 2) {  // the masked matrix is formed from the dense K (one rank)
+    MLFF_TRY(require_matrix(ctx));
+    if (ctx->world != 1)
+      return set_error(ctx, MLFF_ERR_ARG, "eig atomic_interactions mask needs a single rank");
+  } else {
+    MLFF_TRY(require_operator(ctx));
+  }
+  if (k < 1 || k > ctx->N) return set_error(ctx, MLFF_ERR_ARG, "eig: need 1 <= k <= N");
   ctx->precon_kind = MLFF_PRECON_NONE;
   MLFF_TRY(alloc_panel(ctx, k));
   MLFF_TRY(eig_lowrank(ctx, k, mask_mode, dim_i, ctx->T, evals_out, rowlev_out));

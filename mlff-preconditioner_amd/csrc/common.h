@@ -354,6 +354,10 @@ void launch_gemm(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alp
 // G = W W^T (k x k) over ncols columns of W (k x ncols, row stride ldw); split-K
 // with a deterministic slab reduction; work: >= splits * k * k doubles
 int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t ldw, double *G);
+// G = A B^T (k x k) over ncols columns of the wide panels A, B (row stride ldw); split-K
+// with a deterministic slab reduction (syrk_wide is gram_wide(W, W))
+int gram_wide(mlff_ctx *ctx, const double *A, const double *B, int64_t k, int64_t ncols,
+              int64_t ldw, double *G);
 // in-place lower Cholesky of the k x k matrix A (row-major, ld = k)
 int potrf_lower(mlff_ctx *ctx, double *A, int64_t k);
 // W <- L^-1 W, L k x k lower (ld = k), W k x ncols (row stride ldw)
@@ -443,6 +447,12 @@ double mf_bytes(const mlff_ctx *ctx);
 void mf_free(MfData &mf);
 int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,
                      std::vector<int32_t> &Pt, std::vector<int32_t> &piinv);
+
+// ---- operator access for the builds (api.hip) --------------------------------
+// require the operator and resolve its storage (builds the tiles if they are to be used)
+int operator_prepare(mlff_ctx *ctx);
+// y_loc = sigma_K K x over this rank's rows; x_loc = this rank's block (blk entries)
+int operator_apply_local(mlff_ctx *ctx, const double *x_loc, double *y_loc);
 
 // ---- eigen preconditioner (kernels_eig.hip) ----------------------------------
 int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *Lt_out,

@@ -121,6 +121,12 @@ __global__ __launch_bounds__(256) void k_sum_slabs(const double *__restrict__ sl
 }
 
 int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t ldw, double *G) {
+  return gram_wide(ctx, W, W, k, ncols, ldw, G);
+}
+
+int gram_wide(mlff_ctx *ctx, const double *A, const double *Bm, int64_t k, int64_t ncols,
+              int64_t ldw, double *G) {
+  const double *W = A;
   const int64_t tiles = ((k + 63) / 64) * ((k + 63) / 64);
   int64_t splits = (1024 + tiles - 1) / tiles;
   const int64_t max_splits = (ncols + 511) / 512;
@@ -128,14 +134,14 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
   if (splits < 1) splits = 1;
   if (splits > 256) splits = 256;
   if (splits == 1) {
-    gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, W, ldw, 0.0, G, k, 1, 0, ctx->stream);
+    gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, Bm, ldw, 0.0, G, k, 1, 0, ctx->stream);
     MLFF_HIP(ctx, hipGetLastError());
     return MLFF_OK;
   }
   ScratchScope scope(ctx);
   double *slabs = nullptr;
   MLFF_TRY(scratch_alloc(ctx, &slabs, splits * k * k));
-  gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, W, ldw, 0.0, slabs, k, (int)splits, k * k,
+  gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, Bm, ldw, 0.0, slabs, k, (int)splits, k * k,
               ctx->stream);
   const int64_t n = k * k;
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)),

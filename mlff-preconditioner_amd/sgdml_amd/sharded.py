@@ -167,9 +167,15 @@ class ShardedKernelSolver:
     def precon_nystrom(self, idx, variant=0):
         return max(self._each("precon_nystrom", idx, variant))
 
-    def precon_eig(self, *a, **k):
-        raise NotImplementedError("the eigen preconditioners factor all of K on one GPU "
-                                  "(rocSOLVER dsyevd); use a single device")
+    def precon_eig(self, k, mask_mode=0, dim_i=0, build_woodbury=True, want_evals=False,
+                   want_rowlev=False):
+        """Truncated eigensolver over all ranks (evals and global row norms from rank 0);
+        mask_mode 2 needs the dense K on one device."""
+        if mask_mode == 2:
+            raise NotImplementedError("the atomic-interactions mask is formed from the dense K "
+                                      "of one device; use a single device")
+        return self._each("precon_eig", k, mask_mode, dim_i, build_woodbury, want_evals,
+                          want_rowlev)[0]
 
     def lev_scores(self, idx, lam):
         return self._each("lev_scores", idx, lam)[0]  # global scores on every rank

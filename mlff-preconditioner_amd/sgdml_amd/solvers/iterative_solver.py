@@ -11,8 +11,9 @@ AssertionError for a non-PSD pivot, LinAlgError for a failed Cholesky).
 What runs where:
   * the operator is the reference's matrix-free K_op (:383-445) evaluated on the GPU
     from R_desc/R_d_desc; preconditioner builds fetch their columns through it (as
-    IterativeCholesky does), so no N x N matrix is formed -- except for the eigen
-    preconditioners, which factor all of K and assemble it on the GPU first;
+    IterativeCholesky does) and the eigen preconditioners' truncated eigensolver applies
+    it block-wise, so no N x N matrix is formed -- except for
+    eigvec_precon_atomic_interactions, whose masked K is formed from the assembled K;
   * every preconditioner build (pivoted Cholesky, Nystrom, _sb, leverage
     scores, eigen-decomposition) and the PCG iterations run in libmlffpcg.so;
   * column *selection* stays on the host with NumPy's global RNG exactly as in the
@@ -20,8 +21,8 @@ What runs where:
   * several GPUs (`devices=[0, 1, ...]`, or MLFF_DEVICES="0,1,..." / "all"): the rows of
     the operator and of the preconditioner panel are sharded over the devices from this
     one process (sgdml_amd.sharded, RCCL), as the reference spreads its GPU operator
-    with DataParallel (predict.py:335-341).  The eigen preconditioners factor all of K
-    on the first device.
+    with DataParallel (predict.py:335-341).  The atomic-interactions eigen preconditioner
+    masks the dense K on the first device.
 """
 from __future__ import annotations
 
@@ -80,7 +81,7 @@ class Iterative(object):
 
     # ------------------------------------------------------------ helpers
     def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n, dense):
-        """dense: assemble K on the device (the eigen preconditioners factor all of K);
+        """dense: assemble K on the device (the atomic-interactions mask is formed from it);
         otherwise only the matrix-free operator (the reference's K_op) is set up and
         the preconditioner builds fetch their columns through it, as the reference's
         IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory."""
@@ -142,8 +143,9 @@ class Iterative(object):
             n_inducing_pts_init = len(task["inducing_pts_idxs"]) // (3 * n_atoms)
         n_inducing_pts = min(n_train, n_inducing_pts_init)
 
-        dense = str_preconditioner in EIGVEC_KEYS or str_preconditioner in [
-            "rank_k_lev_scores", "rank_k_lev_scores_custom"]
+        # only the atomic-interactions mask is formed from the dense K; the truncated
+        # eigensolver of the other eigen preconditioners runs on the matrix-free operator
+        dense = str_preconditioner == "eigvec_precon_atomic_interactions"
         self.close()  # the previous solve's contexts (operator tables, panel, communicator)
         solver = self._kernel_solver(task, np.asarray(R_desc), np.asarray(R_d_desc),
                                      tril_perms_lin, n, dense)

@@ -58,13 +58,13 @@ def test_sharded_dropin_vs_reference(sg, golden_dir, name, precon, world):
 
 
 @pytest.mark.timeout(300)
-def test_sharded_dropin_eigen_uses_one_device(sg, golden_dir):
-    """eigvec_precon factors all of K: the drop-in keeps it on the first device."""
+def test_sharded_dropin_eigen(sg, golden_dir):
+    """eigvec_precon: the truncated eigensolver runs on the sharded matrix-free operator."""
     name = "sgdml_ethanol_n270"
     f = load(golden_dir, name)
-    (alphas, num_iters, resid, rmse, idxs, is_conv, info), (kind, _) = run(
+    (alphas, num_iters, resid, rmse, idxs, is_conv, info), (kind, w) = run(
         f, name, "eigvec_precon", [0, 0])
-    assert kind is sg.KernelSolver and info["n_gpus"] == 1
+    assert kind is sg.ShardedKernelSolver and w == 2 and info["n_gpus"] == 2
     assert is_conv
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas,
                       int(f["eigvec_precon__num_iters"]), f["eigvec_precon__trace"],
