@@ -261,6 +261,28 @@ int dev_free(void *p) {
   return MLFF_OK;
 }
 
+void rbf_free(mlff_ctx *ctx) {
+  dev_free(ctx->rbf.Xs);
+  ctx->rbf = RbfData();
+}
+
+// the dense rows of the RBF source, generated on first use (DENSE storage, the masked
+// eigen build); the symmetric tiles and every column access go without them
+int ensure_rows(mlff_ctx *ctx) {
+  if (ctx->has_matrix || !ctx->rbf.ready) return MLFF_OK;
+  MLFF_TRY(ensure_matrix(ctx));
+  if (ctx->blk > ctx->nrows)  // zero padding rows
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->K + ctx->nrows * ctx->ld, 0,
+                                 sizeof(double) * (ctx->blk - ctx->nrows) * ctx->ld, ctx->stream));
+  if (ctx->nrows > 0)
+    launch_gen_rbf(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->N,
+                   ctx->rbf.Xs, ctx->rbf.d, ctx->rbf.jitter, ctx->stream);
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->has_matrix = true;
+  return MLFF_OK;
+}
+
 // allreduce (sum) of n doubles in place, no-op on one rank
 int allreduce(mlff_ctx *ctx, double *buf, size_t n) { return comm_allreduce(ctx, buf, n); }
 
@@ -376,13 +398,18 @@ __global__ void k_unit_idx(double *__restrict__ x, const int64_t *__restrict__ i
 }
 
 // W[j, i] = (sigma_K K)[row0 + i, idx_j] for the local rows: a gather from the
-// dense rows, or one matrix-free operator application per column (the
+// dense rows, evaluated from the RBF points, or from the matrix-free sGDML operator (the
 // reference's own column access, K_op.matvec(e_i), iterative_cholesky.py:152-156)
 int fetch_cols(mlff_ctx *ctx, const int64_t *didx, int64_t k, double *W, int64_t ldw) {
   hipStream_t s = ctx->stream;
   if (ctx->has_matrix) {
     launch_gather_cols(ctx->K, ctx->ld, ctx->nrows, didx, k, ctx->rows_per, ctx->blk, ctx->sigma_K,
                        W, ldw, s);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  if (ctx->rbf.ready) {
+    launch_rbf_cols(ctx->rbf, ctx->N, ctx->row0, ctx->nrows, didx, k, nullptr, ctx->sigma_K, W, ldw, s);
     MLFF_HIP(ctx, hipGetLastError());
     return MLFF_OK;
   }
@@ -452,9 +479,9 @@ int check_idx(mlff_ctx *ctx, const int64_t *idx, int64_t k) {
   return MLFF_OK;
 }
 
-// the operator needs K (dense rows) or the matrix-free sGDML data
+// the operator needs K (dense rows), the RBF points or the matrix-free sGDML data
 int require_operator(mlff_ctx *ctx) {
-  if (!ctx->has_matrix && !ctx->mf.ready)
+  if (!ctx->has_matrix && !ctx->mf.ready && !ctx->rbf.ready)
     return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix / operator set");
   if (!ctx->has_operator) return set_error(ctx, MLFF_ERR_STATE, "mlff_set_operator not called");
   return MLFF_OK;
@@ -463,6 +490,7 @@ int require_operator(mlff_ctx *ctx) {
 // preconditioner builds read columns of the dense K
 int require_matrix(mlff_ctx *ctx) {
   MLFF_TRY(require_operator(ctx));
+  MLFF_TRY(ensure_rows(ctx));
   if (!ctx->has_matrix)
     return set_error(ctx, MLFF_ERR_STATE,
                      "this build needs the dense kernel matrix (assemble it first)");
@@ -480,7 +508,7 @@ int resolve_storage(mlff_ctx *ctx) {
     ctx->use_mf = true;
     return MLFF_OK;
   }
-  if (!ctx->has_matrix) {  // only the matrix-free operator exists
+  if (!ctx->has_matrix && !ctx->rbf.ready) {  // only the matrix-free operator exists
     ctx->use_sym = false;
     ctx->use_mf = true;
     return MLFF_OK;
@@ -496,10 +524,17 @@ int resolve_storage(mlff_ctx *ctx) {
     }
   }
   if (ctx->storage == MLFF_STORAGE_DENSE) {
+    MLFF_TRY(ensure_rows(ctx));
     ctx->use_sym = false;
     return MLFF_OK;
   }
   if (ctx->sym.ready) {
+    ctx->use_sym = true;
+    return MLFF_OK;
+  }
+  if (!ctx->has_matrix) {  // RBF source: the tiles are generated from the points
+    bool symmetric = true;
+    MLFF_TRY(sym_build(ctx, false, &symmetric));
     ctx->use_sym = true;
     return MLFF_OK;
   }
@@ -588,6 +623,11 @@ int mlff::operator_diag(mlff_ctx *ctx, double *out) {
   if (ctx->has_matrix) {
     launch_diag_of(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->sigma_K,
                    out, ctx->stream);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  if (ctx->rbf.ready) {  // K[i, i] = 1 + jitter
+    launch_fill(out, ctx->nrows, ctx->sigma_K * (1.0 + ctx->rbf.jitter), ctx->stream);
     MLFF_HIP(ctx, hipGetLastError());
     return MLFF_OK;
   }
@@ -895,6 +935,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   ctx->scratch_chunks.clear();
   sym_free(ctx->sym);
   mf_free(ctx->mf);
+  rbf_free(ctx);
   if (ctx->h_st) hipHostFree(ctx->h_st);
   for (hipEvent_t e : ctx->timing.ev) hipEventDestroy(e);
   if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -972,6 +1013,7 @@ int mlff_set_matrix_host(mlff_ctx *ctx, const double *K_local, int64_t ld_host) 
   ctx->K_symmetric = false;
   ctx->sym.ready = false;
   mf_free(ctx->mf);
+  rbf_free(ctx);
   return MLFF_OK;
   MLFF_API_END(ctx)
 }
@@ -980,19 +1022,33 @@ int mlff_get_matrix_rows(mlff_ctx *ctx, int64_t r0, int64_t nr, double *out, int
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   if (out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
-  if (!ctx->has_matrix) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_matrix && !ctx->rbf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (r0 < 0 || nr < 0 || r0 + nr > ctx->nrows || ld_out < ctx->N)
     return set_error(ctx, MLFF_ERR_ARG, "row range / ld_out");
-  for (int r = 0; r < ctx->world; ++r) {
-    const int64_t g0 = (int64_t)r * ctx->rows_per;
-    if (g0 >= ctx->N) break;
-    const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
-    MLFF_HIP(ctx, hipMemcpy2DAsync(out + g0, sizeof(double) * ld_out,
-                                   ctx->K + r0 * ctx->ld + (int64_t)r * ctx->blk,
-                                   sizeof(double) * ctx->ld, sizeof(double) * cnt, nr,
-                                   hipMemcpyDeviceToHost, ctx->stream));
+  // rows of the dense K, or of the RBF source generated chunk-wise into scratch
+  ScratchScope scope(ctx);
+  const int64_t chunk = ctx->has_matrix ? nr : std::max<int64_t>(1, std::min<int64_t>(nr, (int64_t)(256e6 / (8.0 * ctx->ld))));
+  double *tmp = nullptr;
+  if (!ctx->has_matrix) MLFF_TRY(scratch_alloc(ctx, &tmp, (size_t)chunk * ctx->ld));
+  for (int64_t c0 = 0; c0 < nr; c0 += chunk) {
+    const int64_t cn = std::min<int64_t>(chunk, nr - c0);
+    const double *src = ctx->K + (r0 + c0) * ctx->ld;
+    if (!ctx->has_matrix) {
+      launch_gen_rbf(tmp, ctx->ld, cn, ctx->row0 + r0 + c0, ctx->rows_per, ctx->blk, ctx->N,
+                     ctx->rbf.Xs, ctx->rbf.d, ctx->rbf.jitter, ctx->stream);
+      MLFF_HIP(ctx, hipGetLastError());
+      src = tmp;
+    }
+    for (int r = 0; r < ctx->world; ++r) {
+      const int64_t g0 = (int64_t)r * ctx->rows_per;
+      if (g0 >= ctx->N) break;
+      const int64_t cnt = std::min<int64_t>(ctx->rows_per, ctx->N - g0);
+      MLFF_HIP(ctx, hipMemcpy2DAsync(out + c0 * ld_out + g0, sizeof(double) * ld_out,
+                                     src + (int64_t)r * ctx->blk, sizeof(double) * ctx->ld,
+                                     sizeof(double) * cnt, cn, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   }
-  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MLFF_OK;
   MLFF_API_END(ctx)
 }
@@ -1002,25 +1058,24 @@ int mlff_gen_rbf(mlff_ctx *ctx, const double *X, int d, double length_scale, dou
   MLFF_ENTER(ctx);
   if (X == nullptr || d < 1 || d > 8 || !(length_scale > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "gen_rbf: need X, 1 <= d <= 8, length_scale > 0");
-  MLFF_TRY(ensure_matrix(ctx));
+  // the points (scaled as sklearn does, X / length_scale) are the kernel: tiles, columns,
+  // diagonal and (for the DENSE storage only) the rows are evaluated from them on device
   std::vector<double> Xs((size_t)ctx->N * d);
-  for (size_t i = 0; i < Xs.size(); ++i) Xs[i] = X[i] / length_scale;  // sklearn: X / length_scale
-  double *dX = nullptr;
-  MLFF_HIP(ctx, hipMalloc(&dX, sizeof(double) * Xs.size()));
-  MLFF_HIP(ctx, hipMemcpy(dX, Xs.data(), sizeof(double) * Xs.size(), hipMemcpyHostToDevice));
-  if (ctx->blk > ctx->nrows)  // zero padding rows
-    MLFF_HIP(ctx, hipMemsetAsync(ctx->K + ctx->nrows * ctx->ld, 0,
-                                 sizeof(double) * (ctx->blk - ctx->nrows) * ctx->ld, ctx->stream));
-  if (ctx->nrows > 0)
-    launch_gen_rbf(ctx->K, ctx->ld, ctx->nrows, ctx->row0, ctx->rows_per, ctx->blk, ctx->N, dX, d,
-                   jitter, ctx->stream);
-  MLFF_HIP(ctx, hipGetLastError());
-  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  hipFree(dX);
-  ctx->has_matrix = true;
-  ctx->K_symmetric = true;
-  ctx->sym.ready = false;
+  for (size_t i = 0; i < Xs.size(); ++i) Xs[i] = X[i] / length_scale;
+  sym_free(ctx->sym);
   mf_free(ctx->mf);
+  rbf_free(ctx);
+  if (ctx->K != nullptr) {  // a dense matrix set earlier is not this kernel
+    (void)hipFree(ctx->K);
+    ctx->K = nullptr;
+  }
+  ctx->has_matrix = false;
+  MLFF_HIP(ctx, hipMalloc(&ctx->rbf.Xs, sizeof(double) * Xs.size()));
+  MLFF_HIP(ctx, hipMemcpy(ctx->rbf.Xs, Xs.data(), sizeof(double) * Xs.size(), hipMemcpyHostToDevice));
+  ctx->rbf.d = d;
+  ctx->rbf.jitter = jitter;
+  ctx->rbf.ready = true;
+  ctx->K_symmetric = true;
   return MLFF_OK;
   MLFF_API_END(ctx)
 }
@@ -1031,6 +1086,7 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: null input or sig <= 0");
+  rbf_free(ctx);
   MLFF_TRY(ensure_matrix(ctx));
   MLFF_TRY(assemble_sgdml(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
   // the matrix-free form of the same operator (chosen by MLFF_STORAGE_AUTO when cheaper)
@@ -1048,6 +1104,7 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_ENTER(ctx);
   if (R_desc == nullptr || R_d_desc == nullptr || perms == nullptr || !(sig > 0.0))
     return set_error(ctx, MLFF_ERR_ARG, "sgdml_operator: null input or sig <= 0");
+  rbf_free(ctx);
   MLFF_TRY(mf_setup(ctx, R_desc, R_d_desc, M, n_atoms, perms, n_perms, sig));
   ctx->use_mf = false;
   ctx->has_matrix = false;  // a dense K set earlier is not this operator
@@ -1148,7 +1205,8 @@ int mlff_matvec(mlff_ctx *ctx, const double *v_global, double *y_local) {
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
-  if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_matrix && !ctx->mf.ready && !ctx->rbf.ready)
+    return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   MLFF_TRY(operator_diag(ctx, ctx->dwork));
   if (ctx->nrows > 0)
     MLFF_HIP(ctx, hipMemcpyAsync(diag_local, ctx->dwork, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, ctx->stream));
@@ -1314,7 +1372,8 @@ int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out) {
 int mlff_lev_scores(mlff_ctx *ctx, const int64_t *idx, int64_t k, double lam, double *scores_out) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
-  if (!ctx->has_matrix && !ctx->mf.ready) return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
+  if (!ctx->has_matrix && !ctx->mf.ready && !ctx->rbf.ready)
+    return set_error(ctx, MLFF_ERR_STATE, "no kernel matrix set");
   if (!(lam > 0.0) || scores_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "lev_scores: bad args");
   MLFF_TRY(check_idx(ctx, idx, k));
   hipStream_t s = ctx->stream;

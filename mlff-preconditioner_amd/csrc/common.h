@@ -94,6 +94,32 @@ struct MfData {
   int32_t *pi_d = nullptr, *piinv_d = nullptr;
 };
 
+// Synthetic RBF kernel source (tools/utils.py:173-187): the points, scaled by 1 / length
+// scale, stay on the device and every consumer evaluates K from them -- the symmetric
+// tiles are generated directly, columns / the diagonal / requested rows on demand -- so no
+// dense N x N copy exists unless the DENSE storage asks for it (mlff_gen_rbf).
+struct RbfData {
+  bool ready = false;
+  double *Xs = nullptr;  // N x d
+  int d = 0;
+  double jitter = 0.0;
+};
+
+// K[i, g] (i != g) of the sklearn RBF kernel: exp(-0.5 * sum_t (xs_i - xs_g)^2), the
+// squared distance formed without FMA contraction (scipy pdist 'sqeuclidean' order).
+// (xs_i - xs_g)^2 == (xs_g - xs_i)^2 exactly, so the generated kernel is exactly symmetric.
+__device__ __forceinline__ double rbf_value(const double (&xi)[8], const double *__restrict__ Xs,
+                                            int64_t g, int d) {
+  double s = 0.0;
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+    if (t < d) {
+      const double df = __dsub_rn(xi[t], Xs[g * d + t]);
+      s = __dadd_rn(s, __dmul_rn(df, df));
+    }
+  return exp(-0.5 * s);
+}
+
 // The scipy stop test of iteration `it` (k_stoptest), done by every workgroup of the
 // next iteration's first kernel instead of a launch of its own (rr_part == nullptr: none).
 struct StopFold {
@@ -164,6 +190,7 @@ struct mlff_ctx {
   bool use_mf = false;              // resolved: matrix-free sGDML operator in use
   mlff::SymPack sym;
   mlff::MfData mf;                  // matrix-free sGDML operator (optional)
+  mlff::RbfData rbf;                // synthetic RBF kernel from its points (optional)
 
   // CG vectors.  local: blk entries; p_full / xg: ld entries (rank blocks)
   double *x = nullptr, *r = nullptr, *z = nullptr, *q = nullptr, *b = nullptr;
@@ -382,6 +409,12 @@ void launch_gather_cols(const double *K, int64_t ld, int64_t nrows, const int64_
 // Smm[j, j'] = W[j, idx_j' - row0] if idx_j' is local else 0
 void launch_gather_mm(const double *W, int64_t ldw, const int64_t *idx, int64_t k,
                       int64_t row0, int64_t nrows, double *Smm, hipStream_t s);
+// out[jc * ldo + r] = sigma K[row0 + r, col_jc] of the RBF source for the local rows;
+// col_jc = cols[jc] (device, ncols) or, with cols == nullptr, st->m_pi
+void launch_rbf_cols(const RbfData &rbf, int64_t N, int64_t row0, int64_t nrows,
+                     const int64_t *cols, int64_t ncols, const DevState *st, double sigma,
+                     double *out, int64_t ldo, hipStream_t s);
+void launch_fill(double *y, int64_t n, double v, hipStream_t s);
 int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                    int n_atoms, const int32_t *perms, int n_perms, double sig);
 int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,

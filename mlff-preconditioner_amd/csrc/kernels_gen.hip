@@ -32,22 +32,52 @@ __global__ __launch_bounds__(256) void k_gen_rbf(double *__restrict__ K, int64_t
     const int64_t rk = pos / blk, off = pos % blk;
     const int64_t g = rk * rows_per + off;
     double val = 0.0;
-    if (off < rows_per && g < N) {
-      if (g == gi) {
-        val = 1.0 + jitter;
-      } else {
-        double s = 0.0;
-#pragma unroll
-        for (int t = 0; t < 8; ++t)
-          if (t < d) {
-            const double df = __dsub_rn(xi[t], Xs[g * d + t]);
-            s = __dadd_rn(s, __dmul_rn(df, df));
-          }
-        val = exp(-0.5 * s);
-      }
-    }
+    if (off < rows_per && g < N) val = (g == gi) ? 1.0 + jitter : rbf_value(xi, Xs, g, d);
     __builtin_nontemporal_store(val, row + pos);
   }
+}
+
+// columns of the RBF kernel for the local rows (the Nystrom / pivoted-Cholesky column
+// fetch of the RBF source): out[jc * ldo + r] = sigma K[row0 + r, g_jc]
+__global__ __launch_bounds__(256) void k_rbf_cols(const double *__restrict__ Xs, int d,
+                                                  double jitter, int64_t row0, int64_t nrows,
+                                                  const int64_t *__restrict__ cols,
+                                                  const DevState *__restrict__ st, double sigma,
+                                                  double *__restrict__ out, int64_t ldo) {
+  const int64_t g = cols != nullptr ? cols[blockIdx.y] : (int64_t)st->m_pi;
+  if (g < 0) return;
+  double xg[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) xg[t] = (t < d) ? Xs[g * d + t] : 0.0;
+  double *o = out + (int64_t)blockIdx.y * ldo;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows;
+       r += (int64_t)gridDim.x * 256) {
+    const int64_t gi = row0 + r;
+    // K[gi, g] = K[g, gi]: evaluated with the column point first, as the tiles store it
+    // for gi > g and the rows for g > gi -- the same bits either way
+    o[r] = sigma * ((gi == g) ? 1.0 + jitter : rbf_value(xg, Xs, gi, d));
+  }
+}
+
+void launch_rbf_cols(const RbfData &rbf, int64_t N, int64_t row0, int64_t nrows,
+                     const int64_t *cols, int64_t ncols, const DevState *st, double sigma,
+                     double *out, int64_t ldo, hipStream_t s) {
+  (void)N;
+  if (nrows <= 0 || ncols <= 0) return;
+  const unsigned gx = (unsigned)std::min<int64_t>((nrows + 255) / 256, 64);
+  hipLaunchKernelGGL(k_rbf_cols, dim3(gx, (unsigned)ncols), dim3(256), 0, s, rbf.Xs, rbf.d,
+                     rbf.jitter, row0, nrows, cols, st, sigma, out, ldo);
+}
+
+__global__ void k_fill(double *__restrict__ y, int64_t n, double v) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    y[i] = v;
+}
+
+void launch_fill(double *y, int64_t n, double v, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 1024)), dim3(256), 0, s,
+                     y, n, v);
 }
 
 void launch_gen_rbf(double *K, int64_t ld, int64_t nrows, int64_t row0, int64_t rows_per,

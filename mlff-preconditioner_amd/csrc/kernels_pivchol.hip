@@ -290,12 +290,14 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   for (int64_t i = 0; i < N; ++i) hperm[i] = i;
   MLFF_HIP(ctx, hipMemcpyAsync(ctx->perm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(iperm, hperm.data(), sizeof(int64_t) * N, hipMemcpyHostToDevice, s));
-  const bool mfcols = !ctx->has_matrix;  // columns from the matrix-free operator
-  // matrix-free columns: the single-column path (one training point's pair records,
-  // k_sgdml_col) when its table exists, else K_op e_{m_pi} through the whole operator
-  const bool colpath = mfcols && (ctx->mf.uvk != nullptr || ctx->nrows == 0);
+  // column sources: the dense rows; the RBF points (k_rbf_cols); the matrix-free sGDML
+  // operator -- its single-column path (one training point's pair records, k_sgdml_col)
+  // when the table exists, else K_op e_{m_pi} through the whole operator
+  const bool rbfcols = !ctx->has_matrix && ctx->rbf.ready;
+  const bool mfcols = !ctx->has_matrix && !rbfcols;
+  const bool colpath = rbfcols || (mfcols && (ctx->mf.uvk != nullptr || ctx->nrows == 0));
   double *colbuf = nullptr, *part = nullptr;
-  if (mfcols) {
+  if (!ctx->has_matrix) {
     MLFF_TRY(operator_diag(ctx, ctx->dwork));
     MLFF_TRY(scratch_alloc(ctx, &colbuf, blk));
     MLFF_HIP(ctx, hipMemsetAsync(ctx->xg, 0, sizeof(double) * ctx->ld, s));
@@ -329,7 +331,9 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                        nrows, ctx->T, blk, ctx->pivflag, multi ? ctx->prow : nullptr, xunit,
                        ctx->rows_per, blk, ctx->st, iperm);
     if (multi && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
-    if (colpath)
+    if (rbfcols)
+      launch_rbf_cols(ctx->rbf, N, ctx->row0, nrows, nullptr, 1, ctx->st, ctx->sigma_K, colbuf, blk, s);
+    else if (colpath)
       mf_columns(ctx, nullptr, 1, ctx->sigma_K, colbuf, blk);  // column st->m_pi
     else if (mfcols)
       launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);

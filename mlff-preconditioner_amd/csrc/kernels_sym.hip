@@ -572,6 +572,44 @@ __global__ __launch_bounds__(256) void k_sym_pack(const double *__restrict__ K, 
   if (COMPARE && bad) atomicOr(mismatch, 1);
 }
 
+// Generate one stored tile per workgroup directly from the RBF points (no dense rows):
+// tile (I, J) element (r, c) = K[pos I B + r, pos J B + c] in the padded rank-block index
+// space (zero outside [0, N)); each thread owns 2 columns and walks the 512 rows
+// (non-temporal 4-KB row stores)
+__global__ __launch_bounds__(256) void k_sym_gen_rbf(const int2 *__restrict__ list,
+                                                     const double *__restrict__ Xs, int d,
+                                                     double jitter, int64_t N, int64_t rows_per,
+                                                     int64_t blk, double *__restrict__ tiles) {
+  const int2 t = list[blockIdx.x];
+  double *T = tiles + (int64_t)blockIdx.x * B * B;
+  double xc[2][8];
+  int64_t gc[2];
+  bool vc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int64_t pos = (int64_t)t.y * B + threadIdx.x + 256 * h;
+    const int64_t off = pos % blk;
+    gc[h] = (pos / blk) * rows_per + off;
+    vc[h] = off < rows_per && gc[h] < N;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xc[h][u] = (vc[h] && u < d) ? Xs[gc[h] * d + u] : 0.0;
+  }
+  for (int r = 0; r < B; ++r) {
+    const int64_t pos = (int64_t)t.x * B + r;
+    const int64_t off = pos % blk;
+    const int64_t gr = (pos / blk) * rows_per + off;
+    const bool vr = off < rows_per && gr < N;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double val = 0.0;
+      // K[gr, gc] evaluated from the column point (rbf_value(x_gc, gr)): bitwise the same
+      // as from the row point, see common.h
+      if (vr && vc[h]) val = (gr == gc[h]) ? 1.0 + jitter : rbf_value(xc[h], Xs, gr, d);
+      __builtin_nontemporal_store(val, T + (int64_t)r * B + threadIdx.x + 256 * h);
+    }
+  }
+}
+
 }  // namespace
 
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
@@ -745,8 +783,14 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     const int64_t rowbase = (int64_t)ctx->rank * ctx->blk;
     const double *Ksrc = ctx->K;
     const int64_t ldsrc = ctx->ld;
-    hipLaunchKernelGGL(k_sym_pack<false>, dim3((unsigned)nt), dim3(256), 0, s, Ksrc, ldsrc, rowbase,
-                       ctx->blk, sp.list, dtrans, sp.tiles, dflag);
+    if (!ctx->has_matrix && ctx->rbf.ready) {  // generated from the points (no dense rows)
+      hipLaunchKernelGGL(k_sym_gen_rbf, dim3((unsigned)nt), dim3(256), 0, s, sp.list, ctx->rbf.Xs,
+                         ctx->rbf.d, ctx->rbf.jitter, ctx->N, ctx->rows_per, ctx->blk, sp.tiles);
+      check_symmetry = false;
+    } else {
+      hipLaunchKernelGGL(k_sym_pack<false>, dim3((unsigned)nt), dim3(256), 0, s, Ksrc, ldsrc, rowbase,
+                         ctx->blk, sp.list, dtrans, sp.tiles, dflag);
+    }
     int mism = 0;
     if (check_symmetry) {
       // mirror read: every tile compared against rows J B + c (one rank holds all rows)
