@@ -4,14 +4,17 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2]): synthetic SPD RBF
-kernel, N = 65536 points x ~ U[0,1)^3 (numpy default_rng seed 0), length scale
-0.2, A = K + 1e-6 I, b = sum(x^2), rank-256 Nystrom preconditioner on uniform
-random columns (`random_scores`, seed 0).  K is generated on the GPU (inputs
-resident in HBM before the timed region).  A step = one PCG iteration (the
-fp64 mat-vec over the whole N x N matrix + preconditioner apply + CG updates).
-With N GPUs the same problem is row-sharded (strong scaling); the mat-vec
-operand is all-gathered and the dot products all-reduced over RCCL.
+Workload: synthetic SPD RBF kernel, x ~ U[0,1)^3 (numpy default_rng seed 0), length
+scale 0.2, A = K + 1e-6 I, b = sum(x^2), rank-256 Nystrom preconditioner on uniform
+random columns (`random_scores`, seed 0):
+  --gpus 1:  N = 65536  (BASELINE.json configs[2])
+  --gpus >1: N = 131072 (configs[3], "row-sharded mat-vec + RCCL, 8 x MI355X"): the same
+             problem at 2, 4 and 8 GPUs (strong scaling within configs[3]; --n overrides)
+K is generated on the GPU straight into the symmetric tiles from the points (inputs
+resident in HBM before the timed region; no dense N x N copy).  A step = one PCG
+iteration (the fp64 mat-vec over the whole N x N matrix + preconditioner apply + CG
+updates); with several GPUs the rows are sharded and the iteration runs three RCCL
+collectives (allgather of z, reduce-scatter of the partial K p, allreduce of ||r||^2 | T r).
 
 Prints one JSON line (rank 0) with the driver's keys plus
   roofline:     algorithmic bytes/launch of the K mat-vec / its mean HIP-event
@@ -48,7 +51,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--n", type=int, default=None,
+                    help="kernel size (default 65536 = configs[2] on one GPU, 131072 = "
+                         "configs[3] on several)")
     ap.add_argument("--k", type=int, default=None,
                     help="preconditioner rank (rbf: 256; sGDML: the rule of thumb, e.g. 2701 "
                          "for the nanotube; configs[4] uses 1024)")
@@ -56,13 +61,14 @@ def parse():
     ap.add_argument("--ell", type=float, default=0.2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-solve", action="store_true", help="skip the solve-to-1e-6 legs")
-    ap.add_argument("--cpu-iters", type=int, default=100,
-                    help="PCG iterations of the CPU baseline (~10-20 s of host work at N=65536)")
+    ap.add_argument("--cpu-iters", type=int, default=30,
+                    help="PCG iterations per CPU-baseline sample (3 samples, median; ~5 s each "
+                         "at N=65536 on 16 cores)")
     ap.add_argument("--cpu-iters-sgdml", type=int, default=20,
                     help="PCG iterations of the CPU baseline of the sGDML workloads (~0.45 s each "
                          "at the nanotube size)")
-    ap.add_argument("--cpu-iters-1t", type=int, default=3,
-                    help="PCG iterations of the single-thread CPU baseline")
+    ap.add_argument("--cpu-iters-1t", type=int, default=2,
+                    help="PCG iterations per single-thread CPU-baseline sample (3 samples)")
     ap.add_argument("--workload", choices=["rbf", "nanotube", "ethanol"], default="rbf",
                     help="rbf: configs[2] (default); nanotube: configs[1] (sGDML N=15540, "
                          "pivoted Cholesky k=2701 built on the GPU); ethanol: configs[0] geometry")
@@ -147,6 +153,38 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def usable_cores() -> dict:
+    """Physical cores this process may use: the CPU affinity set (sched_getaffinity) in
+    whole cores, capped by the cgroup CPU quota (cpu.max) -- the GPU box allots a CPU
+    share per GPU, and BLAS threads beyond it only time-slice."""
+    aff = len(os.sched_getaffinity(0))
+    tpc = 1
+    try:
+        sib = open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list").read().strip()
+        tpc = sum((int(b) - int(a) + 1) if "-" in x else 1
+                  for x in sib.split(",") for a, b in [((x.split("-") + [x])[:2])])
+    except (OSError, ValueError):
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    cores = max(1, aff // max(tpc, 1))
+    if quota is not None:
+        cores = max(1, min(cores, int(quota)))
+    return {"cores": cores, "affinity_cpus": aff, "threads_per_core": tpc,
+            "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count()}
+
+
+def _median_rate(fn, samples=3):
+    """fn() -> seconds per iteration; median over `samples` runs (and the spread)."""
+    per = sorted(fn() for _ in range(samples))
+    return per[len(per) // 2], per
+
+
 def _time_pcg(mv, psolve, b, m):
     """Seconds per oracle PCG iteration (after one warm-up iteration) and per mat-vec."""
     from oracle.pcg import cg_legacy
@@ -174,19 +212,21 @@ def cpu_baseline_sgdml(solver, Rd, Rdd, perms, b, lam, iters):
     from oracle.sgdml import kernel_matvec_matrix_free
 
     T = solver.precon_panel()
-    info = threadpoolctl.threadpool_info()
-    threads = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+    cpus = usable_cores()
 
     def mv(v):
         return -kernel_matvec_matrix_free(Rd, Rdd, perms, 10.0, v) + lam * v
 
-    per_it, t_mv = _time_pcg(mv, lambda r: apply_panel(T, 1.0, lam, r), b, iters)
-    return {"value": 1.0 / per_it, "unit": "CG iters/s", "cores": int(threads), "kind": "port",
-            "sample": f"{iters} PCG iterations (oracle cg_legacy + matrix-free sGDML K_op + "
-                      f"Woodbury apply of the GPU-built rank-{T.shape[0]} panel, NumPy) at "
-                      f"N={b.size}",
-            "ms_per_iter": per_it * 1e3, "matvec_ms": t_mv * 1e3, "host_cpu": _cpu_model(),
-            "os_cpu_count": os.cpu_count()}
+    psolve = lambda r: apply_panel(T, 1.0, lam, r)  # noqa: E731
+    with threadpoolctl.threadpool_limits(limits=cpus["cores"], user_api="blas"):
+        per_it, spread = _median_rate(lambda: _time_pcg(mv, psolve, b, iters)[0])
+        t_mv = _time_pcg(mv, psolve, b, 1)[1]
+    return dict({"value": 1.0 / per_it, "unit": "CG iters/s", "cores": cpus["cores"], "kind": "port",
+                 "sample": f"median of 3 x {iters} PCG iterations (oracle cg_legacy + matrix-free "
+                           f"sGDML K_op + Woodbury apply of the GPU-built rank-{T.shape[0]} panel, "
+                           f"NumPy) at N={b.size}",
+                 "ms_per_iter": per_it * 1e3, "ms_per_iter_samples": [t * 1e3 for t in spread],
+                 "matvec_ms": t_mv * 1e3, "host_cpu": _cpu_model()}, **cpus)
 
 
 def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
@@ -200,8 +240,7 @@ def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
     n = b.size
     K = solver.get_matrix_rows()
     B, sp = nystrom_panel(K[:, idx], idx, lam, 0)
-    info = threadpoolctl.threadpool_info()
-    threads = max([i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"] or [1])
+    cpus = usable_cores()
 
     def mv(v):
         y = K @ v
@@ -209,22 +248,25 @@ def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
         return y
 
     psolve = lambda r: apply_panel(B, sp, lam, r)  # noqa: E731
-    per_it, t_mv = _time_pcg(mv, psolve, b, iters)
+    with threadpoolctl.threadpool_limits(limits=cpus["cores"], user_api="blas"):
+        per_it, spread = _median_rate(lambda: _time_pcg(mv, psolve, b, iters)[0])
+        t_mv = _time_pcg(mv, psolve, b, 1)[1]
     one = None
     if iters_1t > 0:
         with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
-            p1, t1 = _time_pcg(mv, psolve, b, iters_1t)
+            p1, s1 = _median_rate(lambda: _time_pcg(mv, psolve, b, iters_1t)[0])
         one = {"value": 1.0 / p1, "cores": 1, "ms_per_iter": p1 * 1e3,
-               "matvec_gbs": (8.0 * n * n) / (t1 * 1e9), "sample": f"{iters_1t} PCG iterations"}
+               "ms_per_iter_samples": [t * 1e3 for t in s1],
+               "sample": f"median of 3 x {iters_1t} PCG iterations"}
     del K
-    return {"value": 1.0 / per_it, "unit": "CG iters/s", "cores": int(threads), "kind": "port",
-            "sample": f"{iters} PCG iterations (oracle cg_legacy + Nystrom apply, NumPy/OpenBLAS) "
-                      f"on the same N={n} fp64 matrix copied from the GPU",
-            "ms_per_iter": per_it * 1e3,
-            "matvec_gbs": (8.0 * n * n) / (t_mv * 1e9),
-            "host_cpu": _cpu_model(),
-            "os_cpu_count": os.cpu_count(),
-            "single_thread": one}
+    return dict({"value": 1.0 / per_it, "unit": "CG iters/s", "cores": cpus["cores"], "kind": "port",
+                 "sample": f"median of 3 x {iters} PCG iterations (oracle cg_legacy + Nystrom "
+                           f"apply, NumPy/OpenBLAS) on the same N={n} fp64 matrix copied from "
+                           f"the GPU",
+                 "ms_per_iter": per_it * 1e3, "ms_per_iter_samples": [t * 1e3 for t in spread],
+                 "matvec_gbs": (8.0 * n * n) / (t_mv * 1e9),
+                 "host_cpu": _cpu_model(),
+                 "single_thread": one}, **cpus)
 
 
 def parity_small(n, k, lam, ell, tol=1e-6):
@@ -298,7 +340,7 @@ def solo_profile(args):
     from sgdml_amd import synthetic
 
     W, R = args.solo_world, args.solo_rank
-    n, k, ell = args.n, (args.k or 256), args.ell
+    n, k, ell = (args.n or 131072), (args.k or 256), args.ell
     X, b = synthetic.rbf_points(n, 3, 0)
     s = sgdml_amd.KernelSolver(n, device=0, rank=R, world=W, comm_id=b"SOLO:")
     try:
@@ -344,6 +386,8 @@ def main():
     import sgdml_amd
     from sgdml_amd import synthetic
 
+    if args.n is None:
+        args.n = 65536 if world == 1 else 131072
     n, k, lam, ell = args.n, (args.k or 256), args.lam, args.ell
     sg_info = None
     if args.workload == "rbf":
@@ -364,6 +408,8 @@ def main():
     t0 = time.perf_counter()
     storage, op_bytes = solver.storage_info()  # builds the symmetric tiles (setup)
     t_pack = time.perf_counter() - t0
+    free_b, total_b = solver.device_memory()
+    used_gb = max_over_ranks(pg, (total_b - free_b) / 1e9)
     r0, r1 = solver.row_range()
     b_loc = np.ascontiguousarray(b[r0:r1])
     # tol = 0: never converges, so exactly warmup + steps iterations run
@@ -381,6 +427,14 @@ def main():
     tm = solver.timing_read()
     gemv_ms = tm["gemv_ms"] / max(tm["gemv_count"], 1)
     iter_ms = tm["iter_ms"] / max(tm["iter_count"], 1)
+    comm = None
+    if world > 1:
+        # HIP-event time of the RCCL collectives on this rank's stream (waits for the
+        # slowest peer included): per iteration and per collective, max over ranks
+        comm = {"ms_per_iter": max_over_ranks(pg, tm["comm_ms"] / max(tm["iter_count"], 1)),
+                "collectives_per_iter": tm["comm_count"] / max(tm["iter_count"], 1),
+                "ms_per_collective": max_over_ranks(pg, tm["comm_ms"] / max(tm["comm_count"], 1)),
+                "operator_ms_max_rank": max_over_ranks(pg, gemv_ms)}
     nloc = r1 - r0
     gemv_bytes = op_bytes  # algorithmic bytes of this rank's operator launch
     achieved = gemv_bytes / (gemv_ms * 1e-3) / 1e9
@@ -451,7 +505,11 @@ def main():
             if args.workload == "nanotube" and n == 15540 else None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": workload, "n": n, "k": k, "lambda": lam,
+            "config": {"workload": workload,
+                       "baseline_config": ("configs[3]" if n == 131072 else
+                                           "configs[2]" if n == 65536 else None)
+                       if sg_info is None else ("configs[1]" if n == 15540 else None),
+                       "n": n, "k": k, "lambda": lam,
                        "length_scale": ell if sg_info is None else 10.0,
                        "precon": "random_scores (Nystrom, iterative_solver.py:95-322)"
                        if sg_info is None else
@@ -466,6 +524,8 @@ def main():
             # with half storage also report against the dense 8 N^2 bytes
             "matvec_gbs_dense_equivalent": dense_equiv,
             "iter_device_ms": iter_ms,
+            "rccl": comm,
+            "device_memory_used_gb_max_rank": used_gb,
             "iter_gbs_algorithmic": per_iter_bytes / (iter_ms * 1e-3) / 1e9,
             "cpu_baseline": cpu,
             "solve_to_1e-6": solve,

@@ -254,7 +254,12 @@ int mlff_timing_read(mlff_ctx *ctx, double *gemv_ms, int64_t *gemv_count, double
 /* summed HIP-event time of the low-rank preconditioner apply (T r, T^T t, z) inside
  * mlff_pcg_run while timing is on (one rank) */
 int mlff_timing_read_precon(mlff_ctx *ctx, double *ms, int64_t *count);
+/* summed HIP-event time of the collectives of the sharded iteration (allgather of z,
+ * reduce-scatter / allreduce of p.q, allreduce of ||r||^2 | T r) and their count */
+int mlff_timing_read_comm(mlff_ctx *ctx, double *ms, int64_t *count);
 int mlff_timing_reset(mlff_ctx *ctx);
+/* free / total bytes of the context's device (hipMemGetInfo) */
+int mlff_device_memory(mlff_ctx *ctx, int64_t *free_out, int64_t *total_out);
 
 #ifdef __cplusplus
 }

@@ -711,7 +711,9 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   } else {
     launch_copy_dot(ctx->r, ctx->nrows, zg, zg + ctx->blk, status, s, fold);
   }
+  size_t c0 = mark_begin(ctx, marks);
   MLFF_TRY(comm_allgather(ctx, zg, ctx->gb, (size_t)ctx->gstride));
+  mark_end(ctx, marks, c0, it, 2);
   launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
                            status, s);
   const size_t e0 = mark_begin(ctx, marks);
@@ -720,24 +722,32 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
     launch_symv(sp, ctx->p_full, sp.P, status, s);
     launch_sym_reduce_ranks(sp, ctx->rank, ctx->world, ctx->blk, ctx->p_full, pq_part(ctx),
                             pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s);
-    MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
     mark_end(ctx, marks, e0, it);
+    c0 = mark_begin(ctx, marks);
+    MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
+    mark_end(ctx, marks, c0, it, 2);
     launch_update_xr_shares(ctx->x, ctx->r, p_loc, sp.yr, sp.yr + ctx->blk, ctx->world, ctx->nrows,
                             ctx->sigma_K, ctx->lam, lowrank ? ctx->tpart_base : rr_part(ctx),
                             ctx->st, status, s);
   } else {
     MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx)));
     mark_end(ctx, marks, e0, it);
+    c0 = mark_begin(ctx, marks);
     MLFF_TRY(allreduce(ctx, pq_part(ctx), kVecGrid));
+    mark_end(ctx, marks, c0, it, 2);
     launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx),
                      lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
   }
   if (lowrank) {
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    c0 = mark_begin(ctx, marks);
     MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
+    mark_end(ctx, marks, c0, it, 2);
     ctx->spec_t = true;
   } else {
+    c0 = mark_begin(ctx, marks);
     MLFF_TRY(allreduce(ctx, rrp, kVecGrid));
+    mark_end(ctx, marks, c0, it, 2);
   }
   if (stop_out) launch_stoptest(rrp, ctx->st, ctx->trace, it, s);
   return MLFF_OK;
@@ -1510,9 +1520,12 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
           if (mk.kind == 0) {
             ctx->timing.gemv_ms += ms;
             ctx->timing.gemv_count += 1;
-          } else {
+          } else if (mk.kind == 1) {
             ctx->timing.pre_ms += ms;
             ctx->timing.pre_count += 1;
+          } else {
+            ctx->timing.comm_ms += ms;
+            ctx->timing.comm_count += 1;
           }
         }
       }
@@ -1605,6 +1618,26 @@ int mlff_timing_read_precon(mlff_ctx *ctx, double *ms, int64_t *count) {
   MLFF_API_END(ctx)
 }
 
+int mlff_timing_read_comm(mlff_ctx *ctx, double *ms, int64_t *count) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (ms) *ms = ctx->timing.comm_ms;
+  if (count) *count = ctx->timing.comm_count;
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
+int mlff_device_memory(mlff_ctx *ctx, int64_t *free_out, int64_t *total_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  size_t fr = 0, tot = 0;
+  MLFF_HIP(ctx, hipMemGetInfo(&fr, &tot));
+  if (free_out) *free_out = (int64_t)fr;
+  if (total_out) *total_out = (int64_t)tot;
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
 int mlff_timing_reset(mlff_ctx *ctx) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
@@ -1614,6 +1647,8 @@ int mlff_timing_reset(mlff_ctx *ctx) {
   ctx->timing.pre_count = 0;
   ctx->timing.iter_ms = 0.0;
   ctx->timing.iter_count = 0;
+  ctx->timing.comm_ms = 0.0;
+  ctx->timing.comm_count = 0;
   return MLFF_OK;
   MLFF_API_END(ctx)
 }

@@ -139,6 +139,8 @@ struct Timing {
   int64_t pre_count = 0;
   double iter_ms = 0.0;
   int64_t iter_count = 0;
+  double comm_ms = 0.0;    // collectives of the sharded iteration (one rank's stream)
+  int64_t comm_count = 0;
 };
 
 

@@ -85,6 +85,8 @@ SIGNATURES = {
     "mlff_timing_read": (_int, [_c_ctx, _p_dbl, _p_i64, _p_dbl, _p_i64]),
     "mlff_timing_reset": (_int, [_c_ctx]),
     "mlff_timing_read_precon": (_int, [_c_ctx, _p_dbl, _p_i64]),
+    "mlff_timing_read_comm": (_int, [_c_ctx, _p_dbl, _p_i64]),
+    "mlff_device_memory": (_int, [_c_ctx, _p_i64, _p_i64]),
 }
 
 _lib = None

@@ -334,8 +334,17 @@ class KernelSolver:
                    ctypes.byref(ic))
         pm, pc = ctypes.c_double(), ctypes.c_int64()
         self._call("mlff_timing_read_precon", ctypes.byref(pm), ctypes.byref(pc))
+        cm, cc = ctypes.c_double(), ctypes.c_int64()
+        self._call("mlff_timing_read_comm", ctypes.byref(cm), ctypes.byref(cc))
         return {"gemv_ms": gm.value, "gemv_count": gc.value, "iter_ms": im.value,
-                "iter_count": ic.value, "precon_ms": pm.value, "precon_count": pc.value}
+                "iter_count": ic.value, "precon_ms": pm.value, "precon_count": pc.value,
+                "comm_ms": cm.value, "comm_count": cc.value}
+
+    def device_memory(self) -> tuple[int, int]:
+        """(free, total) bytes of this context's device."""
+        fr, tot = ctypes.c_int64(), ctypes.c_int64()
+        self._call("mlff_device_memory", ctypes.byref(fr), ctypes.byref(tot))
+        return fr.value, tot.value
 
 
 def sgdml_descriptors(R: np.ndarray) -> tuple[np.ndarray, np.ndarray]:

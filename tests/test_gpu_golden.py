@@ -144,7 +144,7 @@ def test_dropin_solve_nanotube(sg, nanotube, precon):
     if precon == "cholesky":
         assert np.array_equal(info["index_columns"], f["cholesky__index_columns"])
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
-                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], case=f"{NANOTUBE}/{precon}")
 
 
 PRECONS = ["cholesky", "random_scores", "lev_scores", "inverse_lev", "lev_random",
@@ -165,7 +165,7 @@ def test_dropin_solve_n270(sg, golden_dir, precon):
         assert np.array_equal(info["index_columns"], f["cholesky__index_columns"])
         assert info["L.shape"] == (f["y"].size, int(f["k_rot"]))
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
-                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], case=f"{name}/{precon}")
     assert resid <= float(f["solver_tol"]) * np.linalg.norm(f["y"])
     assert abs(rmse - resid / np.sqrt(f["y"].size)) == 0
 
@@ -204,7 +204,7 @@ def test_dropin_solve_larger(sg, golden_dir, name, precon):
     assert is_conv
     assert np.array_equal(idxs, f[f"{precon}__inducing_pts_idxs"])
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
-                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], case=f"{name}/{precon}")
 
 
 def test_dropin_unpreconditioned_maxiter(sg, golden_dir):
@@ -226,7 +226,7 @@ def test_dropin_solve_perm_group(sg, golden_dir, precon):
     assert is_conv
     assert np.array_equal(idxs, f[f"{precon}__inducing_pts_idxs"])
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
-                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], case=f"{name}/{precon}")
 
 
 def test_error_semantics(sg):

@@ -54,7 +54,7 @@ def test_sharded_dropin_vs_reference(sg, golden_dir, name, precon, world):
     if precon == "cholesky":
         assert np.array_equal(info["index_columns"], f["cholesky__index_columns"])
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas, int(f[f"{precon}__num_iters"]),
-                      f[f"{precon}__trace"], f[f"{precon}__alphas"], mode="chaotic")
+                      f[f"{precon}__trace"], f[f"{precon}__alphas"], case=f"{name}/{precon}")
 
 
 @pytest.mark.timeout(300)
@@ -68,7 +68,7 @@ def test_sharded_dropin_eigen(sg, golden_dir):
     assert is_conv
     assert_pcg_parity(num_iters, info["resid_trace"][1:], alphas,
                       int(f["eigvec_precon__num_iters"]), f["eigvec_precon__trace"],
-                      f["eigvec_precon__alphas"], mode="chaotic")
+                      f["eigvec_precon__alphas"], case=f"{name}/eigvec_precon")
 
 
 @pytest.mark.timeout(300)
