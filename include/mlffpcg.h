@@ -197,6 +197,11 @@ int mlff_precon_none(mlff_ctx *ctx);
  * reference's L), readable with mlff_precon_get_panel, and PCG runs unpreconditioned. */
 int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *index_columns_out,
                         double *seconds_out);
+/* per-column device seconds of the last pivoted-Cholesky build (time_cholesky of
+ * incomplete_cholesky.py:48-80: event stamps every 4 columns, split evenly) and the
+ * seconds of its Woodbury build */
+int mlff_pivchol_times(mlff_ctx *ctx, double *col_seconds_out, int64_t k,
+                       double *woodbury_seconds_out);
 /* Nystrom from sorted column indices idx (k).  variant 0 = _init_precon_operator
  * (eig-sign diagonal shift, apply (B^T B r - r)/lam), variant 1 = _sb (1e-16
  * shift, apply -(r - P^T P r)/lam). */

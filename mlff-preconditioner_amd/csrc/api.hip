@@ -1249,14 +1249,30 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
   MLFF_HIP(ctx, hipMalloc(&ctx->prow, sizeof(double) * (k + 1)));
   MLFF_TRY(pivoted_cholesky(ctx, k, index_columns_out));
   ctx->k = k;  // without Woodbury the panel holds L^T (mlff_precon_get_panel), unused by PCG
+  ctx->piv_woodbury_s = 0.0;
   if (build_woodbury) {
+    const auto tw = std::chrono::steady_clock::now();
     MLFF_TRY(woodbury_inplace(ctx, ctx->T, k));
+    ctx->piv_woodbury_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     ctx->precon_kind = MLFF_PRECON_PIVCHOL;
     ctx->sigma_p = 1.0;
   }
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (seconds_out)
     *seconds_out = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
+int mlff_pivchol_times(mlff_ctx *ctx, double *col_seconds_out, int64_t k,
+                       double *woodbury_seconds_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (k < 0 || (k > 0 && col_seconds_out == nullptr)) return set_error(ctx, MLFF_ERR_ARG, "bad output");
+  const int64_t n = std::min<int64_t>(k, (int64_t)ctx->piv_col_s.size());
+  for (int64_t c = 0; c < n; ++c) col_seconds_out[c] = ctx->piv_col_s[c];
+  for (int64_t c = n; c < k; ++c) col_seconds_out[c] = 0.0;
+  if (woodbury_seconds_out) *woodbury_seconds_out = ctx->piv_woodbury_s;
   return MLFF_OK;
   MLFF_API_END(ctx)
 }

@@ -225,6 +225,8 @@ struct mlff_ctx {
   double *dwork = nullptr;   // residual diagonal (local)
   int *pivflag = nullptr;    // local rows already pivoted
   double *prow = nullptr;    // L[m_pi, :m]
+  std::vector<double> piv_col_s;  // device seconds per column of the last build
+  double piv_woodbury_s = 0.0;    // its Woodbury build (G, chol, T)
 
   mlff::Timing timing;
   std::string err;

@@ -309,7 +309,22 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
+  // per-column build times (incomplete_cholesky.py:48-80 records time_cholesky[m] for every
+  // column; tools/create_data.py:117-148 compares the first 20 with the rest): a device
+  // event every kStampEvery columns, the segment's time split evenly over its columns
+  constexpr int64_t kStampEvery = 4;
+  std::vector<hipEvent_t> stamps;
+  stamps.reserve((size_t)(k / kStampEvery + 2));
+  auto stamp = [&]() {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) == hipSuccess) {
+      hipEventRecord(e, s);
+      stamps.push_back(e);
+    }
+  };
+  stamp();
   for (int64_t m = 0; m < k; ++m) {
+    if (m > 0 && m % kStampEvery == 0) stamp();
     // candidates of step m: a scan of the positions [m, N) at m = 0 (and on a rank without
     // rows), afterwards the per-workgroup winners k_piv_fin left from step m - 1
     int npc = (int)gcol;
@@ -354,6 +369,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                          ctx->st, 0.0);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
   }
+  stamp();
   MLFF_HIP(ctx, hipGetLastError());
   int perr = 0;
   MLFF_HIP(ctx, hipMemcpyAsync(&perr, &ctx->st->pivot_err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -361,6 +377,16 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     MLFF_HIP(ctx, hipMemcpyAsync(index_columns_out, ctx->perm, sizeof(int64_t) * N,
                                  hipMemcpyDeviceToHost, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
+  ctx->piv_col_s.assign((size_t)k, 0.0);
+  if (stamps.size() == (size_t)((k + kStampEvery - 1) / kStampEvery + 1)) {
+    for (size_t g = 0; g + 1 < stamps.size(); ++g) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, stamps[g], stamps[g + 1]);
+      const int64_t c0 = (int64_t)g * kStampEvery, c1 = std::min<int64_t>(c0 + kStampEvery, k);
+      for (int64_t c = c0; c < c1; ++c) ctx->piv_col_s[c] = 1e-3 * ms / (double)(c1 - c0);
+    }
+  }
+  for (hipEvent_t e : stamps) (void)hipEventDestroy(e);
   if (perr)
     return set_error(ctx, MLFF_ERR_NOT_PSD,
                      "given matrix is not PSD (pivot <= 0 in pivoted Cholesky)");

@@ -70,6 +70,7 @@ SIGNATURES = {
     "mlff_precon_none": (_int, [_c_ctx]),
     "mlff_precon_pivchol": (_int, [_c_ctx, _i64, _int, _p_i64, _p_dbl]),
     "mlff_precon_nystrom": (_int, [_c_ctx, _p_i64, _i64, _int, _p_dbl]),
+    "mlff_pivchol_times": (_int, [_c_ctx, _p_dbl, _i64, _p_dbl]),
     "mlff_precon_lowrank": (_int, [_c_ctx, _p_dbl, _i64]),
     "mlff_precon_eig": (_int, [_c_ctx, _i64, _int, _i64, _int, _p_dbl, _p_dbl]),
     "mlff_precon_info": (_int, [_c_ctx, _p_int, _p_i64]),

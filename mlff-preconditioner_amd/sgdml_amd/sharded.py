@@ -164,6 +164,11 @@ class ShardedKernelSolver:
         out = self._each("precon_pivchol", k, build_woodbury)
         return out[0]  # index_columns are replicated on every rank
 
+    def pivchol_times(self, k):
+        """per-column times of the slowest rank (the build is collective per column)"""
+        out = self._each("pivchol_times", k)
+        return np.max(np.stack([t for t, _ in out]), axis=0), max(w for _, w in out)
+
     def precon_nystrom(self, idx, variant=0):
         return max(self._each("precon_nystrom", idx, variant))
 

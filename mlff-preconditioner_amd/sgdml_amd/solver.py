@@ -208,6 +208,14 @@ class KernelSolver:
                    ctypes.byref(sec))
         return idx, sec.value
 
+    def pivchol_times(self, k: int) -> tuple[np.ndarray, float]:
+        """(device seconds of every column of the last pivoted-Cholesky build, seconds of its
+        Woodbury build): the reference's info['time_cholesky'] (incomplete_cholesky.py:48-80)."""
+        t = np.empty(int(k))
+        w = ctypes.c_double()
+        self._call("mlff_pivchol_times", nat.dptr(t), int(k), ctypes.byref(w))
+        return t, w.value
+
     def precon_nystrom(self, idx: np.ndarray, variant: int = 0) -> float:
         idx = np.ascontiguousarray(idx, dtype=np.int64)
         sec = ctypes.c_double()

@@ -190,9 +190,11 @@ class Iterative(object):
             solver.precon_nystrom(np.asarray(inducing_pts_idxs, dtype=np.int64), variant=variant)
         elif str_preconditioner == "cholesky":
             k = int(break_percentage * n)
-            t0 = timeit.default_timer()
             index_columns, sec = solver.precon_pivchol(k, build_woodbury=True)
-            info_cholesky = {"time_cholesky": np.full(k, (timeit.default_timer() - t0) / max(k, 1)),
+            # per-column device times of the build (incomplete_cholesky.py:48-80), the
+            # Woodbury build (iterative_cholesky.py:141-143) reported on its own
+            t_cols, t_woodbury = solver.pivchol_times(k)
+            info_cholesky = {"time_cholesky": t_cols, "time_woodbury": t_woodbury,
                              "L.shape": (n, k), "index_columns": index_columns}
             inducing_pts_idxs = np.arange(int(break_percentage * n))
         elif str_preconditioner in EIGVEC_KEYS:
@@ -211,6 +213,7 @@ class Iterative(object):
         maxiter = 3 * n_atoms * n_train * 5
         progress = _Checkpointer(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std,
                                  inducing_pts_idxs, num_iters0, save_progr_callback)
+        op_storage, op_bytes = solver.storage_info()
         solver.timing(True)
         solver.timing_reset()
         tic = timeit.default_timer()
@@ -232,8 +235,11 @@ class Iterative(object):
                 # additions of this backend
                 "resid_trace": res.trace,
                 "cg_iterations": res.iters,
-                "gbps_matvec": (8.0 * n * n + 16.0 * n) / (t["gemv_ms"] / t["gemv_count"]) / 1e6
+                # algorithmic bytes of the operator in the storage it ran on (matrix-free:
+                # the descriptor tables; tiles: 4 N^2) over its mean HIP-event time
+                "gbps_matvec": op_bytes / (t["gemv_ms"] / t["gemv_count"]) / 1e6
                 if t["gemv_count"] else float("nan"),
+                "operator_storage": op_storage,
                 "n_gpus": getattr(solver, "world", 1)}
         if info_cholesky is not None:
             info.update(info_cholesky)
