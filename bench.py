@@ -448,6 +448,10 @@ def main():
                           "matfree": "k_mf_pair (+Zt) + k_mf_pair_fin + k_mf_h + k_mf_jt + k_mf_jt_fin "
                                      "(matrix-free sGDML operator)"}.get(storage, storage),
                "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
+    if storage == "matfree":
+        roof_op["note"] = ("five dependent launches of ~5-13 us each over 5-22 MB: neither "
+                           "HBM- nor FP64-bound (PMC traffic and L2 hit rates in "
+                           "profiles/pmc_traffic.json; DESIGN.md 'matrix-free operator')")
     # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials
     roof_pre = None
     if tm.get("precon_count"):
