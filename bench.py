@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--k", type=int, default=None,
                     help="preconditioner rank (rbf: 256; sGDML: the rule of thumb, e.g. 2701 "
                          "for the nanotube; configs[4] uses 1024)")
+    ap.add_argument("--strong-n", type=int, default=65536,
+                    help="with several GPUs and the rbf workload, also time this size (the "
+                         "one-GPU configs[2] size) for a like-for-like strong-scaling number; "
+                         "0 skips it")
     ap.add_argument("--lam", type=float, default=1e-6)
     ap.add_argument("--ell", type=float, default=0.2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -329,6 +333,43 @@ def sgdml_workload(args, rank, world, local, pg):
                              "perms": np.arange(n_atoms)[None, :]}
 
 
+def strong_leg(args, rank, world, local, pg, n, k, lam, ell):
+    """Iterations/s of the rbf workload at size n on all ranks (same generator, Nystrom rank,
+    storage and timing as the main leg): with n = 65536 the same problem as the one-GPU
+    line, so value_N / value_1 is a strong-scaling ratio even though the multi-GPU `value`
+    is quoted on configs[3] (N = 131072)."""
+    from sgdml_amd import synthetic
+
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    s = make_solver(n, rank, world, local, pg)
+    try:
+        s.gen_rbf(X, ell)
+        s.set_operator(1.0, lam)
+        s.precon_nystrom(idx, variant=0)
+        s.set_storage(args.storage)
+        _, op_bytes = s.storage_info()
+        r0, r1 = s.row_range()
+        s.pcg_start(np.ascontiguousarray(b[r0:r1]), tol=0.0,
+                    maxiter=args.warmup + args.steps + 1)
+        if args.warmup:
+            s.pcg_run(args.warmup, args.warmup)
+        s.timing(True)
+        s.timing_reset()
+        barrier(pg, s)
+        t0 = time.perf_counter()
+        s.pcg_run(args.steps, args.steps)
+        barrier(pg, s)
+        el = max_over_ranks(pg, time.perf_counter() - t0)
+        tm = s.timing_read()
+        op_ms = max_over_ranks(pg, tm["gemv_ms"] / max(tm["gemv_count"], 1))
+        return {"n": n, "k": k, "value": args.steps / el, "ms_per_step": el / args.steps * 1e3,
+                "operator_ms_max_rank": op_ms,
+                "rccl_ms_per_iter": max_over_ranks(pg, tm["comm_ms"] / max(tm["iter_count"], 1))}
+    finally:
+        s.close()
+
+
 def solo_profile(args):
     """One rank of a --solo-world W row split on one GPU with the library's SOLO transport
     (every collective keeps only this rank's contribution): the kernels, sizes and launch
@@ -538,8 +579,18 @@ def main():
                             {"descriptors_and_operator": t_gen, "pivoted_cholesky_build": t_pre},
                             storage_pack=t_pack),
         }
-        print(json.dumps(out), flush=True)
     solver.close()
+    if world > 1 and args.workload == "rbf" and args.strong_n and args.strong_n != n:
+        try:
+            strong = strong_leg(args, rank, world, local, pg, args.strong_n, k, lam, ell)
+        except Exception as e:  # the configs[3] line above must still be printed
+            strong = {"n": args.strong_n, "value": None, "error": repr(e)}
+        if out is not None:
+            out["strong_scaling_leg"] = dict(strong, baseline_config="configs[2]", note=(
+                "the one-GPU line's problem on all ranks: compare its value with BENCH at "
+                "N=1 for strong scaling; `value` above is configs[3] (N=131072)"))
+    if out is not None:
+        print(json.dumps(out), flush=True)
     if pg is not None:
         pg.barrier()
         pg.destroy_process_group()
