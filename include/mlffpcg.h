@@ -151,6 +151,17 @@ int mlff_assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
  * permutation sets it is the reference's K_op. */
 int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M,
                         int n_atoms, const int32_t *perms, int n_perms, double sig);
+
+/* Energy constraints (use_E_cstr), set BEFORE mlff_assemble_sgdml / mlff_sgdml_operator:
+ * the system gets M energy rows / columns after the 3 n_atoms M force rows (the context's
+ * N must be 3 n_atoms M + M).  The assembly appends the reference's K_fe / K_ee border
+ * (train.py:212-236, _assemble_kernel_mat(use_E_cstr=True)); the matrix-free operator is
+ * the reference's _K_vec with energy coefficients (iterative_solver.py:416-443: x = [x_F;
+ * x_E], forces from GDMLPredict with alphas_E, predict.py:206-218, and the predicted
+ * energies with a flipped sign); the diagonal includes K[E_i, E_i].  One rank only
+ * (MLFF_ERR_ARG otherwise).  Replaces: the use_E_cstr argument of the reference's
+ * assembly and operator (its Iterative.solve itself cannot run with it). */
+int mlff_set_energy_constraints(mlff_ctx *ctx, int use_E_cstr);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out);
 

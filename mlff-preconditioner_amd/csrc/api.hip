@@ -1123,6 +1123,16 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_API_END(ctx)
 }
 
+int mlff_set_energy_constraints(mlff_ctx *ctx, int use_E_cstr) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (use_E_cstr && ctx->world > 1)
+    return set_error(ctx, MLFF_ERR_ARG, "use_E_cstr: energy constraints run on one rank");
+  ctx->use_E_cstr = use_E_cstr != 0;
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out) {
   MLFF_API_BEGIN

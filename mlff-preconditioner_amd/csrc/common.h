@@ -92,6 +92,12 @@ struct MfData {
   // whole operator)
   double *uvk = nullptr;
   int32_t *pi_d = nullptr, *piinv_d = nullptr;
+  // energy constraints (use_E_cstr, train.py:212-236; iterative_solver.py:423-440): the
+  // operand and result carry M energy entries after the nF = 3 n M force entries (one rank)
+  bool E = false;
+  int64_t nF = 0;
+  double *kee = nullptr;    // ni x M: sum_p (1 + nrm/sig (1 + nrm/(3 sig))) exp(-nrm/sig)
+  double *eterm = nullptr;  // ni x (M n_perms): a_ijp w_ijp of the last application
 };
 
 // Synthetic RBF kernel source (tools/utils.py:173-187): the points, scaled by 1 / length
@@ -186,7 +192,8 @@ struct mlff_ctx {
   bool has_matrix = false;
   double sigma_K = 1.0, lam = 0.0;
   bool has_operator = false;
-  bool K_symmetric = false;  // known symmetric by construction (generated / assembled)
+  bool K_symmetric = false;
+  bool use_E_cstr = false;   // mlff_set_energy_constraints: sGDML systems of size 3 n M + M  // known symmetric by construction (generated / assembled)
   int storage = MLFF_STORAGE_AUTO;  // requested operator storage
   bool use_sym = false;             // resolved: symmetric tiles in use
   bool use_mf = false;              // resolved: matrix-free sGDML operator in use
@@ -423,6 +430,9 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
                    int n_atoms, const int32_t *perms, int n_perms, double sig);
 int sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc,
                       double *R_d_desc);
+// kee[il * M + j] = sum_p Kee(sqrt5 |Rd_{i0+il} - Rd_j[P_p]|) (use_E_cstr, train.py:232-234)
+void launch_sgdml_kee(const double *Rd, int64_t M, int64_t D, int64_t i0, int64_t ni,
+                      const int32_t *Pt, int n_perms, double sig, double *kee, hipStream_t s);
 // (r = i, s = j) point-pair records of the local points [i0, i0 + ni) (k_sgdml_uv, no mirror)
 void launch_sgdml_records(const double *Rd, const double *Rdd, int64_t M, int n, int64_t D,
                           int64_t i0, int64_t ni, const int32_t *Pt, const int32_t *piinv,

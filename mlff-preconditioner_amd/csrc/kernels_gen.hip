@@ -397,6 +397,66 @@ __global__ __launch_bounds__(256) void k_sgdml_block(double *__restrict__ K, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// Energy constraints (use_E_cstr).  The reference appends M energy rows / columns to K
+// (train.py:212-236) and its K_op predicts energies with energy coefficients
+// (iterative_solver.py:423-440, predict.py:206-218):
+//   K[E_i, E_j] = -sum_p Kee(nrm_ijp),  Kee(r) = (1 + r/sig (1 + r/(3 sig))) exp(-r/sig),
+//   nrm_ijp = sqrt5 |Rd_i - Rd_j[P_p]|.
+// kee[il * M + j] = sum_p Kee(nrm_ijp) for i = i0 + il (p summed in order)
+__global__ __launch_bounds__(256) void k_sgdml_kee(const double *__restrict__ Rd, int64_t M,
+                                                   int64_t D, int64_t i0,
+                                                   const int32_t *__restrict__ Pt, int n_perms,
+                                                   double sig, double *__restrict__ kee) {
+  const int64_t j = blockIdx.x, il = blockIdx.y;
+  const double *ri = Rd + (i0 + il) * D;
+  const double *rj = Rd + j * D;
+  __shared__ double sh[4];
+  double total = 0.0;
+  for (int p = 0; p < n_perms; ++p) {
+    const int32_t *P = Pt + (int64_t)p * D;
+    double acc = 0.0;
+    for (int64_t d = threadIdx.x; d < D; d += 256) {
+      const double df = ri[d] - rj[P[d]];
+      acc = fma(df, df, acc);
+    }
+    acc = wave_sum(acc);
+    __syncthreads();  // sh is reused per permutation
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const double nrm = sqrt(5.0) * sqrt((sh[0] + sh[1]) + (sh[2] + sh[3]));
+    total += (1.0 + (nrm / sig) * (1.0 + nrm / (3.0 * sig))) * exp(-nrm / sig);
+  }
+  if (threadIdx.x == 0) kee[il * M + j] = total;
+}
+
+// Border of the assembled K for the energy constraints (one rank), from the (r = i, s = j)
+// point-pair records of every pair (k_sgdml_uv, mirror = 0) and kee:
+//   K[j 3n + t, nF + i] = K[nF + i, j 3n + t] = -sum_p w_p v_p[t]   (train.py:221-230:
+//     K_fe = -sum_{p,d} w_p diff_p[d] J_j[P_p d, t] with diff_p = Rd_i - Rd_j[P_p])
+//   K[nF + i, nF + j] = -kee[min(i,j), max(i,j)]   (train.py:232-234; column worker
+//     max(i, j) writes the pair last)
+__global__ __launch_bounds__(256) void k_sgdml_eborder(double *__restrict__ K, int64_t ld,
+                                                       const double *__restrict__ uv0,
+                                                       const double *__restrict__ kee, int64_t M,
+                                                       int n, int n_perms, int64_t nF) {
+  const int64_t j = blockIdx.x, i = blockIdx.y;
+  const int n3 = 3 * n;
+  const int64_t rs = 6 * n + 2;
+  const double *rec = uv0 + (i * M + j) * n_perms * rs;
+  for (int t = threadIdx.x; t < n3; t += 256) {
+    double acc = 0.0;
+    for (int p = 0; p < n_perms; ++p) acc = fma(rec[p * rs + 6 * n + 1], rec[p * rs + n3 + t], acc);
+    const int64_t g = j * n3 + t;
+    K[g * ld + nF + i] = -acc;
+    K[(nF + i) * ld + g] = -acc;
+  }
+  if (threadIdx.x == 0) {
+    const int64_t a = i < j ? i : j, b = i < j ? j : i;
+    K[(nF + i) * ld + nF + j] = -kee[a * M + b];
+  }
+}
+
 // descriptor permutations P_p[pair(a,b)] = pair(pi a, pi b) (Desc.perm, desc.py:360-389)
 // and inverse atom maps; validates that every row of perms is a permutation
 int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,
@@ -429,14 +489,19 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
   const int64_t D = (int64_t)n * (n - 1) / 2;
   const int64_t n3 = 3 * n;
   if (n < 2 || M < 1 || n_perms < 1) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: bad sizes");
-  if (n3 * M != ctx->N)
-    return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: N != 3 * n_atoms * M");
+  const bool E = ctx->use_E_cstr;
+  const int64_t nF = n3 * M;
+  if (nF + (E ? M : 0) != ctx->N)
+    return set_error(ctx, MLFF_ERR_ARG, E ? "assemble_sgdml: N != 3 * n_atoms * M + M (use_E_cstr)"
+                                          : "assemble_sgdml: N != 3 * n_atoms * M");
+  if (E && ctx->world > 1)
+    return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: use_E_cstr runs on one rank");
   if (n_perms > 1024) return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: too many permutations");
   std::vector<int32_t> Pt, piinv;
   MLFF_TRY(desc_perm_tables(ctx, perms, n, n_perms, Pt, piinv));
   // training points whose rows intersect this rank
-  const int64_t i0 = ctx->row0 / n3;
-  const int64_t i1 = (ctx->row0 + ctx->nrows + n3 - 1) / n3;  // exclusive
+  const int64_t i0 = std::min<int64_t>(ctx->row0 / n3, M);
+  const int64_t i1 = std::min<int64_t>((ctx->row0 + ctx->nrows + n3 - 1) / n3, M);  // exclusive
   const int64_t mi = i1 - i0;
   double *dRd = nullptr, *dRdd = nullptr, *uv = nullptr;
   int32_t *dP = nullptr, *dpi = nullptr, *dpiinv = nullptr;
@@ -455,12 +520,28 @@ int assemble_sgdml(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, 
   MLFF_HIP(ctx, hipMemcpyAsync(dpi, perms, sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemcpyAsync(dpiinv, piinv.data(), sizeof(int32_t) * n_perms * n, hipMemcpyHostToDevice, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->K, 0, sizeof(double) * ctx->blk * ctx->ld, s));
-  hipLaunchKernelGGL(k_sgdml_uv, dim3((unsigned)M, (unsigned)mi, (unsigned)n_perms), dim3(256), 0,
-                     s, dRd, dRdd, M, n, D, i0, dP, dpiinv, sig, uv, 0);
-  hipLaunchKernelGGL(k_sgdml_block, dim3((unsigned)n, (unsigned)mi, (unsigned)M), dim3(256),
-                     sizeof(double) * 9 * n_perms, s, ctx->K, ctx->ld, ctx->row0, ctx->nrows,
-                     ctx->rows_per, ctx->blk, dRdd, M, n, D, i0, dpi, dpiinv, n_perms, uv, 0,
-                     (double *)nullptr);
+  if (mi > 0) {
+    hipLaunchKernelGGL(k_sgdml_uv, dim3((unsigned)M, (unsigned)mi, (unsigned)n_perms), dim3(256), 0,
+                       s, dRd, dRdd, M, n, D, i0, dP, dpiinv, sig, uv, 0);
+    hipLaunchKernelGGL(k_sgdml_block, dim3((unsigned)n, (unsigned)mi, (unsigned)M), dim3(256),
+                       sizeof(double) * 9 * n_perms, s, ctx->K, ctx->ld, ctx->row0, ctx->nrows,
+                       ctx->rows_per, ctx->blk, dRdd, M, n, D, i0, dpi, dpiinv, n_perms, uv, 0,
+                       (double *)nullptr);
+  }
+  if (E) {  // one rank: rows and columns are global indices
+    const double rec_bytes = 8.0 * (double)M * (double)M * n_perms * (double)rec;
+    if (rec_bytes > 4.0e9)
+      return set_error(ctx, MLFF_ERR_ARG, "assemble_sgdml: use_E_cstr pair records exceed 4 GB");
+    double *uv0 = nullptr, *kee = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &uv0, M * M * n_perms * rec));
+    MLFF_TRY(scratch_alloc(ctx, &kee, M * M));
+    hipLaunchKernelGGL(k_sgdml_uv, dim3((unsigned)M, (unsigned)M, (unsigned)n_perms), dim3(256), 0,
+                       s, dRd, dRdd, M, n, D, (int64_t)0, dP, dpiinv, sig, uv0, 0, 0);
+    hipLaunchKernelGGL(k_sgdml_kee, dim3((unsigned)M, (unsigned)M), dim3(256), 0, s, dRd, M, D,
+                       (int64_t)0, dP, n_perms, sig, kee);
+    hipLaunchKernelGGL(k_sgdml_eborder, dim3((unsigned)M, (unsigned)M), dim3(256), 0, s, ctx->K,
+                       ctx->ld, uv0, kee, M, n, n_perms, nF);
+  }
   MLFF_HIP(ctx, hipGetLastError());
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
@@ -473,9 +554,11 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
                const int32_t *dP, const int32_t *perms_host, const int32_t *piinv_host,
                int n_perms, double sig, double *diag_out) {
   const int64_t D = (int64_t)n * (n - 1) / 2, n3 = 3 * (int64_t)n;
-  if (ctx->nrows == 0) return MLFF_OK;
+  // force rows only (the energy rows of use_E_cstr follow them; mf_diag fills those)
+  const int64_t nrows = std::max<int64_t>(0, std::min<int64_t>(ctx->nrows, n3 * M - ctx->row0));
+  if (nrows == 0) return MLFF_OK;
   const int64_t i0 = ctx->row0 / n3;
-  const int64_t mi = (ctx->row0 + ctx->nrows + n3 - 1) / n3 - i0;
+  const int64_t mi = (ctx->row0 + nrows + n3 - 1) / n3 - i0;
   hipStream_t s = ctx->stream;
   double *uv = nullptr;
   int32_t *dpi = nullptr, *dpiinv = nullptr;
@@ -490,10 +573,9 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
                      (int64_t)1, n, D, i0, dP, dpiinv, sig, uv, 1);
   hipLaunchKernelGGL(k_sgdml_block, dim3((unsigned)n, (unsigned)mi, 1), dim3(256),
                      sizeof(double) * 9 * n_perms, s, (double *)nullptr, ctx->ld, ctx->row0,
-                     ctx->nrows, ctx->rows_per, ctx->blk, dRdd, (int64_t)1, n, D, i0, dpi, dpiinv,
+                     nrows, ctx->rows_per, ctx->blk, dRdd, (int64_t)1, n, D, i0, dpi, dpiinv,
                      n_perms, uv, 1, diag_out);
   MLFF_HIP(ctx, hipGetLastError());
-  (void)M;
   return MLFF_OK;
 }
 
@@ -579,6 +661,13 @@ __global__ __launch_bounds__(64) void k_sgdml_col(const double *__restrict__ Rdd
     }
   }
   if (act) out[(int64_t)blockIdx.y * ldo + r] = sigma * acc;
+}
+
+void launch_sgdml_kee(const double *Rd, int64_t M, int64_t D, int64_t i0, int64_t ni,
+                      const int32_t *Pt, int n_perms, double sig, double *kee, hipStream_t s) {
+  if (ni <= 0) return;
+  hipLaunchKernelGGL(k_sgdml_kee, dim3((unsigned)M, (unsigned)ni), dim3(256), 0, s, Rd, M, D, i0, Pt,
+                     n_perms, sig, kee);
 }
 
 void launch_sgdml_records(const double *Rd, const double *Rdd, int64_t M, int n, int64_t D,

@@ -202,13 +202,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8))) voi
 
 // MODE 0: m5 = 5 m, w from the squared norms; MODE 1: c = m5 * dot; MODE 2 (energies):
 // w * dot.  One wave per output: lanes stride over the nz slices, fixed-order wave sum.
+// Energy constraints (MODE 1, xE != nullptr): c += x_E[j] w (the energy coefficients' force
+// term, predict.py:210-213) and eterm = dot * w (their energy term, predict.py:207).
+struct EPair {
+  const double *xE = nullptr;  // energy entries of the operand (M)
+  const double *w = nullptr;   // ni x MP
+  double *eterm = nullptr;     // ni x MP
+  int64_t MP = 1;
+  int n_perms = 1;
+};
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ part, int nz,
                                                      int64_t nout, double sig,
                                                      const double *__restrict__ m5,
                                                      double *__restrict__ out0,
                                                      double *__restrict__ out1,
-                                                     const int *__restrict__ status) {
+                                                     const int *__restrict__ status,
+                                                     EPair ep = {}) {
   if (MODE >= 1 && status != nullptr && *status != ST_RUNNING) return;
   const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -232,6 +242,10 @@ __global__ __launch_bounds__(256) void k_mf_pair_fin(const double *__restrict__ 
     const double m = exp(-norm / sig) * 5.0 / (3.0 * sig * sig * sig * sig);
     out0[o] = 5.0 * m;
     out1[o] = (sig * sig + sig * norm) * m;
+  } else if (MODE == 1 && ep.xE != nullptr) {
+    const int64_t j = (o % ep.MP) / ep.n_perms;
+    out0[o] = fma(ep.xE[j], ep.w[o], m5[o] * s);
+    ep.eterm[o] = s * ep.w[o];
   } else {
     out0[o] = m5[o] * s;  // MODE 2: m5 holds w
   }
@@ -432,6 +446,13 @@ __global__ __launch_bounds__(256) void k_mf_jt(const double *__restrict__ Rdd,
 // y = sigma * sum_z part[z] + lam * x (fixed slice order).  PQ: also the x . y partials
 // of the CG step, on the kVecGrid grid-stride layout of k_dot_part (same terms, same
 // order: the separate dot launch it replaces gives the same bits)
+// Energy rows (one rank, use_E_cstr): row nF + i = -(sum_jp eterm[i, jp] + sum_j kee[i, j]
+// x_E[j]) (the predicted energy with a flipped sign, iterative_solver.py:439-440).
+struct ERows {
+  int64_t nF = INT64_MAX;  // rows >= nF are energy rows
+  const double *eterm = nullptr, *kee = nullptr, *xE = nullptr;
+  int64_t M = 0, MP = 0;
+};
 template <bool PQ>
 __global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ part, int js,
                                                    int64_t nrows,
@@ -439,14 +460,22 @@ __global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ pa
                                                    const double *__restrict__ xloc,
                                                    double *__restrict__ y,
                                                    double *__restrict__ pq_part,
-                                                   const int *__restrict__ status) {
+                                                   const int *__restrict__ status, ERows er = {}) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[8];
   double acc = 0.0;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < nrows;
        r += (int64_t)gridDim.x * 256) {
     double s = 0.0;
-    for (int z = 0; z < js; ++z) s += part[(int64_t)z * nrows + r];
+    if (r >= er.nF) {
+      const int64_t i = r - er.nF;
+      double e = 0.0;
+      for (int64_t jp = 0; jp < er.MP; ++jp) e += er.eterm[i * er.MP + jp];
+      for (int64_t j = 0; j < er.M; ++j) e = fma(er.kee[i * er.M + j], er.xE[j], e);
+      s = -e;
+    } else {
+      for (int z = 0; z < js; ++z) s += part[(int64_t)z * nrows + r];
+    }
     double yv = sigma * s;
     if (xloc != nullptr) yv += lam * xloc[r];
     y[r] = yv;
@@ -458,6 +487,11 @@ __global__ __launch_bounds__(256) void k_mf_jt_fin(const double *__restrict__ pa
   }
 }
 
+__global__ void k_mf_ediag(const double *__restrict__ kee, int64_t M, double *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < M) out[i] = -kee[i * M + i];
+}
+
 }  // namespace
 
 int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
@@ -467,7 +501,12 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   const int n = n_atoms;
   const int64_t D = (int64_t)n * (n - 1) / 2, n3 = 3 * (int64_t)n;
   if (n < 2 || M < 1 || n_perms < 1) return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: bad sizes");
-  if (n3 * M != ctx->N) return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: N != 3 * n_atoms * M");
+  const bool E = ctx->use_E_cstr;
+  if (n3 * M + (E ? M : 0) != ctx->N)
+    return set_error(ctx, MLFF_ERR_ARG, E ? "sgdml operator: N != 3 * n_atoms * M + M (use_E_cstr)"
+                                          : "sgdml operator: N != 3 * n_atoms * M");
+  if (E && ctx->world > 1)
+    return set_error(ctx, MLFF_ERR_ARG, "sgdml operator: use_E_cstr runs on one rank");
   std::vector<int32_t> Pt, piinv;
   MLFF_TRY(desc_perm_tables(ctx, perms, n, n_perms, Pt, piinv));
   std::vector<int32_t> ps(D), pt(D);
@@ -484,7 +523,9 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   mf.n_perms = n_perms;
   mf.sig = sig;
   mf.i0 = ctx->row0 / n3;
-  mf.ni = ctx->nrows > 0 ? (ctx->row0 + ctx->nrows + n3 - 1) / n3 - mf.i0 : 0;
+  mf.ni = ctx->nrows > 0 ? std::min<int64_t>((ctx->row0 + ctx->nrows + n3 - 1) / n3, M) - mf.i0 : 0;
+  mf.E = E;
+  mf.nF = n3 * M;
   const int64_t MP = M * n_perms;
   const int64_t nic = std::max<int64_t>(mf.ni, 1);
   hipStream_t s = ctx->stream;
@@ -526,7 +567,11 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   // single-column path: the (r = i, s = j) pair records of the local points (3.5 MB for
   // the nanotube, M = 14; ni M n_perms (6 n + 2) doubles in general)
   const double col_bytes = 8.0 * (double)mf.ni * (double)MP * (double)(6 * n + 2);
-  if (mf.ni > 0 && col_bytes <= kMfColTableBytes) {
+  if (E) {  // energy tables; columns go through the whole operator (K_op e_g)
+    MLFF_HIP(ctx, hipMalloc(&mf.kee, sizeof(double) * nic * M));
+    MLFF_HIP(ctx, hipMalloc(&mf.eterm, sizeof(double) * nic * MP));
+    launch_sgdml_kee(mf.Rd, M, D, mf.i0, mf.ni, mf.Pt, n_perms, sig, mf.kee, s);
+  } else if (mf.ni > 0 && col_bytes <= kMfColTableBytes) {
     MLFF_HIP(ctx, hipMalloc(&mf.uvk, (size_t)col_bytes));
     MLFF_HIP(ctx, hipMalloc(&mf.pi_d, sizeof(int32_t) * n_perms * n));
     MLFF_HIP(ctx, hipMalloc(&mf.piinv_d, sizeof(int32_t) * n_perms * n));
@@ -581,8 +626,14 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                      (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
                      mf.Rd, Rt, (const double *)nullptr, mf.D, mf.dslice, mf.i0, mf.ni, MP,
                      mf.part, status, zs);
+  EPair ep;
+  ERows er;
+  if (mf.E) {  // one rank: the operand's energy entries follow its nF force entries
+    ep = EPair{xc + mf.nF, mf.w, mf.eterm, MP, (int)mf.n_perms};
+    er = ERows{mf.nF, mf.eterm, mf.kee, xc + mf.nF, mf.M, MP};
+  }
   hipLaunchKernelGGL(k_mf_pair_fin<1>, dim3((unsigned)((mf.ni * MP + 3) / 4)), dim3(256), 0, s,
-                     mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status);
+                     mf.part, mf.nz, mf.ni * MP, mf.sig, mf.m5, mf.c, (double *)nullptr, status, ep);
   const int64_t dblk = (mf.D + 63) / 64, dblk8 = (dblk + 7) / 8 * 8;
   if (dblk * (int64_t)gi >= 4096) {
     hipLaunchKernelGGL(k_mf_h<kIC>, dim3((unsigned)(dblk8 * gi)), dim3(64), 0, s, mf.Rd, Rt,
@@ -599,12 +650,13 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   }
   if (pq_part != nullptr) {
     hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js, ctx->nrows,
-                       sigma, lam, x_loc, y_loc, pq_part, status);
+                       sigma, lam, x_loc, y_loc, pq_part, status, er);
     return;
   }
   if (ctx->nrows <= 0) return;
   hipLaunchKernelGGL(k_mf_jt_fin<false>, dim3((unsigned)((ctx->nrows + 255) / 256)), dim3(256), 0,
-                     s, mf.ypart, js, ctx->nrows, sigma, lam, x_loc, y_loc, (double *)nullptr, status);
+                     s, mf.ypart, js, ctx->nrows, sigma, lam, x_loc, y_loc, (double *)nullptr, status,
+                     er);
 }
 
 // Training-set energies of the model with coefficients `alphas` (contiguous global
@@ -614,6 +666,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
 // E_pairs (ni x M n_perms, host), summed by the caller in pair order.
 int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host) {
   MfData &mf = ctx->mf;
+  if (mf.E) return set_error(ctx, MLFF_ERR_STATE, "sgdml_energies: not with use_E_cstr");
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
   double *da = nullptr;
@@ -644,6 +697,9 @@ int mf_diag(mlff_ctx *ctx, double *out) {
   MfData &mf = ctx->mf;
   MLFF_TRY(sgdml_diag(ctx, mf.Rd, mf.Rdd, mf.M, mf.n, mf.Pt, mf.perms.data(), mf.piinv.data(),
                       mf.n_perms, mf.sig, out));
+  if (mf.E)  // K[E_i, E_i] = -kee[i, i] (one rank)
+    hipLaunchKernelGGL(k_mf_ediag, dim3((unsigned)((mf.M + 255) / 256)), dim3(256), 0, ctx->stream,
+                       mf.kee, mf.M, out + mf.nF);
   if (ctx->nrows > 0) launch_scale_copy(out, out, ctx->nrows, ctx->sigma_K, ctx->stream);
   MLFF_HIP(ctx, hipGetLastError());
   return MLFF_OK;
@@ -670,7 +726,8 @@ void mf_free(MfData &mf) {
   for (void *p : {(void *)mf.Rd, (void *)mf.Rdd, (void *)mf.Rt, (void *)mf.Zt, (void *)mf.Pt,
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
                   (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc,
-                  (void *)mf.uvk, (void *)mf.pi_d, (void *)mf.piinv_d})
+                  (void *)mf.uvk, (void *)mf.pi_d, (void *)mf.piinv_d, (void *)mf.kee,
+                  (void *)mf.eterm})
     if (p) (void)hipFree(p);
   mf = MfData();
 }

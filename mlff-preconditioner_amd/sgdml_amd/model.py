@@ -150,7 +150,9 @@ def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
     if task.get("use_cprsn", False) or "lattice" in task:
         raise NotImplementedError("symmetry compression / periodic lattices are not supported")
     if task.get("use_E", False) and task.get("use_E_cstr", False):
-        raise NotImplementedError("energy constraints (use_E_cstr) are not supported")
+        # as the reference's train -> Iterative.solve (see Iterative.solve)
+        raise ValueError("use_E_cstr: the reference's iterative solve cannot run with energy "
+                         "constraints (operator sized 3 n M, labels 3 n M + M)")
     n_train, n_atoms = task["R_train"].shape[:2]
     perms = np.atleast_2d(np.asarray(task["perms"]))
     tpl = tril_perms_lin(perms)

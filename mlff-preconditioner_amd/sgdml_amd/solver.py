@@ -125,8 +125,11 @@ class KernelSolver:
         self._call("mlff_gen_rbf", nat.dptr(X), int(X.shape[1]), float(length_scale), float(jitter))
 
     def sgdml_operator(self, R_desc: np.ndarray, R_d_desc: np.ndarray, perms: np.ndarray,
-                       sig: float):
-        """Matrix-free sGDML operator (the reference's K_op) without assembling K."""
+                       sig: float, use_E_cstr: bool = False):
+        """Matrix-free sGDML operator (the reference's K_op) without assembling K.
+        use_E_cstr: the solver's N is 3 n_atoms M + M and the operator is the reference's
+        _K_vec with energy coefficients (iterative_solver.py:416-443); one rank only."""
+        self._call("mlff_set_energy_constraints", int(bool(use_E_cstr)))
         R_desc = np.ascontiguousarray(R_desc, dtype=np.float64)
         R_d_desc = np.ascontiguousarray(R_d_desc, dtype=np.float64)
         perms = np.ascontiguousarray(np.atleast_2d(perms), dtype=np.int32)
@@ -138,7 +141,11 @@ class KernelSolver:
                    nat.i32ptr(perms), perms.shape[0], float(sig))
 
     def assemble_sgdml(self, R_desc: np.ndarray, R_d_desc: np.ndarray, perms: np.ndarray,
-                       sig: float):
+                       sig: float, use_E_cstr: bool = False):
+        """Dense sGDML kernel (_assemble_kernel_mat, train.py:81-236, 1121-1308) and the
+        matrix-free operator of the same inputs; use_E_cstr appends the M energy rows /
+        columns (train.py:212-236; N = 3 n_atoms M + M, one rank only)."""
+        self._call("mlff_set_energy_constraints", int(bool(use_E_cstr)))
         R_desc = np.ascontiguousarray(R_desc, dtype=np.float64)
         R_d_desc = np.ascontiguousarray(R_d_desc, dtype=np.float64)
         perms = np.ascontiguousarray(np.atleast_2d(perms), dtype=np.int32)

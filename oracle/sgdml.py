@@ -50,13 +50,18 @@ def d_desc_from_comp(R_d_desc, n):
     return out.reshape(D, 3 * n)
 
 
-def assemble_kernel(R_desc, R_d_desc, tril_perms_lin_, sig):
-    """GDMLTrain._assemble_kernel_mat with col_idxs = all (train.py:81-236, 1121-1308)."""
+def assemble_kernel(R_desc, R_d_desc, tril_perms_lin_, sig, use_E_cstr=False):
+    """GDMLTrain._assemble_kernel_mat with col_idxs = all (train.py:81-236, 1121-1308).
+    use_E_cstr: M energy rows / columns appended (train.py:212-236, 1205-1208), filled by
+    column worker j for every row point i in increasing j (the order a one-process Pool
+    runs the workers in, so for a non-group permutation set the E-E entry (a, b) holds
+    the value of worker max(a, b))."""
     M, D = R_desc.shape
     n = int((1 + np.sqrt(8 * D + 1)) / 2)
     dim_i = 3 * n
     n_perms = int(len(tril_perms_lin_) / D)
-    K = np.empty((M * dim_i, M * dim_i))
+    nE = M if use_E_cstr else 0
+    K = np.empty((M * dim_i + nE, M * dim_i + nE))
     mat52_base_div = 3 * sig ** 4
     sqrt5 = np.sqrt(5.0)
     sig_pow2 = sig ** 2
@@ -76,10 +81,21 @@ def assemble_kernel(R_desc, R_d_desc, tril_perms_lin_, sig):
             blk = J[i].T.dot(O)
             K[i * dim_i:(i + 1) * dim_i, j * dim_i:(j + 1) * dim_i] = blk
             K[j * dim_i:(j + 1) * dim_i, i * dim_i:(i + 1) * dim_i] = blk.T
+        if use_E_cstr:
+            e0 = M * dim_i
+            for i in range(M):
+                diff = R_desc[i, :] - rj_desc_perms
+                norm = sqrt5 * np.linalg.norm(diff, axis=1)
+                kfe = 5 * diff / (3 * sig ** 3) * (norm[:, None] + sig) * np.exp(-norm / sig)[:, None]
+                kfe = -np.einsum("ik,jki -> j", kfe, rj_d_desc_perms)
+                K[j * dim_i:(j + 1) * dim_i, e0 + i] = kfe
+                K[e0 + i, j * dim_i:(j + 1) * dim_i] = kfe
+                K[e0 + i, e0 + j] = K[e0 + j, e0 + i] = -(
+                    1 + (norm / sig) * (1 + norm / (3 * sig))).dot(np.exp(-norm / sig))
     return K
 
 
-def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
+def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x, use_E_cstr=False):
     """K x without forming K, as the reference's CG operator evaluates it: the
     force prediction of GDMLPredict with alphas = x (predict.py:72-234, set_alphas
     :400-445, Desc.d_desc_dot_vec / vec_dot_d_desc desc.py:464-508) for every
@@ -90,14 +106,21 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
         y_i      = J_i^T F_i
     with m = exp(-norm/sig) 5/(3 sig^4), w = (sig^2 + sig norm) m.  For a
     permutation group this equals the assembled K @ x; for other permutation sets
-    it is the reference's K_op (not its mirrored assembly)."""
+    it is the reference's K_op (not its mirrored assembly).
+    use_E_cstr: x = [x_F (3 n M); x_E (M)] (iterative_solver.py:423-440, predict.py:206-218):
+        F_i     += sum_jp x_E[j] w diff
+        out_E_i  = -(sum_jp a_ijp w + sum_jp K_ee x_E[j]),
+        K_ee     = (1 + norm/sig (1 + norm/(3 sig))) exp(-norm/sig)."""
     R_desc = np.asarray(R_desc, dtype=np.float64)
     M, D = R_desc.shape
     n = int((1 + np.sqrt(8 * D + 1)) / 2)
     perms = np.atleast_2d(perms)
     P = np.array([desc_perm(p) for p in perms])  # n_perms x D descriptor maps
     s_at, t_at = np.tril_indices(n, k=-1)          # pair d = (s, t), s > t
-    X = np.asarray(x, dtype=np.float64).reshape(M, n, 3)
+    x = np.asarray(x, dtype=np.float64)
+    xE = x[3 * n * M:] if use_E_cstr else None
+    X = x[:3 * n * M].reshape(M, n, 3)
+    outE = np.empty(M)
     z = np.einsum("mdc,mdc->md", R_d_desc, X[:, t_at, :] - X[:, s_at, :])
     Rt = R_desc[:, P]                               # M x n_perms x D: Rd_j[P_p d]
     Zt = z[:, P]
@@ -110,28 +133,39 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x):
         w = (sig ** 2 + sig * norm) * m
         a = np.einsum("jpd,jpd->jp", diff, Zt)
         F = np.einsum("jp,jpd->d", 5.0 * m * a, diff) - np.einsum("jp,jpd->d", w, Zt)
+        if use_E_cstr:
+            F = F + np.einsum("jp,jpd->d", xE[:, None] * w, diff)
+            kee = (1 + (norm / sig) * (1 + norm / (3 * sig))) * np.exp(-norm / sig)
+            outE[i] = -(np.sum(a * w) + np.sum(kee * xE[:, None]))
         # y_i = J_i^T F: atom t gets +Rdd F, atom s gets -Rdd F
         contrib = R_d_desc[i] * F[:, None]
         yi = np.zeros((n, 3))
         np.add.at(yi, t_at, contrib)
         np.add.at(yi, s_at, -contrib)
         y[i] = yi
-    return y.reshape(-1)
+    return np.concatenate([y.reshape(-1), outE]) if use_E_cstr else y.reshape(-1)
 
 
-def kernel_diag(R_desc, R_d_desc, perms, sig):
+def kernel_diag(R_desc, R_d_desc, perms, sig, use_E_cstr=False):
     """diag(K) of the assembled sGDML kernel, one diagonal block K[i, i] per training point
     (IterativeCholesky._assemble_kernel_mat_diag, iterative_cholesky.py:241-373, which
     returns -diag for the PSD operator -K).  The block is
         K_ii = J_i^T (5 sum_p m_p diff_p (diff_p . J_i[P_p]) - sum_p w_p J_i[P_p]),
     diff_p = Rd_i - Rd_i[P_p].  For a single identity permutation diff = 0 and
     diag_(a,c) = -(5 / (3 sig^2)) sum_{b != a} Rdd_i[pair(a, b), c]^2, evaluated without
-    forming the D x 3n Jacobian (the nanotube's is 68265 x 1110)."""
+    forming the D x 3n Jacobian (the nanotube's is 68265 x 1110).
+    use_E_cstr: the M energy entries K[E_i, E_i] = -sum_p K_ee(|Rd_i - Rd_i[P_p]|) of
+    train.py:232-234 appended."""
     R_desc = np.asarray(R_desc, dtype=np.float64)
     R_d_desc = np.asarray(R_d_desc, dtype=np.float64)
     M, D = R_desc.shape
     n = int((1 + np.sqrt(8 * D + 1)) / 2)
     perms = np.atleast_2d(perms)
+    if use_E_cstr:
+        P = np.array([desc_perm(p) for p in perms])
+        norm = np.sqrt(5.0) * np.linalg.norm(R_desc[:, None, :] - R_desc[:, P], axis=2)  # M x n_perms
+        kee = ((1 + (norm / sig) * (1 + norm / (3 * sig))) * np.exp(-norm / sig)).sum(axis=1)
+        return np.concatenate([kernel_diag(R_desc, R_d_desc, perms, sig), -kee])
     s_at, t_at = np.tril_indices(n, k=-1)
     out = np.empty((M, n, 3))
     if perms.shape[0] == 1 and np.array_equal(perms[0], np.arange(n)):

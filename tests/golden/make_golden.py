@@ -453,7 +453,49 @@ def fx_model():
     save("sgdml_model_ethanol_n621", **out)
 
 
+def fx_ecstr(M, name, seed, perms=None):
+    """use_E_cstr (energy constraints in the kernel, train.py:212-236, 837-845): the
+    assembled (N + M) x (N + M) kernel, the matrix-free operator with energy coefficients
+    (iterative_solver.py:416-443: GDMLPredict with alphas_E, predict.py:206-218) on a fixed
+    vector, and what the reference's Iterative.solve does with it (records the exception)."""
+    ds = synthetic.ethanol_like(M, seed=seed)
+    task = dict(make_task(ds, perms=perms), use_E_cstr=True)
+    desc, tpl, R_desc, R_d_desc, _, _ = prepare(task)
+    n = 3 * M * ds["R"].shape[1]
+    y = task["F_train"].ravel().copy()
+    E_train = task["E_train"].ravel().copy()
+    y = np.hstack((y, -E_train + np.mean(E_train)))
+    y_std = np.std(y)
+    y /= y_std
+    K = gdml_train()._assemble_kernel_mat(R_desc, R_d_desc, tpl, 10, desc, use_E_cstr=True,
+                                          col_idxs=np.s_[:], callback=noop)
+    # _init_kernel_operator cannot be built at the system size n + M (create_model reshapes
+    # the n + M dummy alphas to forces and raises), and at size n its LinearOperator
+    # rejects an (n + M)-vector; the closure _K_vec itself (iterative_solver.py:416-443)
+    # splits v into forces and energies as intended, so it is called directly
+    _, K_op = kernel_operator(task, desc, R_desc, R_d_desc, tpl, n)
+    rng = np.random.default_rng(seed + 200)
+    v = rng.standard_normal(n + M)
+    out = {"R": ds["R"], "F": ds["F"], "E": ds["E"], "z": ds["z"], "perms": task["perms"],
+           "tril_perms_lin": tpl, "R_desc": R_desc, "R_d_desc": R_d_desc, "y": y,
+           "y_std": np.float64(y_std), "sig": np.float64(10.0), "lam": np.float64(1e-10),
+           "K": np.array(K), "v": v, "Kop_v": K_op._matvec(v)}
+    # the solve entry point with use_E_cstr: record what the reference does
+    for precon in ("cholesky", "eigvec_precon"):
+        try:
+            run_solver(task, desc, tpl, R_desc, R_d_desc, y, y_std, precon, 0.2, seed=1)
+            out[f"{precon}__error"] = np.array("")
+        except Exception as e:  # noqa: BLE001 - the reference's failure mode is the datum
+            out[f"{precon}__error"] = np.array(f"{type(e).__name__}: {e}")
+            print(f"  {name} {precon}: reference raised {type(e).__name__}: {e}", flush=True)
+    save(name, **out)
+
+
 FIXTURES = {
+    "ecstr_n270": lambda: fx_ecstr(10, "sgdml_ethanol_n270_ecstr", seed=3),
+    "ecstr_n270_perms": lambda: fx_ecstr(
+        10, "sgdml_ethanol_n270_perms_ecstr", seed=5,
+        perms=[np.arange(9), [0, 1, 2, 4, 5, 3, 6, 7, 8], [0, 1, 2, 5, 3, 4, 6, 7, 8]]),
     "model": fx_model,
     "descriptors": fx_descriptors,
     "rule_of_thumb": fx_rule_of_thumb,
