@@ -43,6 +43,9 @@ sys.path[:0] = [str(REPO), str(REPO / "mlff-preconditioner_amd")]
 import numpy as np  # noqa: E402
 
 METRIC = "CG iters/sec + GB/s on N×N fp64 kernel mat-vec; iters-to-1e-6 vs CPU ref"
+# MLFF_BENCH_REHEARSE=1 with several ranks: the multi-rank bench flow on ONE GPU (SOLO library
+# ranks, gloo) -- checks the script's distributed logic; its numbers are not a measurement
+REHEARSE = os.environ.get("MLFF_BENCH_REHEARSE", "0") == "1"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
@@ -99,8 +102,13 @@ def dist_setup(args):
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        if REHEARSE:
+            # one-GPU rehearsal of the multi-rank bench flow: every rank is a SOLO rank of
+            # the library on device 0 (no data exchange), torch.distributed over gloo
+            dist.init_process_group(backend="gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend="nccl")
         pg = dist
     return rank, world, local, pg
 
@@ -111,7 +119,7 @@ def barrier(pg, solver):
         import torch
 
         torch.cuda.synchronize()
-        pg.barrier()
+        pg.barrier()  # gloo in a rehearsal
 
 
 def max_over_ranks(pg, v: float) -> float:
@@ -119,7 +127,7 @@ def max_over_ranks(pg, v: float) -> float:
         return v
     import torch
 
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64, device="cpu" if REHEARSE else "cuda")
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
 
@@ -128,6 +136,8 @@ def make_solver(n, rank, world, local, pg):
     import sgdml_amd
 
     comm_id = None
+    if world > 1 and REHEARSE:
+        return sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world, comm_id=b"SOLO:")
     if world > 1:
         obj = [sgdml_amd.comm_unique_id() if rank == 0 else None]
         pg.broadcast_object_list(obj, src=0)
@@ -333,6 +343,18 @@ def sgdml_workload(args, rank, world, local, pg):
                              "perms": np.arange(n_atoms)[None, :]}
 
 
+def precon_rbf(solver, idx) -> float:
+    """Rank-k Nystrom build (random_scores) of the rbf workloads; in a rehearsal (SOLO ranks
+    exchange nothing, so the Nystrom Gram matrices would be partial) a random panel of the
+    same shape stands in."""
+    if REHEARSE and solver.world > 1:
+        r0, r1 = solver.row_range()
+        solver.precon_lowrank(np.random.default_rng(solver.rank).standard_normal(
+            (idx.size, r1 - r0)) * 1e-3)
+        return 0.0
+    return solver.precon_nystrom(idx, variant=0)
+
+
 def strong_leg(args, rank, world, local, pg, n, k, lam, ell):
     """Iterations/s of the rbf workload at size n on all ranks (same generator, Nystrom rank,
     storage and timing as the main leg): with n = 65536 the same problem as the one-GPU
@@ -346,7 +368,7 @@ def strong_leg(args, rank, world, local, pg, n, k, lam, ell):
     try:
         s.gen_rbf(X, ell)
         s.set_operator(1.0, lam)
-        s.precon_nystrom(idx, variant=0)
+        precon_rbf(s, idx)
         s.set_storage(args.storage)
         _, op_bytes = s.storage_info()
         r0, r1 = s.row_range()
@@ -440,7 +462,7 @@ def main():
         solver.gen_rbf(X, ell)
         t_gen = time.perf_counter() - t0
         solver.set_operator(1.0, lam)
-        t_pre = solver.precon_nystrom(idx, variant=0)
+        t_pre = precon_rbf(solver, idx)
     else:
         solver, n, k, b, sg_info = sgdml_workload(args, rank, world, local, pg)
         workload, lam = sg_info["workload"], 1e-10
@@ -536,6 +558,7 @@ def main():
             par = parity_small(8192, k, lam, ell)
         out = {
             "metric": METRIC,
+            **({"rehearsal": "SOLO ranks on one GPU: not a measurement"} if REHEARSE else {}),
             "value": args.steps / el,
             "unit": "CG iters/s",
             "n_gpus": world,

@@ -705,9 +705,12 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
       fold = StopFold{};
       MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     }
+    // the low-rank apply: T r (issued at the end of the previous iteration, kind 3) + z here
+    const size_t pm = mark_begin(ctx, marks);
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, zg, ctx->nrows,
                     ctx->sigma_p, 1.0 / ctx->lam, zg + ctx->blk, status, s, ctx->zpart, ctx->zsplit,
                     fold);
+    mark_end(ctx, marks, pm, it, 1);
   } else {
     launch_copy_dot(ctx->r, ctx->nrows, zg, zg + ctx->blk, status, s, fold);
   }
@@ -739,7 +742,9 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
                      lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
   }
   if (lowrank) {
+    const size_t tm = mark_begin(ctx, marks);
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    mark_end(ctx, marks, tm, it, 3);
     c0 = mark_begin(ctx, marks);
     MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));
     mark_end(ctx, marks, c0, it, 2);
@@ -1546,9 +1551,9 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
           if (mk.kind == 0) {
             ctx->timing.gemv_ms += ms;
             ctx->timing.gemv_count += 1;
-          } else if (mk.kind == 1) {
+          } else if (mk.kind == 1 || mk.kind == 3) {  // 3: second part of one apply
             ctx->timing.pre_ms += ms;
-            ctx->timing.pre_count += 1;
+            if (mk.kind == 1) ctx->timing.pre_count += 1;
           } else {
             ctx->timing.comm_ms += ms;
             ctx->timing.comm_count += 1;
