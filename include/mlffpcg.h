@@ -162,6 +162,15 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
  * (MLFF_ERR_ARG otherwise).  Replaces: the use_E_cstr argument of the reference's
  * assembly and operator (its Iterative.solve itself cannot run with it). */
 int mlff_set_energy_constraints(mlff_ctx *ctx, int use_E_cstr);
+
+/* Spectrum diagnostics of Iterative.solve(flag_eigvals=True) (iterative_solver.py:978-989,
+ * 1100-1102; dev_utils.get_eigvals, dev_utils.py:8-25): eig_out (N) = the eigenvalues,
+ * descending, of P_op A with the current low-rank preconditioner (preconditioned != 0 and
+ * one is set) or of A = sigma_K K + lam I itself (the reference's eigvals_K).  P_op A is
+ * similar to the symmetric R^T W R (A = R R^T), so its eigenvalues are real; the
+ * reference's scipy.linalg.eigvals returns them as complex in LAPACK order.  Dense O(N^3)
+ * on the device (Cholesky, GEMM, Jacobi); one rank. */
+int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out);
 

@@ -1128,6 +1128,15 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_API_END(ctx)
 }
 
+int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (eig_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null pointer");
+  MLFF_TRY(require_operator(ctx));
+  return spectrum(ctx, preconditioned != 0, eig_out);
+  MLFF_API_END(ctx)
+}
+
 int mlff_set_energy_constraints(mlff_ctx *ctx, int use_E_cstr) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);

@@ -504,6 +504,9 @@ int operator_apply_local(mlff_ctx *ctx, const double *x_loc, double *y_loc);
 // ---- eigen preconditioner (kernels_eig.hip) ----------------------------------
 int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *Lt_out,
                 double *evals_out, double *rowlev_out);
+// eigenvalues (descending) of P_op A (preconditioned, the set low-rank preconditioner) or of
+// A = sigma K + lam I: Iterative.solve(flag_eigvals=True) diagnostics, one rank
+int spectrum(mlff_ctx *ctx, bool preconditioned, double *eig_out);
 
 // ---- pivoted Cholesky (kernels_pivchol.hip) ---------------------------------
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out);

@@ -456,4 +456,69 @@ int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *
   return MLFF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Spectrum diagnostics of Iterative.solve(flag_eigvals=True) (iterative_solver.py:978-989,
+// dev_utils.py:8-25): the reference forms K = -K_op column by column, P_K = P_op @ K and
+// takes scipy.linalg.eigvals(P_K) (and of K alone for eigvals_K).  Here, with A = sigma K +
+// lam I the PCG operator (= -K_op for the sGDML sign) and P_op = sigma_p (I - T^T T) / lam
+// the low-rank preconditioner: A = R R^T (Cholesky), eig(P_op A) = sigma_p eig(R^T W R) with
+// the symmetric R^T W R = (R^T R - (T R)^T (T R)) / lam, W = (I - T^T T) / lam; without a
+// preconditioner eig(A).  Symmetric eigenvalues by the device Jacobi, sorted descending.
+// One rank; O(N^3) like the reference's dense eigvals.
+namespace {
+__global__ void k_copy_block_diag(const double *__restrict__ Y, int64_t ldy, int64_t n, double lam,
+                                  double *__restrict__ A) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n * n;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / n, j = e % n;
+    A[e] = Y[i * ldy + j] + (i == j ? lam : 0.0);
+  }
+}
+}  // namespace
+
+int spectrum(mlff_ctx *ctx, bool preconditioned, double *eig_out) {
+  hipStream_t s = ctx->stream;
+  const int64_t n = ctx->N, blk = ctx->blk;
+  if (ctx->world > 1) return set_error(ctx, MLFF_ERR_ARG, "spectrum: one rank only");
+  if (n > 46340) return set_error(ctx, MLFF_ERR_ARG, "spectrum: N too large for a dense N x N");
+  if (preconditioned && ctx->precon_kind == MLFF_PRECON_NONE) preconditioned = false;
+  MLFF_TRY(operator_prepare(ctx));
+  ScratchScope scope(ctx);
+  double *Y = nullptr, *A = nullptr, *V = nullptr, *x = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &Y, (size_t)round_up(n, 8) * blk));
+  MLFF_TRY(scratch_alloc(ctx, &A, (size_t)n * n));
+  MLFF_TRY(scratch_alloc(ctx, &V, (size_t)n * n));
+  MLFF_TRY(scratch_alloc(ctx, &x, (size_t)round_up(n, 8) * blk));
+  // A = sigma K + lam I, row j = the operator applied to e_j (K symmetric)
+  MLFF_HIP(ctx, hipMemsetAsync(x, 0, sizeof(double) * round_up(n, 8) * blk, s));
+  hipLaunchKernelGGL(k_eig_identity, dim3(grid1(n)), dim3(256), 0, s, x, blk, n, (int64_t)0, ctx->nrows);
+  for (int64_t j = 0; j < n; ++j) MLFF_TRY(operator_apply_local(ctx, x + j * blk, Y + j * blk));
+  hipLaunchKernelGGL(k_copy_block_diag, dim3(grid1(n * n)), dim3(256), 0, s, Y, blk, n, ctx->lam, A);
+  hipLaunchKernelGGL(k_symmetrize, dim3(grid1(n * n)), dim3(256), 0, s, A, (int)n);
+  double *H = A;
+  if (preconditioned) {
+    // R = chol(A) (lower, in place in a copy); H = (R^T R - X^T X) / lam, X = T R (k x n)
+    double *R = Y;  // Y is free now (n x n fits in its n x blk)
+    MLFF_HIP(ctx, hipMemcpyAsync(R, A, sizeof(double) * n * n, hipMemcpyDeviceToDevice, s));
+    MLFF_TRY(potrf_lower(ctx, R, n));
+    const int64_t k = ctx->k;
+    double *X = x;  // k x n
+    launch_gemm(false, false, k, n, n, 1.0, ctx->T, blk, R, n, 0.0, X, n, s);
+    launch_gemm(true, false, n, n, n, 1.0 / ctx->lam, R, n, R, n, 0.0, A, n, s);
+    launch_gemm(true, false, n, n, k, -1.0 / ctx->lam, X, n, X, n, 1.0, A, n, s);
+    hipLaunchKernelGGL(k_symmetrize, dim3(grid1(n * n)), dim3(256), 0, s, A, (int)n);
+    MLFF_HIP(ctx, hipGetLastError());
+  }
+  MLFF_TRY(jacobi_eigh(ctx, H, (int)n, V));
+  std::vector<double> d(n);
+  MLFF_HIP(ctx, hipMemcpy2DAsync(d.data(), sizeof(double), H, sizeof(double) * (n + 1), sizeof(double),
+                                 n, hipMemcpyDeviceToHost, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  const double sg = preconditioned ? ctx->sigma_p : 1.0;
+  for (int64_t i = 0; i < n; ++i) d[i] *= sg;
+  std::sort(d.begin(), d.end(), [](double a, double b) { return a > b; });
+  std::copy(d.begin(), d.end(), eig_out);
+  return MLFF_OK;
+}
+
 }  // namespace mlff

@@ -249,8 +249,6 @@ def cg_steps_record(task: dict, model: dict, n_datapoints: int, preconditioner_s
     trained model: Cholesky step timings and their begin/end medians (:123-131), the
     preconditioner size actually used (:116-120), CG step count and the solver's timings
     (:142-149), the task and its info keys (:150-152)."""
-    if flag_eigvals:
-        raise NotImplementedError("flag_eigvals: eigenvalue spectra are not computed here")
     n = len(model["alphas_F"])
     actual = len(model["inducing_pts_idxs"]) / n
     k = int(actual * n)
@@ -263,7 +261,10 @@ def cg_steps_record(task: dict, model: dict, n_datapoints: int, preconditioner_s
         rec["chol_t_begin"] = t_begin
         rec["chol_t_end"] = t_end
         rec["chol_t_correction"] = t_end / t_begin - 1
-    if model["is_conv"] is False:
+    if flag_eigvals:  # create_data.py:133-135
+        rec[f"eigvals_{preconditioner}_{preconditioner_strength * 100:.2f}"] = model["eigvals"]
+        rec[f"eigvals_{preconditioner}_{0}"] = model["eigvals_K"]
+    if model["is_conv"] is False and flag_eigvals is False:  # :137 (not for eigvals runs)
         raise RuntimeError("Solver is not converged.")
     rec[f"{preconditioner}_percentage"] = actual
     rec[f"{preconditioner}_cgsteps"] = model["solver_iters"]

@@ -197,6 +197,13 @@ class KernelSolver:
         self._call("mlff_matvec", nat.dptr(v), nat.dptr(y))
         return y
 
+    def spectrum(self, preconditioned: bool = True) -> np.ndarray:
+        """Eigenvalues (descending) of P_op A, or of A = sigma_K K + lam I: the flag_eigvals
+        diagnostics of Iterative.solve (iterative_solver.py:978-989).  One rank, dense."""
+        out = np.empty(self.n)
+        self._call("mlff_spectrum", int(bool(preconditioned)), nat.dptr(out))
+        return out
+
     def diag(self) -> np.ndarray:
         d = np.empty(self.nrows)
         self._call("mlff_get_diag", nat.dptr(d))

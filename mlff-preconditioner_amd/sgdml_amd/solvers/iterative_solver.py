@@ -137,8 +137,6 @@ class Iterative(object):
             raise ValueError(f"use_E_cstr: the system has {n + n_train} entries (forces and "
                              f"energies) but the reference's solve builds its operator and "
                              f"preconditioner at {n}")
-        if flag_eigvals:
-            raise NotImplementedError("flag_eigvals (dense O(N^3) spectrum diagnostics) is out of scope")
 
         alphas0_F = task["alphas0_F"] if "alphas0_F" in task else None
         num_iters0 = task["solver_iters"] if "solver_iters" in task else 0
@@ -216,8 +214,17 @@ class Iterative(object):
         stop_preconditioner = timeit.default_timer()
         total_time_preconditioner = stop_preconditioner - start_preconditioner
 
+        eig_info = None
+        if flag_eigvals:
+            # iterative_solver.py:978-989 (dev_utils.get_eigvals): the spectra of P_op K and
+            # of K, K = -K_op (the PCG operator), dense on the device (mlff_spectrum); real
+            # and descending here, complex in LAPACK order in the reference
+            if getattr(solver, "world", 1) > 1:
+                raise NotImplementedError("flag_eigvals: the dense spectrum runs on one GPU")
+            eig_info = {"eigvals": solver.spectrum(True), "eigvals_K": solver.spectrum(False)}
         x0 = None if alphas0_F is None else -np.asarray(alphas0_F, dtype=np.float64)
-        maxiter = 3 * n_atoms * n_train * 5
+        # the reference stops the CG after 10 iterations when the spectra are requested (:1002)
+        maxiter = 3 * n_atoms * n_train * 5 if not flag_eigvals else 10
         progress = _Checkpointer(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std,
                                  inducing_pts_idxs, num_iters0, save_progr_callback)
         op_storage, op_bytes = solver.storage_info()
@@ -250,6 +257,8 @@ class Iterative(object):
                 "n_gpus": getattr(solver, "world", 1)}
         if info_cholesky is not None:
             info.update(info_cholesky)
+        if eig_info is not None:
+            info.update(eig_info)  # iterative_solver.py:1100-1102
         train_rmse = resid / np.sqrt(len(y))
         return alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info
 

@@ -211,7 +211,8 @@ def noop(*a, **k):
     pass
 
 
-def run_solver(task, desc, tril_perms_lin, R_desc, R_d_desc, y, y_std, precon, bp, seed):
+def run_solver(task, desc, tril_perms_lin, R_desc, R_d_desc, y, y_std, precon, bp, seed,
+               flag_eigvals=False):
     """Iterative.solve exactly as GDMLTrain.train calls it (train.py:859-890)."""
     iterative_solver.glob_U = None
     iterative_solver.glob_s = None
@@ -222,7 +223,7 @@ def run_solver(task, desc, tril_perms_lin, R_desc, R_d_desc, y, y_std, precon, b
     it = iterative_solver.Iterative(gdml_train(), desc, callback=noop, max_processes=1, use_torch=False)
     t0 = time.time()
     out = it.solve(task, R_desc, R_d_desc, tril_perms_lin, y, y_std, save_progr_callback=None,
-                   break_percentage=bp, str_preconditioner=precon, flag_eigvals=False)
+                   break_percentage=bp, str_preconditioner=precon, flag_eigvals=flag_eigvals)
     alphas, num_iters, resid, train_rmse, idxs, is_conv, info = out
     res = {
         "alphas": np.asarray(alphas), "num_iters": np.int64(num_iters), "resid": np.float64(resid),
@@ -231,6 +232,9 @@ def run_solver(task, desc, tril_perms_lin, R_desc, R_d_desc, y, y_std, precon, b
     }
     if precon == "cholesky":
         res["index_columns"] = np.asarray(info["index_columns"], dtype=np.int64)
+    if flag_eigvals:
+        res["eigvals"] = np.asarray(info["eigvals"])
+        res["eigvals_K"] = np.asarray(info["eigvals_K"])
     return res
 
 
@@ -491,7 +495,35 @@ def fx_ecstr(M, name, seed, perms=None):
     save(name, **out)
 
 
+def fx_eigvals(M, name, seed, precons):
+    """Iterative.solve(flag_eigvals=True) (iterative_solver.py:978-989, 1002, 1100-1102):
+    the spectra of P_op K and of K (dev_utils.get_eigvals, complex, LAPACK order) and the
+    10-iteration CG it runs instead of a full solve."""
+    iterative_solver.glob_eigvals_K = None
+    ds = synthetic.ethanol_like(M, seed=seed)
+    task = make_task(ds)
+    desc, tpl, R_desc, R_d_desc, y, y_std = prepare(task)
+    n = y.size
+    m, kmin, _ = plot_data.get_params("ethanol")
+    k_rot = int(plot_data.rule_of_thumb(n=n, k_min=kmin, m=m))
+    out = {"R": ds["R"], "F": ds["F"], "E": ds["E"], "z": ds["z"], "perms": task["perms"],
+           "tril_perms_lin": tpl, "R_desc": R_desc, "R_d_desc": R_d_desc, "y": y,
+           "y_std": np.float64(y_std), "sig": np.float64(10.0), "lam": np.float64(1e-10),
+           "solver_tol": np.float64(task["solver_tol"]), "k_rot": np.int64(k_rot)}
+    for p in precons:
+        iterative_solver.glob_eigvals_K = None  # the reference caches eigvals_K module-wide
+        res = run_solver(task, desc, tpl, R_desc, R_d_desc, y, y_std, p, k_rot / n,
+                         seed=1000 + seed, flag_eigvals=True)
+        for key, val in res.items():
+            out[f"{p}__{key}"] = val
+        print(f"  {name} {p}: iters={res['num_iters']} eig range "
+              f"{np.abs(res['eigvals']).min():.3e}..{np.abs(res['eigvals']).max():.3e}", flush=True)
+    save(name, **out)
+
+
 FIXTURES = {
+    "eigvals_n270": lambda: fx_eigvals(10, "sgdml_ethanol_n270_eigvals", 3,
+                                       ["cholesky", "random_scores", "eigvec_precon"]),
     "ecstr_n270": lambda: fx_ecstr(10, "sgdml_ethanol_n270_ecstr", seed=3),
     "ecstr_n270_perms": lambda: fx_ecstr(
         10, "sgdml_ethanol_n270_perms_ecstr", seed=5,
