@@ -171,6 +171,14 @@ int mlff_set_energy_constraints(mlff_ctx *ctx, int use_E_cstr);
  * reference's scipy.linalg.eigvals returns them as complex in LAPACK order.  Dense O(N^3)
  * on the device (Cholesky, GEMM, Jacobi); one rank. */
 int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out);
+
+/* Test hook (no reference counterpart): C = alpha op(A) op(B) + beta C through the library's
+ * fp64 GEMM (matrix-core path for M >= 64, N >= 128, K >= 32; VALU otherwise), host arrays,
+ * row-major; splits > 1 runs the split-K slab path and returns C - alpha op(A) op(B)
+ * (beta must be 1).  Lets the tests check every operand layout with asymmetric data. */
+int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha,
+                   const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                   double *C, int64_t ldc, int splits);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out);
 

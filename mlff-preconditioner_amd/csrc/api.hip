@@ -1128,6 +1128,18 @@ int mlff_sgdml_operator(mlff_ctx *ctx, const double *R_desc, const double *R_d_d
   MLFF_API_END(ctx)
 }
 
+int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha,
+                   const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
+                   double *C, int64_t ldc, int splits) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (A == nullptr || B == nullptr || C == nullptr || M < 0 || N < 0 || K < 0 || splits < 1 ||
+      lda < (ta ? M : K) || ldb < (tb ? K : N) || ldc < N)
+    return set_error(ctx, MLFF_ERR_ARG, "test_gemm: bad arguments");
+  return test_gemm(ctx, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits);
+  MLFF_API_END(ctx)
+}
+
 int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);

@@ -507,6 +507,11 @@ int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *
 // eigenvalues (descending) of P_op A (preconditioned, the set low-rank preconditioner) or of
 // A = sigma K + lam I: Iterative.solve(flag_eigvals=True) diagnostics, one rank
 int spectrum(mlff_ctx *ctx, bool preconditioned, double *eig_out);
+// test hook: C = alpha op(A) op(B) + beta C on the device from host arrays (splits > 1: the
+// split-K slab path, returning C - alpha op(A) op(B) with beta = 1)
+int test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+              const double *A, int64_t lda, const double *B, int64_t ldb, double beta, double *C,
+              int64_t ldc, int splits);
 
 // ---- pivoted Cholesky (kernels_pivchol.hip) ---------------------------------
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out);

@@ -8,6 +8,8 @@
 // contiguous 512-B row segments.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace mlff {
 
 // ---------------------------------------------------------------------------
@@ -82,12 +84,149 @@ __global__ __launch_bounds__(256) void k_gemm(int64_t M, int64_t N, int64_t K, d
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same GEMM on the matrix cores (v_mfma_f64_16x16x4_f64): BM x 128 output tile per
+// 256-thread workgroup (BM = 64 or 128), the four waves 2 x 2 over it, each wave BM/2 x 64
+// as (BM/32) x 4 blocks of 16 x 16; K staged through LDS 16 at a time exactly as k_gemm
+// stages it.  Lane l of a 16x16x4 step holds A[row l&15][k l>>4] and B[k l>>4][col l&15];
+// register r of its result is C[row (l>>4) + 4r][col l&15] (cdna_hip_programming.md, f64
+// MFMA layout).  LDS rows padded to 144 doubles (288 dwords = 32 mod 64 banks): the four
+// k rows one step reads fall on disjoint bank halves pairwise (2 passes, the minimum).
+// Fixed summation order (k ascending, 4 per instruction): deterministic.
+typedef double v4d __attribute__((ext_vector_type(4)));
+template <int BM, bool TA, bool TB>
+__global__ __launch_bounds__(256) void k_gemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
+                                                   const double *__restrict__ A, int64_t lda,
+                                                   const double *__restrict__ B, int64_t ldb,
+                                                   double beta, double *__restrict__ C,
+                                                   int64_t ldc, int64_t kchunk,
+                                                   int64_t slab_stride) {
+  constexpr int BN = 128, BK = 16, LP = 144;
+  constexpr int IM = BM / 32, JN = 4;  // 16 x 16 blocks per wave
+  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // staged elements per thread
+  __shared__ double As[BK][LP];
+  __shared__ double Bs[BK][LP];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wm = (wv >> 1) * (BM / 2), wn = (wv & 1) * 64;
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
+  const int64_t kb = (int64_t)blockIdx.z * kchunk;
+  int64_t ke = kb + kchunk;
+  if (ke > K) ke = K;
+  C += (int64_t)blockIdx.z * slab_stride;
+  v4d acc[IM][JN];
+#pragma unroll
+  for (int i = 0; i < IM; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) acc[i][j] = v4d{0.0, 0.0, 0.0, 0.0};
+  // software pipeline: the next K tile's global loads are in flight while the matrix
+  // cores work on the current one (one wave per SIMD at this register count)
+  double va[LA], vb[LB];
+  auto load_tile = [&](int64_t k0) {
+#pragma unroll
+    for (int l = 0; l < LA; ++l) {
+      const int e = tid + 256 * l;
+      const int mm = TA ? (e % BM) : (e / BK), kk = TA ? (e / BM) : (e % BK);
+      const int64_t gm = m0 + mm, gk = k0 + kk;
+      va[l] = (gm < M && gk < ke) ? (TA ? A[gk * lda + gm] : A[gm * lda + gk]) : 0.0;
+    }
+#pragma unroll
+    for (int l = 0; l < LB; ++l) {
+      const int e = tid + 256 * l;
+      const int nn = TB ? (e / BK) : (e % BN), kk = TB ? (e % BK) : (e / BN);
+      const int64_t gn = n0 + nn, gk = k0 + kk;
+      vb[l] = (gn < N && gk < ke) ? (TB ? B[gn * ldb + gk] : B[gk * ldb + gn]) : 0.0;
+    }
+  };
+  if (kb < ke) load_tile(kb);
+  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+    __syncthreads();  // the previous step's fragment reads are done
+#pragma unroll
+    for (int l = 0; l < LA; ++l) {
+      const int e = tid + 256 * l;
+      As[TA ? (e / BM) : (e % BK)][TA ? (e % BM) : (e / BK)] = va[l];
+    }
+#pragma unroll
+    for (int l = 0; l < LB; ++l) {
+      const int e = tid + 256 * l;
+      Bs[TB ? (e % BK) : (e / BN)][TB ? (e / BK) : (e % BN)] = vb[l];
+    }
+    __syncthreads();
+    if (k0 + BK < ke) load_tile(k0 + BK);
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const int kr = 4 * ks + (lane >> 4);
+      double a[IM], b[JN];
+#pragma unroll
+      for (int i = 0; i < IM; ++i) a[i] = As[kr][wm + 16 * i + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < JN; ++j) b[j] = Bs[kr][wn + 16 * j + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IM; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t gm = m0 + wm + 16 * i + (lane >> 4) + 4 * r;
+        const int64_t gn = n0 + wn + 16 * j + (lane & 15);
+        if (gm >= M || gn >= N) continue;
+        double v = alpha * acc[i][j][r];
+        if (beta != 0.0) v = fma(beta, C[gm * ldc + gn], v);
+        C[gm * ldc + gn] = v;
+      }
+}
+
+template <int BM>
+static void gemm_mfma_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+                             const double *A, int64_t lda, const double *B, int64_t ldb,
+                             double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
+                             int64_t slab_stride, hipStream_t s) {
+  dim3 grid((unsigned)((Nc + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
+  if (!ta && !tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
+                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (!ta && tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
+                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (ta && !tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
+                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
+                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+}
+
+// the matrix-core path for every GEMM at least 64 x 128 with a K of 32 or more
+// (MLFF_GEMM_VALU=1 keeps the VALU kernel for A/B sweeps)
+static bool use_mfma(int64_t M, int64_t Nc, int64_t Kd) {
+  static const bool valu = [] {
+    const char *e = std::getenv("MLFF_GEMM_VALU");
+    return e != nullptr && e[0] == '1';
+  }();
+  return !valu && M >= 64 && Nc >= 128 && Kd >= 32;
+}
+
 static void gemm_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                         const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                         double *C, int64_t ldc, int splits, int64_t slab_stride, hipStream_t s) {
   if (M <= 0 || Nc <= 0) return;
   int64_t kchunk = (Kd + splits - 1) / splits;
   kchunk = round_up(kchunk < 1 ? 1 : kchunk, 16);
+  if (use_mfma(M, Nc, Kd)) {
+    if (M >= 128)
+      gemm_mfma_launch<128>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, splits,
+                            slab_stride, s);
+    else
+      gemm_mfma_launch<64>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, splits,
+                           slab_stride, s);
+    return;
+  }
   dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)splits);
   if (!ta && !tb)
     hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
@@ -127,7 +266,10 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
 int gram_wide(mlff_ctx *ctx, const double *A, const double *Bm, int64_t k, int64_t ncols,
               int64_t ldw, double *G) {
   const double *W = A;
-  const int64_t tiles = ((k + 63) / 64) * ((k + 63) / 64);
+  // workgroup tiles of the GEMM path taken (matrix cores: up to 128 x 128, VALU: 64 x 64)
+  const int64_t tm = use_mfma(k, k, ncols) ? (k >= 128 ? 128 : 64) : 64;
+  const int64_t tn = use_mfma(k, k, ncols) ? 128 : 64;
+  const int64_t tiles = ((k + tm - 1) / tm) * ((k + tn - 1) / tn);
   int64_t splits = (1024 + tiles - 1) / tiles;
   const int64_t max_splits = (ncols + 511) / 512;
   if (splits > max_splits) splits = max_splits;
@@ -291,13 +433,46 @@ __global__ __launch_bounds__(256) void k_trsm_diag_wide(const double *__restrict
     if (r < ib) W[(i0 + r) * ldw + c] = x[r];
 }
 
+// W_blk -= sum_s slab_s (deterministic order), ib x ncols
+__global__ __launch_bounds__(256) void k_sub_slabs(const double *__restrict__ slabs, int splits,
+                                                   int ib, int64_t ncols, double *__restrict__ W,
+                                                   int64_t ldw) {
+  const int64_t n = (int64_t)ib * ncols;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    double a = 0.0;
+    for (int sp = 0; sp < splits; ++sp) a += slabs[(int64_t)sp * n + e];
+    const int64_t r = e / ncols, c = e % ncols;
+    W[r * ldw + c] -= a;
+  }
+}
+
 int trsm_lower_wide(mlff_ctx *ctx, const double *L, int64_t k, double *W, int64_t ncols,
                     int64_t ldw) {
+  ScratchScope scope(ctx);
+  double *slabs = nullptr;
+  int64_t slab_cap = 0;
   for (int64_t i0 = 0; i0 < k; i0 += 64) {
     const int ib = (int)std::min<int64_t>(64, k - i0);
-    if (i0 > 0)
-      gemm_launch(false, false, ib, ncols, i0, -1.0, L + i0 * k, k, W, ldw, 1.0, W + i0 * ldw,
-                  ldw, 1, 0, ctx->stream);
+    if (i0 > 0) {
+      // W[i0 : i0 + ib] -= L[i0 : i0 + ib, :i0] W[:i0]: one 64-row band, so split K until
+      // the band's tiles (ncols / 128 of them) fill the chip
+      const int64_t tiles = (ncols + 127) / 128;
+      int64_t splits = std::min<int64_t>((512 + tiles - 1) / tiles, (i0 + 63) / 64);
+      if (!use_mfma(ib, ncols, i0) || splits < 2) {
+        gemm_launch(false, false, ib, ncols, i0, -1.0, L + i0 * k, k, W, ldw, 1.0, W + i0 * ldw,
+                    ldw, 1, 0, ctx->stream);
+      } else {
+        const int64_t need = splits * ib * ncols;
+        if (need > slab_cap) {
+          MLFF_TRY(scratch_alloc(ctx, &slabs, (size_t)need));
+          slab_cap = need;
+        }
+        gemm_launch(false, false, ib, ncols, i0, 1.0, L + i0 * k, k, W, ldw, 0.0, slabs, ncols,
+                    (int)splits, ib * ncols, ctx->stream);
+        hipLaunchKernelGGL(k_sub_slabs, dim3((unsigned)std::min<int64_t>((ib * ncols + 255) / 256, 4096)),
+                           dim3(256), 0, ctx->stream, slabs, (int)splits, ib, ncols, W + i0 * ldw, ldw);
+      }
+    }
     hipLaunchKernelGGL(k_trsm_diag_wide, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0,
                        ctx->stream, L, k, i0, ib, W, ldw, ncols);
   }
@@ -323,6 +498,35 @@ void launch_colsumsq(const double *W, int64_t k, int64_t ncols, int64_t ldw, dou
   if (ncols <= 0) return;
   hipLaunchKernelGGL(k_colsumsq, dim3((unsigned)((ncols + 255) / 256)), dim3(256), 0, s, W, k,
                      ncols, ldw, out);
+}
+
+int test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+              const double *A, int64_t lda, const double *B, int64_t ldb, double beta, double *C,
+              int64_t ldc, int splits) {
+  hipStream_t s = ctx->stream;
+  const int64_t na = (ta ? Kd : M) * lda, nb = (tb ? Nc : Kd) * ldb, nc = M * ldc;
+  ScratchScope scope(ctx);
+  double *dA = nullptr, *dB = nullptr, *dC = nullptr, *slabs = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &dA, (size_t)na));
+  MLFF_TRY(scratch_alloc(ctx, &dB, (size_t)nb));
+  MLFF_TRY(scratch_alloc(ctx, &dC, (size_t)nc));
+  MLFF_HIP(ctx, hipMemcpyAsync(dA, A, sizeof(double) * na, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(dB, B, sizeof(double) * nb, hipMemcpyHostToDevice, s));
+  MLFF_HIP(ctx, hipMemcpyAsync(dC, C, sizeof(double) * nc, hipMemcpyHostToDevice, s));
+  if (splits <= 1) {
+    gemm_launch(ta != 0, tb != 0, M, Nc, Kd, alpha, dA, lda, dB, ldb, beta, dC, ldc, 1, 0, s);
+  } else {  // the split-K slab path of gram_wide / trsm_lower_wide: C = beta C + alpha sum_s
+    MLFF_TRY(scratch_alloc(ctx, &slabs, (size_t)splits * M * ldc));
+    gemm_launch(ta != 0, tb != 0, M, Nc, Kd, alpha, dA, lda, dB, ldb, 0.0, slabs, ldc, splits,
+                M * ldc, s);
+    if (beta != 1.0) return set_error(ctx, MLFF_ERR_ARG, "test_gemm: split path needs beta = 1");
+    hipLaunchKernelGGL(k_sub_slabs, dim3(256), dim3(256), 0, s, slabs, splits, (int)M, ldc, dC, ldc);
+    // k_sub_slabs subtracts: report C - alpha AB for the caller to compare
+  }
+  MLFF_HIP(ctx, hipGetLastError());
+  MLFF_HIP(ctx, hipMemcpyAsync(C, dC, sizeof(double) * nc, hipMemcpyDeviceToHost, s));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
+  return MLFF_OK;
 }
 
 }  // namespace mlff
