@@ -576,7 +576,9 @@ def main():
             "config": {"workload": workload,
                        "baseline_config": ("configs[3]" if n == 131072 else
                                            "configs[2]" if n == 65536 else None)
-                       if sg_info is None else ("configs[1]" if n == 15540 else None),
+                       if sg_info is None else (None if n != 15540 else
+                                                ("configs[4]" if k == 1024 and world > 1
+                                                 else "configs[1]")),
                        "n": n, "k": k, "lambda": lam,
                        "length_scale": ell if sg_info is None else 10.0,
                        "precon": "random_scores (Nystrom, iterative_solver.py:95-322)"
