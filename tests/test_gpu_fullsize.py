@@ -82,3 +82,28 @@ def test_nanotube_n15540_matfree_operator(sg):
     nr = np.linalg.norm(ref)
     assert np.linalg.norm(y_mf - ref) <= 1e-12 * nr
     assert np.linalg.norm(y_dense - ref) <= 1e-12 * nr
+
+
+@pytest.mark.timeout(600)
+def test_rbf_configs2_solve_true_residual(sg):
+    """configs[2] workload (N = 65536 RBF, l = 0.2, lam = 1e-6, rank-256 Nystrom with the
+    bench's seeded columns) solved to 1e-6 on the symmetric tiles; the true residual
+    ||b - A x|| is then recomputed with the DENSE-row operator (a different kernel over a
+    separately generated copy of K) and meets the tolerance.  Size-independent check of the
+    whole bench path (generator, Nystrom build, tiles, PCG) at full size."""
+    from sgdml_amd import synthetic
+
+    n, ell, lam, k = 65536, 0.2, 1e-6, 256
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, ell)
+        s.set_operator(1.0, lam)
+        s.precon_nystrom(idx, variant=0)
+        s.set_storage("sym")
+        res = s.pcg(b, tol=1e-6, maxiter=20000)
+        assert res.info == 0
+        s.set_storage("dense")
+        r = b - s.matvec(res.x)
+    # 1.1: the two operators round differently (~1e-16 ||A|| ||x||, far below 1e-6 ||b||)
+    assert np.linalg.norm(r) <= 1.1e-6 * np.linalg.norm(b)
