@@ -94,20 +94,22 @@ __global__ __launch_bounds__(256) void k_gemm(int64_t M, int64_t N, int64_t K, d
 // k rows one step reads fall on disjoint bank halves pairwise (2 passes, the minimum).
 // Fixed summation order (k ascending, 4 per instruction): deterministic.
 typedef double v4d __attribute__((ext_vector_type(4)));
-template <int BM, bool TA, bool TB>
-__global__ __launch_bounds__(256) void k_gemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
+template <int BM, bool TA, bool TB, int NTH = 256>
+__global__ __launch_bounds__(NTH) void k_gemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
                                                    const double *__restrict__ A, int64_t lda,
                                                    const double *__restrict__ B, int64_t ldb,
                                                    double beta, double *__restrict__ C,
                                                    int64_t ldc, int64_t kchunk,
                                                    int64_t slab_stride) {
   constexpr int BN = 128, BK = 16, LP = 144;
-  constexpr int IM = BM / 32, JN = 4;  // 16 x 16 blocks per wave
-  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // staged elements per thread
+  constexpr int WR = NTH / 128;        // wave rows (two wave columns of 64)
+  constexpr int IM = BM / WR / 16, JN = 4;  // 16 x 16 blocks per wave
+  static_assert(IM >= 1, "tile too small for the wave grid");
+  constexpr int LA = BM * BK / NTH, LB = BN * BK / NTH;  // staged elements per thread
   __shared__ double As[BK][LP];
   __shared__ double Bs[BK][LP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wm = (wv >> 1) * (BM / 2), wn = (wv & 1) * 64;
+  const int wm = (wv >> 1) * (BM / WR), wn = (wv & 1) * 64;
   const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
   const int64_t kb = (int64_t)blockIdx.z * kchunk;
   int64_t ke = kb + kchunk;
@@ -124,14 +126,14 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(int64_t M, int64_t N, int64_t
   auto load_tile = [&](int64_t k0) {
 #pragma unroll
     for (int l = 0; l < LA; ++l) {
-      const int e = tid + 256 * l;
+      const int e = tid + NTH * l;
       const int mm = TA ? (e % BM) : (e / BK), kk = TA ? (e / BM) : (e % BK);
       const int64_t gm = m0 + mm, gk = k0 + kk;
       va[l] = (gm < M && gk < ke) ? (TA ? A[gk * lda + gm] : A[gm * lda + gk]) : 0.0;
     }
 #pragma unroll
     for (int l = 0; l < LB; ++l) {
-      const int e = tid + 256 * l;
+      const int e = tid + NTH * l;
       const int nn = TB ? (e / BK) : (e % BN), kk = TB ? (e % BK) : (e / BN);
       const int64_t gn = n0 + nn, gk = k0 + kk;
       vb[l] = (gn < N && gk < ke) ? (TB ? B[gn * ldb + gk] : B[gk * ldb + gn]) : 0.0;
@@ -142,12 +144,12 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(int64_t M, int64_t N, int64_t
     __syncthreads();  // the previous step's fragment reads are done
 #pragma unroll
     for (int l = 0; l < LA; ++l) {
-      const int e = tid + 256 * l;
+      const int e = tid + NTH * l;
       As[TA ? (e / BM) : (e % BK)][TA ? (e % BM) : (e / BK)] = va[l];
     }
 #pragma unroll
     for (int l = 0; l < LB; ++l) {
-      const int e = tid + 256 * l;
+      const int e = tid + NTH * l;
       Bs[TB ? (e % BK) : (e / BN)][TB ? (e / BK) : (e % BN)] = vb[l];
     }
     __syncthreads();
@@ -182,24 +184,46 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(int64_t M, int64_t N, int64_t
       }
 }
 
+template <int BM, int NTH>
+static void gemm_mfma_launch_t(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
+                               const double *A, int64_t lda, const double *B, int64_t ldb,
+                               double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
+                               int64_t slab_stride, hipStream_t s) {
+  dim3 grid((unsigned)((Nc + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
+  if (!ta && !tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (!ta && tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else if (ta && !tb)
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  else
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+}
+
+// workgroup size of the matrix-core GEMM (MLFF_GEMM_NTH = 256 / 512 for A/B sweeps)
+static int gemm_nth() {
+  static const int nth = [] {
+    const char *e = std::getenv("MLFF_GEMM_NTH");
+    return (e != nullptr && std::atoi(e) == 256) ? 256 : 512;
+  }();
+  return nth;
+}
+
 template <int BM>
 static void gemm_mfma_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                              const double *A, int64_t lda, const double *B, int64_t ldb,
                              double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
                              int64_t slab_stride, hipStream_t s) {
-  dim3 grid((unsigned)((Nc + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
-  if (!ta && !tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, false, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
-                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
-  else if (!ta && tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, false, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
-                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
-  else if (ta && !tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, true, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
-                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+  if (gemm_nth() == 512)
+    gemm_mfma_launch_t<BM, 512>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
+                                splits, slab_stride, s);
   else
-    hipLaunchKernelGGL((k_gemm_mfma<BM, true, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A,
-                       lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+    gemm_mfma_launch_t<BM, 256>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
+                                splits, slab_stride, s);
 }
 
 // the matrix-core path for every GEMM at least 64 x 128 with a K of 32 or more
