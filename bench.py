@@ -46,6 +46,12 @@ METRIC = "CG iters/sec + GB/s on N×N fp64 kernel mat-vec; iters-to-1e-6 vs CPU 
 # MLFF_BENCH_REHEARSE=1 with several ranks: the multi-rank bench flow on ONE GPU (SOLO library
 # ranks, gloo) -- checks the script's distributed logic; its numbers are not a measurement
 REHEARSE = os.environ.get("MLFF_BENCH_REHEARSE", "0") == "1"
+# the reference's published seconds per PCG step for the nanotube
+# (its matrix-free PyTorch operator on NVIDIA GPUs): N = 15540 (configs[1], 0.105 s,
+# data/data/cg_performance_n=15750/...nanotube_points14_meas31), N ~ 157k (2.073 s on an
+# A100-PCIe 40 GB, data/data/rule_of_thumb/n = 157500) and N ~ 505k (6.600 s on a Quadro RTX
+# 6000, data/data/rule_of_thumb/n = 500000); here M = 14 / 141 / 455 training geometries
+REF_STEP_S = {15540: 0.105, 156510: 2.073, 505050: 6.600}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
@@ -512,9 +518,9 @@ def main():
                                      "(matrix-free sGDML operator)"}.get(storage, storage),
                "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
     if storage == "matfree":
-        roof_op["note"] = ("five dependent launches of ~5-13 us each over 5-22 MB: neither "
-                           "HBM- nor FP64-bound (PMC traffic and L2 hit rates in "
-                           "profiles/pmc_traffic.json; DESIGN.md 'matrix-free operator')")
+        roof_op["note"] = ("five dependent launches (pair sums, their finish, F, J^T F, finish): "
+                           "at the nanotube's M = 14 neither HBM- nor FP64-bound (PMC traffic "
+                           "and L2 hit rates in profiles/pmc_traffic.json; DESIGN.md 3.2)")
     # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials
     roof_pre = None
     if tm.get("precon_count"):
@@ -569,8 +575,8 @@ def main():
             "scaling": "strong",
             # BASELINE.md publishes a CG step time only for the nanotube (0.105 s/step at
             # N = 15540, data/data/cg_performance_n=15750/..._nanotube_points14_meas31)
-            "vs_baseline": (args.steps / el) / (1.0 / 0.105)
-            if args.workload == "nanotube" and n == 15540 else None,
+            "vs_baseline": (args.steps / el) / (1.0 / REF_STEP_S[n])
+            if args.workload == "nanotube" and n in REF_STEP_S else None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": workload,

@@ -1275,8 +1275,8 @@ int mlff_precon_pivchol(mlff_ctx *ctx, int64_t k, int build_woodbury, int64_t *i
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   MLFF_TRY(require_operator(ctx));
-  if (k < 1 || k > ctx->N || k > 16384)
-    return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 16384)");
+  if (k < 1 || k > ctx->N || k > 65536)
+    return set_error(ctx, MLFF_ERR_ARG, "pivoted Cholesky rank k must satisfy 1 <= k <= min(N, 65536)");
   const auto t0 = std::chrono::steady_clock::now();
   ctx->precon_kind = MLFF_PRECON_NONE;
   MLFF_TRY(alloc_panel(ctx, k));

@@ -20,8 +20,10 @@ __global__ __launch_bounds__(256) void k_gemm(int64_t M, int64_t N, int64_t K, d
                                               const double *__restrict__ A, int64_t lda,
                                               const double *__restrict__ B, int64_t ldb,
                                               double beta, double *__restrict__ C, int64_t ldc,
-                                              int64_t kchunk, int64_t slab_stride) {
+                                              int64_t kchunk, int64_t slab_stride, int tri) {
   constexpr int BM = 64, BN = 64, BK = 16;
+  // tri: only the tiles touching the lower triangle (a symmetric product, mirrored after)
+  if (tri && (int64_t)blockIdx.x * BN >= (int64_t)blockIdx.y * BM + BM) return;
   __shared__ double As[BK][BM + 1];
   __shared__ double Bs[BK][BN + 1];
   const int tid = threadIdx.x;
@@ -100,8 +102,9 @@ __global__ __launch_bounds__(NTH) void k_gemm_mfma(int64_t M, int64_t N, int64_t
                                                    const double *__restrict__ B, int64_t ldb,
                                                    double beta, double *__restrict__ C,
                                                    int64_t ldc, int64_t kchunk,
-                                                   int64_t slab_stride) {
+                                                   int64_t slab_stride, int tri) {
   constexpr int BN = 128, BK = 16, LP = 144;
+  if (tri && (int64_t)blockIdx.x * BN >= (int64_t)blockIdx.y * BM + BM) return;
   constexpr int WR = NTH / 128;        // wave rows (two wave columns of 64)
   constexpr int IM = BM / WR / 16, JN = 4;  // 16 x 16 blocks per wave
   static_assert(IM >= 1, "tile too small for the wave grid");
@@ -188,20 +191,20 @@ template <int BM, int NTH>
 static void gemm_mfma_launch_t(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                                const double *A, int64_t lda, const double *B, int64_t ldb,
                                double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
-                               int64_t slab_stride, hipStream_t s) {
+                               int64_t slab_stride, hipStream_t s, int tri) {
   dim3 grid((unsigned)((Nc + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
   if (!ta && !tb)
     hipLaunchKernelGGL((k_gemm_mfma<BM, false, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
-                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (!ta && tb)
     hipLaunchKernelGGL((k_gemm_mfma<BM, false, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
-                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (ta && !tb)
     hipLaunchKernelGGL((k_gemm_mfma<BM, true, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
-                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else
     hipLaunchKernelGGL((k_gemm_mfma<BM, true, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
-                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride);
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
 }
 
 // workgroup size of the matrix-core GEMM (MLFF_GEMM_NTH = 256 / 512 for A/B sweeps)
@@ -217,13 +220,13 @@ template <int BM>
 static void gemm_mfma_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                              const double *A, int64_t lda, const double *B, int64_t ldb,
                              double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
-                             int64_t slab_stride, hipStream_t s) {
+                             int64_t slab_stride, hipStream_t s, int tri) {
   if (gemm_nth() == 512)
     gemm_mfma_launch_t<BM, 512>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
-                                splits, slab_stride, s);
+                                splits, slab_stride, s, tri);
   else
     gemm_mfma_launch_t<BM, 256>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
-                                splits, slab_stride, s);
+                                splits, slab_stride, s, tri);
 }
 
 // the matrix-core path for every GEMM at least 64 x 128 with a K of 32 or more
@@ -238,32 +241,33 @@ static bool use_mfma(int64_t M, int64_t Nc, int64_t Kd) {
 
 static void gemm_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                         const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
-                        double *C, int64_t ldc, int splits, int64_t slab_stride, hipStream_t s) {
+                        double *C, int64_t ldc, int splits, int64_t slab_stride, hipStream_t s,
+                        int tri = 0) {
   if (M <= 0 || Nc <= 0) return;
   int64_t kchunk = (Kd + splits - 1) / splits;
   kchunk = round_up(kchunk < 1 ? 1 : kchunk, 16);
   if (use_mfma(M, Nc, Kd)) {
     if (M >= 128)
       gemm_mfma_launch<128>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, splits,
-                            slab_stride, s);
+                            slab_stride, s, tri);
     else
       gemm_mfma_launch<64>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk, splits,
-                           slab_stride, s);
+                           slab_stride, s, tri);
     return;
   }
   dim3 grid((unsigned)((Nc + 63) / 64), (unsigned)((M + 63) / 64), (unsigned)splits);
   if (!ta && !tb)
     hipLaunchKernelGGL((k_gemm<false, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
-                       ldb, beta, C, ldc, kchunk, slab_stride);
+                       ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (!ta && tb)
     hipLaunchKernelGGL((k_gemm<false, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
-                       ldb, beta, C, ldc, kchunk, slab_stride);
+                       ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (ta && !tb)
     hipLaunchKernelGGL((k_gemm<true, false>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
-                       ldb, beta, C, ldc, kchunk, slab_stride);
+                       ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else
     hipLaunchKernelGGL((k_gemm<true, true>), grid, dim3(256), 0, s, M, Nc, Kd, alpha, A, lda, B,
-                       ldb, beta, C, ldc, kchunk, slab_stride);
+                       ldb, beta, C, ldc, kchunk, slab_stride, tri);
 }
 
 void launch_gemm(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
@@ -287,20 +291,36 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
   return gram_wide(ctx, W, W, k, ncols, ldw, G);
 }
 
+// G[j, i] = G[i, j] for i > j (the lower triangle of a symmetric product mirrored up)
+__global__ __launch_bounds__(256) void k_mirror_lower(double *__restrict__ G, int64_t k) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < k * k;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t i = e / k, j = e % k;
+    if (j > i) G[e] = G[j * k + i];
+  }
+}
+
+// G = A B^T over ncols (k x k; A, B "wide" k x ncols panels).  A == B (a Gram matrix / SYRK):
+// only the tiles touching the lower triangle are computed and mirrored -- each entry is the
+// same sum in the same order either way, so G is bitwise what the full product gives
 int gram_wide(mlff_ctx *ctx, const double *A, const double *Bm, int64_t k, int64_t ncols,
               int64_t ldw, double *G) {
   const double *W = A;
+  const int tri = A == Bm ? 1 : 0;
   // workgroup tiles of the GEMM path taken (matrix cores: up to 128 x 128, VALU: 64 x 64)
   const int64_t tm = use_mfma(k, k, ncols) ? (k >= 128 ? 128 : 64) : 64;
   const int64_t tn = use_mfma(k, k, ncols) ? 128 : 64;
-  const int64_t tiles = ((k + tm - 1) / tm) * ((k + tn - 1) / tn);
+  int64_t tiles = ((k + tm - 1) / tm) * ((k + tn - 1) / tn);
+  if (tri) tiles = (tiles + (k + tm - 1) / tm) / 2;
   int64_t splits = (1024 + tiles - 1) / tiles;
   const int64_t max_splits = (ncols + 511) / 512;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   if (splits > 256) splits = 256;
+  const unsigned gm = (unsigned)std::min<int64_t>((k * k + 255) / 256, 4096);
   if (splits == 1) {
-    gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, Bm, ldw, 0.0, G, k, 1, 0, ctx->stream);
+    gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, Bm, ldw, 0.0, G, k, 1, 0, ctx->stream, tri);
+    if (tri) hipLaunchKernelGGL(k_mirror_lower, dim3(gm), dim3(256), 0, ctx->stream, G, k);
     MLFF_HIP(ctx, hipGetLastError());
     return MLFF_OK;
   }
@@ -308,10 +328,12 @@ int gram_wide(mlff_ctx *ctx, const double *A, const double *Bm, int64_t k, int64
   double *slabs = nullptr;
   MLFF_TRY(scratch_alloc(ctx, &slabs, splits * k * k));
   gemm_launch(false, true, k, k, ncols, 1.0, W, ldw, Bm, ldw, 0.0, slabs, k, (int)splits, k * k,
-              ctx->stream);
+              ctx->stream, tri);
   const int64_t n = k * k;
+  // (the skipped upper tiles of the slabs hold stale scratch; their sums are overwritten)
   hipLaunchKernelGGL(k_sum_slabs, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 2048)),
                      dim3(256), 0, ctx->stream, slabs, (int)splits, n, G);
+  if (tri) hipLaunchKernelGGL(k_mirror_lower, dim3(gm), dim3(256), 0, ctx->stream, G, k);
   MLFF_HIP(ctx, hipGetLastError());
   return MLFF_OK;
 }

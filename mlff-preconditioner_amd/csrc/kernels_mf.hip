@@ -36,8 +36,14 @@ namespace {
 
 constexpr int kIC = 16;  // training points per workgroup in the pair / F kernels
 // largest pair-record table of the single-column path (beyond it, columns run through the
-// whole operator as K_op e_i)
+// whole operator as K_op e_i): 2 GB, or 5 % of the device's memory if that is more (the
+// N = 505050 nanotube, M = 455, needs 3.7 GB)
 constexpr double kMfColTableBytes = 2.0e9;
+double col_table_cap() {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return kMfColTableBytes;
+  return std::max(kMfColTableBytes, 0.05 * (double)tot);
+}
 
 __device__ __forceinline__ int64_t xpos(int64_t g, int64_t rows_per, int64_t blk) {
   return (g / rows_per) * blk + g % rows_per;
@@ -571,7 +577,7 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
     MLFF_HIP(ctx, hipMalloc(&mf.kee, sizeof(double) * nic * M));
     MLFF_HIP(ctx, hipMalloc(&mf.eterm, sizeof(double) * nic * MP));
     launch_sgdml_kee(mf.Rd, M, D, mf.i0, mf.ni, mf.Pt, n_perms, sig, mf.kee, s);
-  } else if (mf.ni > 0 && col_bytes <= kMfColTableBytes) {
+  } else if (mf.ni > 0 && col_bytes <= col_table_cap()) {
     MLFF_HIP(ctx, hipMalloc(&mf.uvk, (size_t)col_bytes));
     MLFF_HIP(ctx, hipMalloc(&mf.pi_d, sizeof(int32_t) * n_perms * n));
     MLFF_HIP(ctx, hipMalloc(&mf.piinv_d, sizeof(int32_t) * n_perms * n));
