@@ -346,7 +346,12 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
                          const int *status, hipStream_t s, StopFold fold = StopFold{},
-                         int64_t cached_rows = 0, const long long *tcol = nullptr);
+                         int64_t cached_rows = 0, const long long *tcol = nullptr,
+                         const int *spec_hit = nullptr, int64_t spec_m0 = 0);
+// C (M x N) = op(A) op(B) with K split over enough workgroups to fill the chip, the slices
+// summed in a fixed order (deterministic); scratch from the context's arena
+int gemm_splitk(mlff_ctx *ctx, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const double *A,
+                int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc);
 int choose_ksplit(int64_t k, int64_t ncols);
 // leading rows of a k x ldt panel read with default-policy (MALL-resident) loads
 int64_t panel_cached_rows(int64_t k, int64_t ldt);

@@ -291,6 +291,41 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
   return gram_wide(ctx, W, W, k, ncols, ldw, G);
 }
 
+// C (M x N, ld ldc) = sum_s slab_s (M x N each, ld N), fixed slab order
+__global__ __launch_bounds__(256) void k_sum_slabs_ld(const double *__restrict__ slabs, int splits,
+                                                      int64_t M, int64_t N, double *__restrict__ C,
+                                                      int64_t ldc) {
+  const int64_t n = M * N;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    double a = 0.0;
+    for (int sp = 0; sp < splits; ++sp) a += slabs[(int64_t)sp * n + e];
+    C[(e / N) * ldc + e % N] = a;
+  }
+}
+
+int gemm_splitk(mlff_ctx *ctx, bool ta, bool tb, int64_t M, int64_t N, int64_t K, const double *A,
+                int64_t lda, const double *B, int64_t ldb, double *C, int64_t ldc) {
+  if (M <= 0 || N <= 0) return MLFF_OK;
+  const bool mf = use_mfma(M, N, K);
+  const int64_t tiles = ((M + (mf ? (M >= 128 ? 127 : 63) : 63)) / (mf ? (M >= 128 ? 128 : 64) : 64)) *
+                        ((N + (mf ? 127 : 63)) / (mf ? 128 : 64));
+  int64_t splits = std::min<int64_t>((512 + tiles - 1) / tiles, std::max<int64_t>(1, K / 256));
+  if (splits > 64) splits = 64;
+  if (splits <= 1) {
+    gemm_launch(ta, tb, M, N, K, 1.0, A, lda, B, ldb, 0.0, C, ldc, 1, 0, ctx->stream);
+    MLFF_HIP(ctx, hipGetLastError());
+    return MLFF_OK;
+  }
+  ScratchScope scope(ctx);
+  double *slabs = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &slabs, (size_t)(splits * M * N)));
+  gemm_launch(ta, tb, M, N, K, 1.0, A, lda, B, ldb, 0.0, slabs, N, (int)splits, M * N, ctx->stream);
+  hipLaunchKernelGGL(k_sum_slabs_ld, dim3((unsigned)std::min<int64_t>((M * N + 255) / 256, 4096)),
+                     dim3(256), 0, ctx->stream, slabs, (int)splits, M, N, C, ldc);
+  MLFF_HIP(ctx, hipGetLastError());
+  return MLFF_OK;
+}
+
 // G[j, i] = G[i, j] for i > j (the lower triangle of a symmetric product mirrored up)
 __global__ __launch_bounds__(256) void k_mirror_lower(double *__restrict__ G, int64_t k) {
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < k * k;

@@ -12,7 +12,16 @@
 // the pivot row L[m_pi, :m] an allreduce of a vector only its owner fills.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace mlff {
+
+// speculative blocks of the Schur GEMV (see k_spec_top_part)
+constexpr int kSpecB = 16;        // steps per speculative block
+constexpr int kSpecC = 64;        // candidates per block
+constexpr int kSpecGroups = 128;  // first-level groups of the candidate selection
+constexpr int kSpecPer = 4;       // candidates kept per group (512 to merge)
+constexpr int64_t kSpecMin = 64;  // no speculation before this many columns
 
 struct ArgMax {
   double v;
@@ -110,7 +119,9 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
                                                       double *__restrict__ xunit,
                                                       int64_t rows_per, int64_t blk,
                                                       DevState *st,
-                                                      int64_t *__restrict__ iperm) {
+                                                      int64_t *__restrict__ iperm,
+                                                      const int64_t *__restrict__ Cspec,
+                                                      int *__restrict__ spec_hit) {
   __shared__ double sv[256];
   __shared__ long long sp[256];
   __shared__ long long s_mpi;
@@ -169,6 +180,16 @@ __global__ __launch_bounds__(256) void k_piv_finalize(const double *__restrict__
     st->sqrt_piv = sq;
     s_mpi = mpi;
     s_sq = sq;
+    if (Cspec != nullptr) {  // speculation: is the pivot row one of the block's candidates?
+      const long long gl = mpi - row0;
+      int h = -1;
+      for (int j = 0; j < kSpecC && mpi >= 0; ++j)
+        if (Cspec[j] == gl) {
+          h = j;
+          break;
+        }
+      *spec_hit = h;
+    }
     if (xunit != nullptr && mpi >= 0) xunit[(mpi / rows_per) * blk + mpi % rows_per] = 1.0;
   }
   __syncthreads();
@@ -203,10 +224,15 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
                                                  const int64_t *__restrict__ iperm,
                                                  int64_t row0, int64_t N,
                                                  double *__restrict__ pv,
-                                                 long long *__restrict__ pp) {
+                                                 long long *__restrict__ pp,
+                                                 const double *__restrict__ Gspec,
+                                                 const int *__restrict__ spec_hit) {
   __shared__ double sv[256];
   __shared__ long long sp[256];
   const long long mpi = st->m_pi;
+  // speculation hit j: the Schur sum over the columns before the block is row j of Gspec
+  const int hitj = spec_hit != nullptr ? *spec_hit : -1;
+  const double *grow = hitj >= 0 ? Gspec + (int64_t)hitj * ldl : nullptr;
   if (mpi < 0) {  // no pivot (error already flagged): an empty candidate set
     if (threadIdx.x == 0) {
       pv[blockIdx.x] = -INFINITY;
@@ -234,6 +260,7 @@ __global__ __launch_bounds__(256) void k_piv_fin(const double *__restrict__ K, i
       for (int u = 0; u < 8; ++u) s0 += t[u];
     }
     for (; ks < ksplit; ++ks) s0 += part[(int64_t)ks * ldp + i];
+    if (grow != nullptr) s0 += grow[i];
     const double v = (col - s0) / sq;
     Lt[m * ldl + i] = v;
     const double dn = dwork[i] - v * v;
@@ -271,6 +298,137 @@ __global__ void k_unit_pivot(double *__restrict__ x, int64_t rows_per, int64_t b
   if (mpi >= 0) x[(mpi / rows_per) * blk + mpi % rows_per] = val;
 }
 
+// ---------------------------------------------------------------------------
+// Speculative blocks (one rank).  The Schur GEMV of step m reads L[:, :m] (m N 8 bytes):
+// summed over the build that is k^2 N 4 bytes (2.4 PB at the reference's N = 505050,
+// k = 34609).  At the start of a block of kSpecB steps the kSpecC rows with the largest
+// residual diagonal are the likely pivots of the block (measured on the golden systems:
+// 83-93 % of the block's pivots are among the top 2-4 x block-size candidates); one GEMM
+// G = L[C, :m0] L[:, :m0]^T reads L[:, :m0] once for all of them.  A step whose pivot is a
+// candidate adds its G row and runs the GEMV over the block's own columns [m0, m) only; any
+// other pivot runs the full GEMV.  Exact either way (a different summation order).
+
+// (v, i) before (w, j) in the candidate order: value descending, then row ascending; an
+// empty slot (i < 0) after everything
+__device__ __forceinline__ bool cand_before(double v, long long i, double w, long long j) {
+  if (i < 0) return false;
+  if (j < 0) return true;
+  return v > w || (v == w && i < j);
+}
+
+// best (value, row) over the 256 threads, broadcast to all of them
+__device__ __forceinline__ void block_best(double &v, long long &i, double *sv, long long *si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(v, o, 64);
+    const long long i2 = __shfl_xor(i, o, 64);
+    if (cand_before(v2, i2, v, i)) {
+      v = v2;
+      i = i2;
+    }
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sv[threadIdx.x >> 6] = v;
+    si[threadIdx.x >> 6] = i;
+  }
+  __syncthreads();
+  v = sv[0];
+  i = si[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (cand_before(sv[w], si[w], v, i)) {
+      v = sv[w];
+      i = si[w];
+    }
+}
+
+// top kSpecPer (value, row) of the non-pivoted rows of a chunk, in order (one workgroup per
+// chunk): round r takes the best row after round r - 1's pick
+__global__ __launch_bounds__(256) void k_spec_top_part(const double *__restrict__ dwork,
+                                                       const int *__restrict__ pivflag,
+                                                       int64_t nrows, double *__restrict__ cv,
+                                                       long long *__restrict__ ci) {
+  __shared__ double sv[4];
+  __shared__ long long si[4];
+  const int64_t cs = (nrows + gridDim.x - 1) / gridDim.x;
+  const int64_t a = (int64_t)blockIdx.x * cs, b = a + cs < nrows ? a + cs : nrows;
+  double pv = INFINITY;
+  long long pi = -1;
+  for (int r = 0; r < kSpecPer; ++r) {
+    double bv = -INFINITY;
+    long long bi = -1;
+    for (int64_t i = a + threadIdx.x; i < b; i += 256) {
+      if (pivflag[i]) continue;
+      const double v = dwork[i];
+      const bool later = pi < 0 || v < pv || (v == pv && i > pi);  // after the last pick
+      if (later && cand_before(v, i, bv, bi)) {
+        bv = v;
+        bi = i;
+      }
+    }
+    block_best(bv, bi, sv, si);
+    if (threadIdx.x == 0) {
+      cv[(int64_t)blockIdx.x * kSpecPer + r] = bv;
+      ci[(int64_t)blockIdx.x * kSpecPer + r] = bi;
+    }
+    if (bi < 0) {  // chunk exhausted
+      for (int r2 = r + 1 + threadIdx.x; r2 < kSpecPer; r2 += 256)
+        ci[(int64_t)blockIdx.x * kSpecPer + r2] = -1;
+      return;
+    }
+    pv = bv;
+    pi = bi;
+  }
+}
+
+// the block's candidates C[0..kSpecC): the best of the groups' kSpecGroups x kSpecPer picks,
+// by a bitonic sort of the 512 (value, row) pairs in LDS (one workgroup)
+__global__ __launch_bounds__(256) void k_spec_top_merge(const double *__restrict__ cv,
+                                                        const long long *__restrict__ ci,
+                                                        int64_t *__restrict__ C) {
+  constexpr int n = kSpecGroups * kSpecPer;
+  static_assert(n == 512, "two pairs per thread");
+  __shared__ double sv[n];
+  __shared__ long long si[n];
+  for (int t = threadIdx.x; t < n; t += 256) {
+    si[t] = ci[t];
+    sv[t] = si[t] >= 0 ? cv[t] : -INFINITY;
+  }
+  __syncthreads();
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n / 2; t += 256) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;  // this sub-sequence sorts best-first
+        const bool swap = up ? cand_before(sv[hi], si[hi], sv[lo], si[lo])
+                             : cand_before(sv[lo], si[lo], sv[hi], si[hi]);
+        if (swap) {
+          const double tv = sv[lo];
+          sv[lo] = sv[hi];
+          sv[hi] = tv;
+          const long long ti = si[lo];
+          si[lo] = si[hi];
+          si[hi] = ti;
+        }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x < kSpecC) C[threadIdx.x] = si[threadIdx.x];
+}
+
+// A[c, j] = Lt[c, C_j] for c < m0 (m0 x kSpecC, zero for an empty candidate)
+__global__ __launch_bounds__(256) void k_spec_gather(const double *__restrict__ Lt, int64_t ldl,
+                                                     int64_t m0, const int64_t *__restrict__ C,
+                                                     double *__restrict__ A) {
+  const int64_t n = m0 * kSpecC;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const int64_t c = e / kSpecC, j = e % kSpecC;
+    const int64_t g = C[j];
+    A[e] = g >= 0 ? Lt[c * ldl + g] : 0.0;
+  }
+}
+
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   hipStream_t s = ctx->stream;
   const int64_t N = ctx->N, nrows = ctx->nrows, blk = ctx->blk;
@@ -306,6 +464,26 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   }
   const int kmax_split = choose_ksplit(k, blk);
   MLFF_TRY(scratch_alloc(ctx, &part, kmax_split * blk));
+  // speculative blocks (one rank; MLFF_PIVCHOL_SPEC=0 disables for A/B)
+  static const bool spec_env = [] {
+    const char *e = std::getenv("MLFF_PIVCHOL_SPEC");
+    return e == nullptr || e[0] != '0';
+  }();
+  const bool spec = spec_env && ctx->world == 1 && k > kSpecMin + kSpecB &&
+                    nrows > (int64_t)kSpecGroups * kSpecPer;
+  double *Gspec = nullptr, *Aspec = nullptr, *cv = nullptr;
+  long long *ci = nullptr;
+  int64_t *Cspec = nullptr;
+  int *hit = nullptr;
+  if (spec) {
+    MLFF_TRY(scratch_alloc(ctx, &Gspec, (size_t)kSpecC * blk));
+    MLFF_TRY(scratch_alloc(ctx, &Aspec, (size_t)k * kSpecC));
+    MLFF_TRY(scratch_alloc(ctx, &cv, (size_t)kSpecGroups * kSpecPer));
+    MLFF_TRY(scratch_alloc(ctx, &ci, (size_t)kSpecGroups * kSpecPer));
+    MLFF_TRY(scratch_alloc(ctx, &Cspec, (size_t)kSpecC));
+    MLFF_TRY(scratch_alloc(ctx, &hit, 1));
+  }
+  int64_t spec_m0 = -1;  // start of the current speculative block (-1: none)
   MLFF_HIP(ctx, hipMemsetAsync(ctx->pivflag, 0, sizeof(int) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(ctx->T, 0, sizeof(double) * round_up(k, 8) * blk, s));
   MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->pivot_err, 0, sizeof(int), s));
@@ -333,6 +511,18 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                          ctx->row0, nrows, pv, pp);
       npc = np;
     }
+    if (spec && m >= kSpecMin && m % kSpecB == 0) {
+      // a new block: candidates from the residual diagonal after step m - 1, and the
+      // Schur sums of all of them over the columns [0, m) in one GEMM
+      spec_m0 = m;
+      hipLaunchKernelGGL(k_spec_top_part, dim3(kSpecGroups), dim3(256), 0, s, ctx->dwork,
+                         ctx->pivflag, nrows, cv, ci);
+      hipLaunchKernelGGL(k_spec_top_merge, dim3(1), dim3(256), 0, s, (const double *)cv,
+                         (const long long *)ci, Cspec);
+      hipLaunchKernelGGL(k_spec_gather, dim3((unsigned)std::min<int64_t>((m * kSpecC + 255) / 256, 4096)),
+                         dim3(256), 0, s, ctx->T, blk, m, Cspec, Aspec);
+      MLFF_TRY(gemm_splitk(ctx, true, false, kSpecC, blk, m, Aspec, kSpecC, ctx->T, blk, Gspec, blk));
+    }
     const bool multi = ctx->world > 1;
     if (multi) {
       double *my = wins + 2 * ctx->rank;
@@ -344,7 +534,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                        multi ? nullptr : (const double *)pv,
                        multi ? nullptr : (const long long *)pp, npc, ctx->perm, m, ctx->row0,
                        nrows, ctx->T, blk, ctx->pivflag, multi ? ctx->prow : nullptr, xunit,
-                       ctx->rows_per, blk, ctx->st, iperm);
+                       ctx->rows_per, blk, ctx->st, iperm, spec_m0 >= 0 ? Cspec : nullptr, hit);
     if (multi && m > 0) MLFF_TRY(comm_allreduce(ctx, ctx->prow, (size_t)m));
     if (rbfcols)
       launch_rbf_cols(ctx->rbf, N, ctx->row0, nrows, nullptr, 1, ctx->st, ctx->sigma_K, colbuf, blk, s);
@@ -353,17 +543,20 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     else if (mfcols)
       launch_mf_operator(ctx, ctx->xg, colbuf, nullptr, nullptr, ctx->sigma_K, 0.0);
     const int ks = m > 0 ? std::min(kmax_split, choose_ksplit(m, blk)) : 0;
-    // Schur column GEMV over L[:, :m]; the panel's leading rows (up to 128 MB) are read
-    // with default-policy loads so they stay in the MALL from one step to the next
+    const bool in_spec = spec_m0 >= 0;
+    // Schur column GEMV over L[:, :m] (on a speculation hit only over [spec_m0, m)); the
+    // panel's leading rows (up to 128 MB) are read with default-policy loads so they stay in
+    // the MALL from one step to the next
     if (ks > 0)
       launch_colgemv_part(ctx->T, blk, m, ctx->prow, 1, m, ks, part, nullptr, s, StopFold{},
                           panel_cached_rows(m, blk),
-                          multi ? nullptr : (const long long *)&ctx->st->m_pi);
+                          multi ? nullptr : (const long long *)&ctx->st->m_pi,
+                          in_spec ? hit : nullptr, in_spec ? spec_m0 : 0);
     if (gcol > 0)
       hipLaunchKernelGGL(k_piv_fin, dim3(gcol), dim3(256), 0, s, ctx->K, ctx->ld, ctx->sigma_K,
                        (const double *)colbuf, ctx->rows_per, blk, nrows, m, part, ks, blk,
                        ctx->T, blk, ctx->pivflag, ctx->dwork, ctx->st, xunit, iperm, ctx->row0, N,
-                       pv, pp);
+                       pv, pp, (const double *)Gspec, in_spec ? (const int *)hit : nullptr);
     else if (mfcols && !colpath)
       hipLaunchKernelGGL(k_unit_pivot, dim3(1), dim3(64), 0, s, ctx->xg, ctx->rows_per, blk,
                          ctx->st, 0.0);

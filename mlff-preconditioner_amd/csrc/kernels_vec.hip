@@ -279,12 +279,17 @@ __global__ __launch_bounds__(256) void k_colgemv_part(const double *__restrict__
                                                       int64_t kslice, double *__restrict__ part,
                                                       const int *__restrict__ status,
                                                       StopFold fold, int64_t cached_rows,
-                                                      const long long *__restrict__ tcol) {
+                                                      const long long *__restrict__ tcol,
+                                                      const int *__restrict__ spec_hit,
+                                                      int64_t spec_m0) {
   if (status != nullptr && *status != ST_RUNNING) return;
   extern __shared__ double t_sh[];
   if (!stop_prologue(fold, t_sh)) return;
-  const int64_t j0 = (int64_t)blockIdx.y * kslice;
+  int64_t j0 = (int64_t)blockIdx.y * kslice;
   const int64_t j1 = (j0 + kslice) < k ? (j0 + kslice) : k;
+  // pivoted-Cholesky speculation hit: the rows below spec_m0 are already summed (a GEMM at
+  // the block start); this slice keeps only its rows from spec_m0 on (zeros if none)
+  if (spec_hit != nullptr && *spec_hit >= 0 && j0 < spec_m0) j0 = spec_m0 < j1 ? spec_m0 : j1;
   if (tcol != nullptr) {  // t = column *tcol of W itself (the pivot row of L, one rank)
     const int64_t gc = *tcol < 0 ? 0 : (int64_t)*tcol;  // no pivot: the result is unused
     for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) t_sh[j - j0] = W[j * ldw + gc];
@@ -319,16 +324,16 @@ int choose_ksplit(int64_t k, int64_t ncols) {
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,
                          const int *status, hipStream_t s, StopFold fold, int64_t cached_rows,
-                         const long long *tcol) {
+                         const long long *tcol, const int *spec_hit, int64_t spec_m0) {
   const int64_t kslice = (k + ksplit - 1) / ksplit;
   const dim3 grid((unsigned)((ldw / 2 + 255) / 256), (unsigned)ksplit);
   const size_t shm = sizeof(double) * (kslice + 1 > 8 ? kslice + 1 : 8);
   if (panel_streams(k, ldw))
     hipLaunchKernelGGL(k_colgemv_part<true>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
-                       tstride, kslice, part, status, fold, cached_rows, tcol);
+                       tstride, kslice, part, status, fold, cached_rows, tcol, spec_hit, spec_m0);
   else
     hipLaunchKernelGGL(k_colgemv_part<false>, grid, dim3(256), shm, s, W, ldw, k, tsrc, tsplits,
-                       tstride, kslice, part, status, fold, cached_rows, tcol);
+                       tstride, kslice, part, status, fold, cached_rows, tcol, spec_hit, spec_m0);
 }
 
 // z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
