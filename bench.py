@@ -7,9 +7,13 @@
 Workload: synthetic SPD RBF kernel, x ~ U[0,1)^3 (numpy default_rng seed 0), length
 scale 0.2, A = K + 1e-6 I, b = sum(x^2), rank-256 Nystrom preconditioner on uniform
 random columns (`random_scores`, seed 0):
-  --gpus 1:  N = 65536  (BASELINE.json configs[2])
-  --gpus >1: N = 131072 (configs[3], "row-sharded mat-vec + RCCL, 8 x MI355X"): the same
-             problem at 2, 4 and 8 GPUs (strong scaling within configs[3]; --n overrides)
+  value:         N = 65536 (BASELINE.json configs[2]) on every
+                 --gpus N, so the driver's value_N / value_1 is the strong scaling of ONE
+                 problem (the north star's "N=64k 1-GPU ... >=6x strong scaling at 8 GPUs")
+  configs3_leg:  N = 131072 (configs[3], "row-sharded mat-vec + RCCL, 8 x MI355X") timed
+                 the same way on the same ranks, at N = 1 as well (68.7 GB of tiles fit one
+                 GPU), so configs[3]'s own 1 -> 8 GPU speed-up is the ratio
+                 of this leg's values across the BENCH / SCALE lines (--configs3-n 0 skips)
 K is generated on the GPU straight into the symmetric tiles from the points (inputs
 resident in HBM before the timed region; no dense N x N copy).  A step = one PCG
 iteration (the fp64 mat-vec over the whole N x N matrix + preconditioner apply + CG
@@ -61,15 +65,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=None,
-                    help="kernel size (default 65536 = configs[2] on one GPU, 131072 = "
-                         "configs[3] on several)")
+                    help="kernel size of `value` (default 65536 = configs[2], on any number "
+                         "of GPUs)")
     ap.add_argument("--k", type=int, default=None,
                     help="preconditioner rank (rbf: 256; sGDML: the rule of thumb, e.g. 2701 "
                          "for the nanotube; configs[4] uses 1024)")
-    ap.add_argument("--strong-n", type=int, default=65536,
-                    help="with several GPUs and the rbf workload, also time this size (the "
-                         "one-GPU configs[2] size) for a like-for-like strong-scaling number; "
-                         "0 skips it")
+    ap.add_argument("--configs3-n", type=int, default=131072,
+                    help="rbf workload: also time this size (configs[3], N = 131072) on the "
+                         "same ranks (configs3_leg); 0 skips it")
     ap.add_argument("--lam", type=float, default=1e-6)
     ap.add_argument("--ell", type=float, default=0.2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -361,11 +364,10 @@ def precon_rbf(solver, idx) -> float:
     return solver.precon_nystrom(idx, variant=0)
 
 
-def strong_leg(args, rank, world, local, pg, n, k, lam, ell):
+def size_leg(args, rank, world, local, pg, n, k, lam, ell):
     """Iterations/s of the rbf workload at size n on all ranks (same generator, Nystrom rank,
-    storage and timing as the main leg): with n = 65536 the same problem as the one-GPU
-    line, so value_N / value_1 is a strong-scaling ratio even though the multi-GPU `value`
-    is quoted on configs[3] (N = 131072)."""
+    storage and timing as the main leg; no solve, no CPU leg): configs[3] (n = 131072) next
+    to the configs[2] `value`, so each bench line carries both problems' numbers."""
     from sgdml_amd import synthetic
 
     X, b = synthetic.rbf_points(n, 3, 0)
@@ -393,6 +395,8 @@ def strong_leg(args, rank, world, local, pg, n, k, lam, ell):
         op_ms = max_over_ranks(pg, tm["gemv_ms"] / max(tm["gemv_count"], 1))
         return {"n": n, "k": k, "value": args.steps / el, "ms_per_step": el / args.steps * 1e3,
                 "operator_ms_max_rank": op_ms,
+                "operator_gbs_max_rank": op_bytes / (op_ms * 1e-3) / 1e9,
+                "operator_bytes_rank": op_bytes,
                 "rccl_ms_per_iter": max_over_ranks(pg, tm["comm_ms"] / max(tm["iter_count"], 1))}
     finally:
         s.close()
@@ -456,7 +460,7 @@ def main():
     from sgdml_amd import synthetic
 
     if args.n is None:
-        args.n = 65536 if world == 1 else 131072
+        args.n = 65536
     n, k, lam, ell = args.n, (args.k or 256), args.lam, args.ell
     sg_info = None
     if args.workload == "rbf":
@@ -611,15 +615,18 @@ def main():
                             storage_pack=t_pack),
         }
     solver.close()
-    if world > 1 and args.workload == "rbf" and args.strong_n and args.strong_n != n:
+    if args.workload == "rbf" and args.configs3_n and args.configs3_n != n:
         try:
-            strong = strong_leg(args, rank, world, local, pg, args.strong_n, k, lam, ell)
-        except Exception as e:  # the configs[3] line above must still be printed
-            strong = {"n": args.strong_n, "value": None, "error": repr(e)}
+            leg = size_leg(args, rank, world, local, pg, args.configs3_n, k, lam, ell)
+        except Exception as e:  # the configs[2] line above must still be printed
+            leg = {"n": args.configs3_n, "value": None, "error": repr(e)}
         if out is not None:
-            out["strong_scaling_leg"] = dict(strong, baseline_config="configs[2]", note=(
-                "the one-GPU line's problem on all ranks: compare its value with BENCH at "
-                "N=1 for strong scaling; `value` above is configs[3] (N=131072)"))
+            out["configs3_leg"] = dict(leg, baseline_config=(
+                "configs[3]" if args.configs3_n == 131072 else None),
+                n_gpus=world, scaling="strong", note=(
+                    "the configs[3] problem on the same ranks: its value at N GPUs over its "
+                    "value in the N=1 bench line is configs[3]'s strong scaling (BASELINE.md "
+                    "2: >=6x at 8 GPUs); `value` above is configs[2] (N=65536) on N GPUs"))
     if out is not None:
         print(json.dumps(out), flush=True)
     if pg is not None:

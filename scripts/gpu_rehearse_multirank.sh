@@ -1,6 +1,6 @@
 #!/bin/bash
 # One-GPU rehearsal of the multi-rank bench flow (torchrun, W processes, SOLO library ranks,
-# gloo): exercises bench.py's distributed logic (configs[3] size, strong-scaling leg, RCCL /
+# gloo): exercises bench.py's distributed logic (configs[2] value, configs[3] leg, RCCL /
 # memory fields, max-over-ranks timing, the single JSON line) -- not RCCL, not a measurement.
 set -u
 mkdir -p gpurun_out
