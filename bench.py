@@ -518,13 +518,14 @@ def main():
                "traffic": pmc_traffic(workload, storage, world),
                "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
                           "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
-                          "matfree": "k_mf_pair (+Zt) + k_mf_pair_fin + k_mf_h + k_mf_jt + k_mf_jt_fin "
-                                     "(matrix-free sGDML operator)"}.get(storage, storage),
+                          "matfree": "k_rec_g + k_rec_fin (record-factored matrix-free sGDML "
+                                     "operator; k_mf_* when the pair records exceed their cap)"}
+               .get(storage, storage),
                "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
     if storage == "matfree":
-        roof_op["note"] = ("five dependent launches (pair sums, their finish, F, J^T F, finish): "
-                           "at the nanotube's M = 14 neither HBM- nor FP64-bound (PMC traffic "
-                           "and L2 hit rates in profiles/pmc_traffic.json; DESIGN.md 3.2)")
+        roof_op["note"] = ("two dependent launches (Zt, G = sum w Zt and J^T G of a pair block in one "
+                           "workgroup; the finisher): ~33 MB per application at M = 14, latency- "
+                           "not HBM-bound (PMC traffic in profiles/pmc_traffic.json; DESIGN.md 3.2)")
     # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials
     roof_pre = None
     if tm.get("precon_count"):

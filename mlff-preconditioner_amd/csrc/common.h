@@ -92,6 +92,14 @@ struct MfData {
   // whole operator)
   double *uvk = nullptr;
   int32_t *pi_d = nullptr, *piinv_d = nullptr;
+  // record-factored operator (kernels_mf.hip k_rec_g / k_rec_fin), used when uvk exists:
+  // wt = w transposed ((M n_perms) x ni), sv = the per-application pair scalars
+  // 5 m (v . x_j) (ni x M n_perms), rpart = J^T G partial rows of every pair block
+  // (rblk slots x ni x 3n)
+  bool rec = false;
+  int rblk = 0;
+  int64_t ldw = 0;
+  double *wt = nullptr, *sv = nullptr, *rpart = nullptr;
   // energy constraints (use_E_cstr, train.py:212-236; iterative_solver.py:423-440): the
   // operand and result carry M energy entries after the nF = 3 n M force entries (one rank)
   bool E = false;

@@ -498,6 +498,350 @@ __global__ void k_mf_ediag(const double *__restrict__ kee, int64_t M, double *__
   if (i < M) out[i] = -kee[i * M + i];
 }
 
+// ---------------------------------------------------------------------------
+// Record-factored operator.  With the x-independent pair records of the single-column
+// path (k_sgdml_uv, mirror = 0: u = J_i^T diff, v = J_j^T P_p^T diff, m, w per (i, j, p))
+// the reference's K_op (predict.py:172-220 with alphas = x) regroups exactly as
+//   c_ijp = 5 m (diff . Zt_jp) = 5 m (v_ijp . x_j)
+//   y_i   = J_i^T sum_jp (c diff - w Zt_jp) = sum_jp c_ijp u_ijp - J_i^T G_i,
+//   G_i   = sum_jp w_ijp Zt_jp,   Zt_jp = (J_j x_j)[P_p]
+// so the two full-descriptor (O(M^2 D)) reductions of the pair sums and the F pass
+// become one: G, a w-weighted sum of Zt, which k_rec_g forms on the fly (Zt from Rdd
+// and x, never stored) and contracts with J_i^T inside the same workgroup.  Two launches:
+//   k_rec_g    workgroup per (16 x 16 atom pair block (A >= B), 16 query points): Zt of the
+//              block's pairs for every (j, p), G of its points, J_i^T G partial rows into
+//              slot B (atoms of A) and slot A (atoms of B); extra workgroups: the pair
+//              scalars s_ijp = 5 m (v . x_j), one wave each
+//   k_rec_fin  y = sigma (sum_jp s u - sum_slots) + lam x (+ the p.q partials of the step)
+// Rounding: a regrouping of the same products (the noise-band check of this form on all
+// golden solves is in DESIGN.md 3.2).
+constexpr int kRB = 16;  // atoms per edge of a pair block
+constexpr int kRG = 16;  // query points per workgroup (G accumulators per thread)
+constexpr int kRJ = 8;   // (j, p) per batch of Zt loads
+constexpr int kWC = 32;  // (j, p) per chunk of w staged in LDS
+static_assert(kRG % kRJ == 0 && kWC % kRJ == 0, "batches tile the point groups and chunks");
+
+// Zt_jp[d] = (J_j x_j)[P_p d] (z_entry, general permutation)
+__device__ __forceinline__ double rec_zt(const double *__restrict__ Rdd,
+                                         const double *__restrict__ xc,
+                                         const int32_t *__restrict__ Pt,
+                                         const int32_t *__restrict__ ps,
+                                         const int32_t *__restrict__ pt, int64_t D, int n,
+                                         int64_t j, int p, int64_t d) {
+  const int64_t e = Pt[(int64_t)p * D + d];
+  const int s = ps[e], t = pt[e];
+  const double *r = Rdd + (j * D + e) * 3;
+  const double *xj = xc + j * 3 * (int64_t)n;
+  double z = 0.0;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) z = fma(r[c], xj[3 * t + c] - xj[3 * s + c], z);
+  return z;
+}
+
+struct RecArgs {
+  const double *Rdd;   // M x D x 3
+  const double *xc;    // contiguous operand (global index)
+  const int32_t *Pt;   // n_perms x D
+  const int32_t *ps, *pt;
+  const double *uvk;   // records, ni x M x n_perms x (6 n + 2)
+  int64_t M, D, i0, ni, MP;
+  int64_t ldw;         // row length of wt (ngrp kRG, zero padded)
+  int n, n_perms, nblk;
+  double *rpart;       // nblk x ni x 3n
+  double *sv;          // ni x MP
+};
+
+// wt: w transposed, round_up(MP, kRJ) rows of ldw = ngrp kRG entries, zero padded, so
+// the accumulation runs unguarded over whole batches and point groups
+// grid: nsw8 pair-scalar workgroups first (dispatched first, off the tail), then the
+// pair blocks
+template <bool IDENT>
+__global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
+                                               int64_t nbp, int64_t ngrp, int64_t nsw8,
+                                               const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double red[8][3][kRB][kRB + 1];
+  __shared__ double sW[kWC][kRG];
+  const int tid = threadIdx.x;
+  const int n3 = 3 * a.n;
+  if ((int64_t)blockIdx.x < nsw8) {  // pair scalars: one wave per (local point, j, p)
+    const int64_t q = (int64_t)blockIdx.x * 4 + (tid >> 6);
+    if (q >= a.ni * a.MP) return;
+    const int64_t il = q / a.MP, jp = q % a.MP, j = jp / a.n_perms;
+    const double *vv = a.uvk + q * (int64_t)(6 * a.n + 2) + n3;
+    const double *xj = a.xc + j * n3;
+    double acc = 0.0;
+    int t = tid & 63;
+    for (; t + 7 * 64 < n3; t += 8 * 64) {  // 16 loads in flight, summed in t order
+      double va[8], xa[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        va[u] = vv[t + u * 64];
+        xa[u] = xj[t + u * 64];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = fma(va[u], xa[u], acc);
+    }
+    for (; t < n3; t += 64) acc = fma(vv[t], xj[t], acc);
+    acc = wave_sum(acc);
+    if ((tid & 63) == 0) a.sv[il * a.MP + jp] = 5.0 * vv[3 * a.n] * acc;  // 5 m (v . x_j)
+    return;
+  }
+  // XCD-aware order: the point groups of one pair block run on one XCD (workgroup L on
+  // XCD L mod 8), so they share its L2 for the block's Rdd / x lines
+  const int64_t wg = (int64_t)blockIdx.x - nsw8;
+  const int64_t slot = wg / 8, grp = slot % ngrp;
+  const int64_t bp = (slot / ngrp) * 8 + wg % 8;
+  if (bp >= nbp) return;
+  int A = (int)((sqrt(8.0 * (double)bp + 1.0) - 1.0) * 0.5);
+  while ((int64_t)A * (A + 1) / 2 > bp) --A;
+  while ((int64_t)(A + 1) * (A + 2) / 2 <= bp) ++A;
+  const int B = (int)(bp - (int64_t)A * (A + 1) / 2);
+  const int la = tid >> 4, lb = tid & 15;
+  const int aa = A * kRB + la, bb = B * kRB + lb;
+  const bool valid = aa < a.n && bb < a.n && aa > bb;
+  const int64_t d = valid ? (int64_t)aa * (aa - 1) / 2 + bb : 0;
+  // batch slots beyond the last (j, p) and lanes without a pair load in-bounds stand-ins
+  // (d = 0, the last j) unconditionally, so no branch separates a batch's loads
+  const int64_t g0 = grp * kRG;
+  const int ng = (int)((a.ni - g0) < kRG ? (a.ni - g0) : kRG);
+  double acc[kRG];
+#pragma unroll
+  for (int k = 0; k < kRG; ++k) acc[k] = 0.0;
+  const double *wp = wt + g0;
+  const int64_t MPp = (a.MP + kRJ - 1) / kRJ * kRJ;  // rows of wt
+  const int64_t rs = 3 * a.D;
+  const double *rj = a.Rdd + d * 3;
+  // identity: x of the chunk's points at the block's 2 x 16 atoms, staged in LDS (in the
+  // space of the epilogue's reduction buffer), so a batch loads only its Rdd rows
+  double *sx = &red[0][0][0][0];  // [kWC][2][kRB][3]
+  // one identity permutation, point groups aligned to the batches: the query points are
+  // training points j = i0 + g0 + k, so their Rdd rows pass through the batches and are
+  // kept for the epilogue instead of being read a second time
+  double rg[kRG][3];
+#pragma unroll
+  for (int k = 0; k < kRG; ++k) rg[k][0] = rg[k][1] = rg[k][2] = 0.0;
+  const bool capture = IDENT && a.i0 % kRJ == 0;
+  static_assert(8 * 3 * kRB * (kRB + 1) >= kWC * 2 * kRB * 3, "x stage fits in red");
+  int64_t jn = 0;  // general permutations: (j, p) of the next batch slot
+  int pn = 0;
+  for (int64_t c0 = 0; c0 < MPp; c0 += kWC) {
+    // w of the chunk's (j, p) for the group's points, LDS broadcast operands
+    const int cn = (int)((MPp - c0) < kWC ? (MPp - c0) : kWC);
+    // (every thread's staging loads issued together, then stored)
+    constexpr int kWL = kWC * kRG / 256, kXL = kWC * 2 * kRB * 3 / 256;
+    double wl[kWL], xl[IDENT ? kXL : 1];
+#pragma unroll
+    for (int q = 0; q < kWL; ++q) {
+      const int e = tid + q * 256;
+      wl[q] = e < cn * kRG ? wp[(c0 + e / kRG) * a.ldw + e % kRG] : 0.0;
+    }
+    if (IDENT) {
+#pragma unroll
+      for (int q = 0; q < kXL; ++q) {
+        const int e = tid + q * 256;
+        const int jj = e / (2 * kRB * 3), r = e % (2 * kRB * 3);
+        const int atom = (r < kRB * 3 ? A : B) * kRB + (r % (kRB * 3)) / 3;
+        const int64_t j = c0 + jj;
+        xl[q] = (jj < cn && j < a.MP && atom < a.n) ? a.xc[j * n3 + 3 * atom + r % 3] : 0.0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kWL; ++q) (&sW[0][0])[tid + q * 256] = wl[q];
+    if (IDENT) {
+#pragma unroll
+      for (int q = 0; q < kXL; ++q) sx[tid + q * 256] = xl[q];
+    }
+    __syncthreads();
+    for (int jb = 0; jb < cn; jb += kRJ) {
+      double z[kRJ];
+      if (IDENT) {
+        // Zt_j[d] = sum_c Rdd_j[d, c] (x_j[bb, c] - x_j[aa, c])  (z_entry, s = aa, t = bb)
+        double rv[kRJ][3];
+#pragma unroll
+        for (int u = 0; u < kRJ; ++u) {
+          const int64_t j = c0 + jb + u, jc = j < a.MP ? j : a.MP - 1;
+          const double *r = rj + jc * rs;
+          rv[u][0] = r[0];
+          rv[u][1] = r[1];
+          rv[u][2] = r[2];
+        }
+        asm volatile("" ::: "memory");  // the batch's loads are issued together
+        if (capture) {
+          const int64_t off = c0 + jb - (a.i0 + g0);
+#pragma unroll
+          for (int h = 0; h < kRG / kRJ; ++h)
+            if (off == h * kRJ) {
+#pragma unroll
+              for (int u = 0; u < kRJ; ++u) {
+                rg[h * kRJ + u][0] = rv[u][0];
+                rg[h * kRJ + u][1] = rv[u][1];
+                rg[h * kRJ + u][2] = rv[u][2];
+              }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kRJ; ++u) {
+          const double *xs = sx + (jb + u) * (2 * kRB * 3);
+          double zz = 0.0;
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            zz = fma(rv[u][c], xs[kRB * 3 + lb * 3 + c] - xs[la * 3 + c], zz);
+          z[u] = (valid && c0 + jb + u < a.MP) ? zz : 0.0;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < kRJ; ++u) {
+          const bool ok = valid && jn < a.M;
+          const double zz = rec_zt(a.Rdd, a.xc, a.Pt, a.ps, a.pt, a.D, a.n,
+                                   jn < a.M ? jn : a.M - 1, pn, d);
+          z[u] = ok ? zz : 0.0;
+          if (++pn == a.n_perms) {
+            pn = 0;
+            ++jn;
+          }
+        }
+      }
+      // the w reads of one (j, p) at a time (hoisting all 8 x 16 of them costs 256 VGPRs)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < kRJ; ++u) {
+#pragma unroll
+        for (int k = 0; k < kRG; ++k) acc[k] = fma(sW[jb + u][k], z[u], acc[k]);
+        asm volatile("" ::: "memory");
+      }
+    }
+  }
+  // J_i^T G over the block: pair d = (s = aa, t = bb), J[d, t] = +Rdd, J[d, s] = -Rdd;
+  // the query points' Rdd rows are loaded together (one round trip), mostly L2 hits
+  const int64_t pstride = a.ni * n3;
+#pragma unroll
+  for (int k = 0; k < kRG; ++k) {
+    if (!capture && k < ng && valid) {
+      const double *r = a.Rdd + ((a.i0 + g0 + k) * a.D + d) * 3;
+      rg[k][0] = r[0];
+      rg[k][1] = r[1];
+      rg[k][2] = r[2];
+    }
+  }
+#pragma unroll
+  for (int k0 = 0; k0 < kRG; k0 += 8) {
+    if (k0 >= ng) break;
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = k0 + kk;
+      red[kk][0][la][lb] = rg[k][0] * acc[k];
+      red[kk][1][la][lb] = rg[k][1] * acc[k];
+      red[kk][2][la][lb] = rg[k][2] * acc[k];
+    }
+    __syncthreads();
+    // 8 points x (rows of A | columns of B) x 16 atoms x 3 components
+    for (int e = tid; e < 8 * 2 * kRB * 3; e += 256) {
+      const int kk = e / (2 * kRB * 3), rem = e % (2 * kRB * 3);
+      const int side = rem / (kRB * 3), q = rem % (kRB * 3);
+      const int ao = q / 3, c = q % 3;
+      if (k0 + kk >= ng) continue;
+      if (side == 1 && A == B) continue;  // the diagonal block's columns join its rows
+      double v = 0.0;
+      int atom, sl;
+      if (side == 0) {
+        double rs = 0.0;
+#pragma unroll
+        for (int x = 0; x < kRB; ++x) rs += red[kk][c][ao][x];
+        v = -rs;
+        if (A == B) {
+          double cs = 0.0;
+#pragma unroll
+          for (int x = 0; x < kRB; ++x) cs += red[kk][c][x][ao];
+          v += cs;
+        }
+        atom = A * kRB + ao;
+        sl = B;
+      } else {
+        double cs = 0.0;
+#pragma unroll
+        for (int x = 0; x < kRB; ++x) cs += red[kk][c][x][ao];
+        v = cs;
+        atom = B * kRB + ao;
+        sl = A;
+      }
+      if (atom < a.n) a.rpart[sl * pstride + (g0 + k0 + kk) * n3 + 3 * atom + c] = v;
+    }
+  }
+}
+
+// rows of this rank: y = sigma (sum_jp s_ijp u_ijp[t] - sum_slots J^T G) + lam x;
+// PQ: the x . y partials of the CG step on the kVecGrid layout (as k_mf_jt_fin).
+// 2^lg lanes per row (a lane sums every 2^lg-th term of both series, then a butterfly
+// over the group: every lane of it holds the same bits), so the few rows of a small
+// system still spread over the whole grid.
+template <bool PQ>
+__global__ __launch_bounds__(256) void k_rec_fin(const double *__restrict__ uvk,
+                                                 const double *__restrict__ sv,
+                                                 const double *__restrict__ rpart, int nblk,
+                                                 int64_t MP, int n, int64_t i0, int64_t ni,
+                                                 int64_t row0, int64_t nrows, double sigma,
+                                                 double lam, const double *__restrict__ xloc,
+                                                 double *__restrict__ y,
+                                                 double *__restrict__ pq_part, int lg,
+                                                 const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[8];
+  const int64_t n3 = 3 * (int64_t)n, stride = 6 * (int64_t)n + 2, pstride = ni * n3;
+  const int G = 1 << lg, sub = threadIdx.x & (G - 1);
+  const int64_t pass = (int64_t)gridDim.x * (256 >> lg);
+  double pq = 0.0;
+  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> lg; r < nrows; r += pass) {
+    const int64_t g = row0 + r, i = g / n3, t = g - i * n3, il = i - i0, pr = il * n3 + t;
+    const double *u = uvk + il * MP * stride + t;
+    const double *s = sv + il * MP;
+    double acc = 0.0, sl = 0.0;
+    int64_t jp = sub;
+    for (; jp + 3 * G < MP; jp += 4 * G) {
+      double uu[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) uu[q] = u[(jp + q * G) * stride];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = fma(s[jp + q * G], uu[q], acc);
+    }
+    for (; jp < MP; jp += G) acc = fma(s[jp], u[jp * stride], acc);
+    int q = sub;
+    for (; q + 3 * G < nblk; q += 4 * G) {
+      double pp[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pp[e] = rpart[(q + e * G) * pstride + pr];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sl += pp[e];
+    }
+    for (; q < nblk; q += G) sl += rpart[q * pstride + pr];
+    for (int m = G >> 1; m > 0; m >>= 1) {
+      acc += __shfl_xor(acc, m, G);
+      sl += __shfl_xor(sl, m, G);
+    }
+    if (sub == 0) {
+      double yv = sigma * (acc - sl);
+      if (xloc != nullptr) yv += lam * xloc[r];
+      y[r] = yv;
+      if (PQ) pq = fma(xloc[r], yv, pq);
+    }
+  }
+  if (PQ) {
+    const double t = block_sum256(pq, sh);
+    if (threadIdx.x == 0) pq_part[blockIdx.x] = t;
+  }
+}
+
+// w of the records, transposed for k_rec_g's point-group loads (ldw-long rows, the
+// padding zeroed beforehand)
+__global__ void k_rec_wt(const double *__restrict__ uvk, int64_t ni, int64_t MP, int n,
+                         int64_t ldw, double *__restrict__ wt) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= ni * MP) return;
+  wt[(e % MP) * ldw + e / MP] = uvk[e * (6 * (int64_t)n + 2) + 6 * n + 1];
+}
+
 }  // namespace
 
 int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
@@ -586,6 +930,20 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
                                  hipMemcpyHostToDevice, s));
     launch_sgdml_records(mf.Rd, mf.Rdd, M, n, D, mf.i0, mf.ni, mf.Pt, mf.piinv_d, n_perms, sig,
                          mf.uvk, s);
+    // the record-factored operator (MLFF_MF_REC=0: the five-kernel pair/F/J^T path)
+    const char *ev = std::getenv("MLFF_MF_REC");
+    if (ev == nullptr || std::atoi(ev) != 0) {
+      mf.rblk = (n + kRB - 1) / kRB;
+      mf.ldw = round_up(mf.ni, kRG);
+      const int64_t wrows = round_up(MP, kRJ);
+      MLFF_HIP(ctx, hipMalloc(&mf.wt, sizeof(double) * wrows * mf.ldw));
+      MLFF_HIP(ctx, hipMemsetAsync(mf.wt, 0, sizeof(double) * wrows * mf.ldw, s));
+      MLFF_HIP(ctx, hipMalloc(&mf.sv, sizeof(double) * MP * mf.ni));
+      MLFF_HIP(ctx, hipMalloc(&mf.rpart, sizeof(double) * mf.rblk * mf.ni * n3));
+      hipLaunchKernelGGL(k_rec_wt, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0, s,
+                         mf.uvk, mf.ni, MP, n, mf.ldw, mf.wt);
+      mf.rec = true;
+    }
   }
   if (mf.ni > 0) {
     hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)((MP + kPT - 1) / kPT),
@@ -620,6 +978,34 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     if (pq_part != nullptr)  // zero partials of an empty shard
       hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js,
                          (int64_t)0, sigma, lam, x_loc, y_loc, pq_part, status);
+    return;
+  }
+  if (mf.rec) {
+    const RecArgs ra{mf.Rdd, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni, MP,
+                     mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
+    const int64_t nbp = (int64_t)mf.rblk * (mf.rblk + 1) / 2, ngrp = (mf.ni + kRG - 1) / kRG;
+    const int64_t nbp8 = (nbp + 7) / 8 * 8, nsw8 = (mf.ni * MP + 31) / 32 * 8;
+    const dim3 grid((unsigned)(nsw8 + nbp8 * ngrp));
+    if (mf.ident)
+      hipLaunchKernelGGL(k_rec_g<true>, grid, dim3(256), 0, s, ra, (const double *)mf.wt, nbp, ngrp,
+                         nsw8, status);
+    else
+      hipLaunchKernelGGL(k_rec_g<false>, grid, dim3(256), 0, s, ra, (const double *)mf.wt, nbp,
+                         ngrp, nsw8, status);
+    // lanes per row: fill the finisher's grid (kVecGrid workgroups with the p.q partials)
+    int lg = 0;
+    const int64_t threads = (pq_part != nullptr ? (int64_t)kVecGrid : 1024) * 256;
+    while (lg < 4 && ctx->nrows * (2LL << lg) <= threads) ++lg;
+    if (pq_part != nullptr) {
+      hipLaunchKernelGGL(k_rec_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.uvk, mf.sv, mf.rpart,
+                         mf.rblk, MP, (int)mf.n, mf.i0, mf.ni, ctx->row0, ctx->nrows, sigma, lam,
+                         x_loc, y_loc, pq_part, lg, status);
+    } else if (ctx->nrows > 0) {
+      const int64_t nb = std::min<int64_t>((ctx->nrows << lg) / 256 + 1, 1024);
+      hipLaunchKernelGGL(k_rec_fin<false>, dim3((unsigned)nb), dim3(256), 0, s, mf.uvk, mf.sv,
+                         mf.rpart, mf.rblk, MP, (int)mf.n, mf.i0, mf.ni, ctx->row0, ctx->nrows,
+                         sigma, lam, x_loc, y_loc, (double *)nullptr, lg, status);
+    }
     return;
   }
   const unsigned gi = (unsigned)((mf.ni + kIC - 1) / kIC);
@@ -723,6 +1109,16 @@ bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double 
 double mf_bytes(const mlff_ctx *ctx) {
   const MfData &mf = ctx->mf;
   const double MP = (double)(mf.M * mf.n_perms), D = (double)mf.D;
+  if (mf.rec) {
+    // Rdd of every point once per point group (Zt on the fly; the query points' own rows
+    // are the same lines), the u and v halves of the records, the slot partials written
+    // and read, s, the operand and the result
+    const double ngrp = (double)((mf.ni + kRG - 1) / kRG), ni = (double)mf.ni;
+    const double n3 = 3.0 * mf.n;
+    return 8.0 * (3.0 * (double)mf.M * D * ngrp + ni * MP * (2.0 * n3 + 2.0) +
+                  2.0 * mf.rblk * ni * n3 + 2.0 * ni * MP + (double)ctx->N +
+                  2.0 * ctx->nrows);
+  }
   const double chunks = (double)((mf.ni + kIC - 1) / kIC);
   // Zt written once; Rt, Zt read by every point chunk in two kernels; Rd, Rdd, F
   return 8.0 * (MP * D * (1.0 + 4.0 * chunks) + (double)mf.ni * D * 6.0 + 16.0 * ctx->nrows);
@@ -733,7 +1129,7 @@ void mf_free(MfData &mf) {
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
                   (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc,
                   (void *)mf.uvk, (void *)mf.pi_d, (void *)mf.piinv_d, (void *)mf.kee,
-                  (void *)mf.eterm})
+                  (void *)mf.eterm, (void *)mf.wt, (void *)mf.sv, (void *)mf.rpart})
     if (p) (void)hipFree(p);
   mf = MfData();
 }

@@ -255,3 +255,47 @@ def test_matfree_ragged_shards(sg, golden_dir, m, world):
     # (scripts/dev/diag_ragged_iters.py)
     assert abs(outs[0][2].iters - ref[2].iters) <= max(3, 0.1 * ref[2].iters)
     assert np.linalg.norm(x - ref[2].x) <= 1e-6 * np.linalg.norm(ref[2].x)
+
+
+@pytest.mark.parametrize("name", ["nanotube", "sgdml_ethanol_n270_perms",
+                                  "sgdml_ethanol_n270_nongroup"])
+def test_record_factored_operator_matches_pair_path(sg, golden_dir, name, monkeypatch):
+    """The record-factored operator (k_rec_g + k_rec_fin: y = sum c u - J^T G from the
+    pair records, the default when they fit) against the five-kernel pair / F / J^T path
+    (MLFF_MF_REC=0) on the same operand, one rank and three ranks.  Same products,
+    regrouped: 1e-13 of the largest entry."""
+    if name == "nanotube":
+        from sgdml_amd import synthetic
+
+        ds = synthetic.nanotube_like(3, seed=4)
+        Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+        perms, sig = np.arange(370)[None, :], 10.0
+    else:
+        f = load_golden(golden_dir, name)
+        Rd, Rdd, perms, sig = f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"])
+    n = Rd.shape[0] * 3 * int(round((1 + np.sqrt(8 * Rd.shape[1] + 1)) / 2))
+    v = np.random.default_rng(5).standard_normal(n)
+    out = {}
+    for rec in ("1", "0"):
+        monkeypatch.setenv("MLFF_MF_REC", rec)
+        with sg.KernelSolver(n) as s:
+            s.sgdml_operator(Rd, Rdd, perms, sig)
+            s.set_operator(-1.0, 1e-10)
+            out[rec] = (s.matvec(v), s.storage_info()[1])
+    assert out["1"][1] != out["0"][1]  # the two paths report their own algorithmic bytes
+    ref = out["0"][0]
+    np.testing.assert_allclose(out["1"][0], ref, rtol=0, atol=1e-13 * np.abs(ref).max())
+
+    monkeypatch.setenv("MLFF_MF_REC", "1")
+
+    def body(rank, w, key):
+        with sg.KernelSolver(n, device=0, rank=rank, world=w,
+                             comm_id=key if w > 1 else None) as s:
+            s.sgdml_operator(Rd, Rdd, perms, sig)
+            s.set_operator(-1.0, 1e-10)
+            return s.matvec(v)
+
+    from tests.test_gpu_multirank import run_ranks
+
+    y3 = np.concatenate(run_ranks(3, body, timeout=120))
+    np.testing.assert_allclose(y3, ref, rtol=0, atol=1e-13 * np.abs(ref).max())
