@@ -540,6 +540,7 @@ __device__ __forceinline__ double rec_zt(const double *__restrict__ Rdd,
 
 struct RecArgs {
   const double *Rdd;   // M x D x 3
+  const double *Zt;    // (M n_perms) x D, precomputed (ZM == kZStored)
   const double *xc;    // contiguous operand (global index)
   const int32_t *Pt;   // n_perms x D
   const int32_t *ps, *pt;
@@ -554,8 +555,12 @@ struct RecArgs {
 // wt: w transposed, round_up(MP, kRJ) rows of ldw = ngrp kRG entries, zero padded, so
 // the accumulation runs unguarded over whole batches and point groups
 // grid: nsw8 pair-scalar workgroups first (dispatched first, off the tail), then the
-// pair blocks
-template <bool IDENT>
+// pair blocks.  Zt of a batch: gathered from Rdd / x per permutation (kZGather), from the
+// LDS-staged x of the block's atoms (kZIdent: one identity permutation), or read from the
+// Zt table (kZStored: several point groups, where k_mf_z's one pass over Rdd beats a
+// recomputation per group)
+enum { kZGather = 0, kZIdent = 1, kZStored = 2 };
+template <int ZM>
 __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
                                                int64_t nbp, int64_t ngrp, int64_t nsw8,
                                                const int *__restrict__ status) {
@@ -621,7 +626,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   double rg[kRG][3];
 #pragma unroll
   for (int k = 0; k < kRG; ++k) rg[k][0] = rg[k][1] = rg[k][2] = 0.0;
-  const bool capture = IDENT && a.i0 % kRJ == 0;
+  const bool capture = ZM == kZIdent && a.i0 % kRJ == 0;
   static_assert(8 * 3 * kRB * (kRB + 1) >= kWC * 2 * kRB * 3, "x stage fits in red");
   int64_t jn = 0;  // general permutations: (j, p) of the next batch slot
   int pn = 0;
@@ -630,13 +635,13 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
     const int cn = (int)((MPp - c0) < kWC ? (MPp - c0) : kWC);
     // (every thread's staging loads issued together, then stored)
     constexpr int kWL = kWC * kRG / 256, kXL = kWC * 2 * kRB * 3 / 256;
-    double wl[kWL], xl[IDENT ? kXL : 1];
+    double wl[kWL], xl[ZM == kZIdent ? kXL : 1];
 #pragma unroll
     for (int q = 0; q < kWL; ++q) {
       const int e = tid + q * 256;
       wl[q] = e < cn * kRG ? wp[(c0 + e / kRG) * a.ldw + e % kRG] : 0.0;
     }
-    if (IDENT) {
+    if (ZM == kZIdent) {
 #pragma unroll
       for (int q = 0; q < kXL; ++q) {
         const int e = tid + q * 256;
@@ -649,14 +654,23 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kWL; ++q) (&sW[0][0])[tid + q * 256] = wl[q];
-    if (IDENT) {
+    if (ZM == kZIdent) {
 #pragma unroll
       for (int q = 0; q < kXL; ++q) sx[tid + q * 256] = xl[q];
     }
     __syncthreads();
     for (int jb = 0; jb < cn; jb += kRJ) {
       double z[kRJ];
-      if (IDENT) {
+      if (ZM == kZStored) {
+        double zv[kRJ];
+#pragma unroll
+        for (int u = 0; u < kRJ; ++u) {
+          const int64_t jp = c0 + jb + u;
+          zv[u] = a.Zt[(jp < a.MP ? jp : a.MP - 1) * a.D + d];
+        }
+#pragma unroll
+        for (int u = 0; u < kRJ; ++u) z[u] = (valid && c0 + jb + u < a.MP) ? zv[u] : 0.0;
+      } else if (ZM == kZIdent) {
         // Zt_j[d] = sum_c Rdd_j[d, c] (x_j[bb, c] - x_j[aa, c])  (z_entry, s = aa, t = bb)
         double rv[kRJ][3];
 #pragma unroll
@@ -981,17 +995,23 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     return;
   }
   if (mf.rec) {
-    const RecArgs ra{mf.Rdd, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni, MP,
-                     mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
+    const RecArgs ra{mf.Rdd, mf.Zt, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni,
+                     MP, mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
     const int64_t nbp = (int64_t)mf.rblk * (mf.rblk + 1) / 2, ngrp = (mf.ni + kRG - 1) / kRG;
     const int64_t nbp8 = (nbp + 7) / 8 * 8, nsw8 = (mf.ni * MP + 31) / 32 * 8;
     const dim3 grid((unsigned)(nsw8 + nbp8 * ngrp));
-    if (mf.ident)
-      hipLaunchKernelGGL(k_rec_g<true>, grid, dim3(256), 0, s, ra, (const double *)mf.wt, nbp, ngrp,
-                         nsw8, status);
-    else
-      hipLaunchKernelGGL(k_rec_g<false>, grid, dim3(256), 0, s, ra, (const double *)mf.wt, nbp,
-                         ngrp, nsw8, status);
+    const double *wt = mf.wt;
+    if (ngrp > 1) {  // Zt once (k_mf_z), read by every point group
+      const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+      hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd,
+                         mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt, mf.ps, mf.pt,
+                         mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
+      hipLaunchKernelGGL(k_rec_g<kZStored>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+    } else if (mf.ident) {
+      hipLaunchKernelGGL(k_rec_g<kZIdent>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+    } else {
+      hipLaunchKernelGGL(k_rec_g<kZGather>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+    }
     // lanes per row: fill the finisher's grid (kVecGrid workgroups with the p.q partials)
     int lg = 0;
     const int64_t threads = (pq_part != nullptr ? (int64_t)kVecGrid : 1024) * 256;
@@ -1115,9 +1135,12 @@ double mf_bytes(const mlff_ctx *ctx) {
     // and read, s, the operand and the result
     const double ngrp = (double)((mf.ni + kRG - 1) / kRG), ni = (double)mf.ni;
     const double n3 = 3.0 * mf.n;
-    return 8.0 * (3.0 * (double)mf.M * D * ngrp + ni * MP * (2.0 * n3 + 2.0) +
-                  2.0 * mf.rblk * ni * n3 + 2.0 * ni * MP + (double)ctx->N +
-                  2.0 * ctx->nrows);
+    // one point group: Zt formed on the fly from Rdd; several: Zt written once by k_mf_z
+    // and read by every group, the groups' own Rdd rows read by their J^T step
+    const double zt = ngrp > 1 ? 3.0 * (double)mf.M * D + MP * D * (1.0 + ngrp) + 3.0 * ni * D
+                               : 3.0 * (double)mf.M * D;
+    return 8.0 * (zt + ni * MP * (2.0 * n3 + 2.0) + 2.0 * mf.rblk * ni * n3 + 2.0 * ni * MP +
+                  (double)ctx->N + 2.0 * ctx->nrows);
   }
   const double chunks = (double)((mf.ni + kIC - 1) / kIC);
   // Zt written once; Rt, Zt read by every point chunk in two kernels; Rd, Rdd, F
