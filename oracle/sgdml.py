@@ -146,6 +146,64 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x, use_E_cstr=False)
     return np.concatenate([y.reshape(-1), outE]) if use_E_cstr else y.reshape(-1)
 
 
+def pair_records(R_desc, R_d_desc, perms, sig):
+    """The x-independent per-(i, j, p) quantities of the operator above, as the GPU keeps
+    them (kernels_gen.hip k_sgdml_uv, mirror = 0): u = J_i^T diff (query point side),
+    v = J_j^T P_p^T diff (training point side, 3n each), 5 m and w.
+    Returns U, V (M x M x n_perms x 3n), m5, w (M x M x n_perms)."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    P = np.array([desc_perm(p) for p in np.atleast_2d(perms)])
+    npm = P.shape[0]
+    J = [d_desc_from_comp(R_d_desc[m], n) for m in range(M)]  # D x 3n
+    sqrt5 = np.sqrt(5.0)
+    U = np.empty((M, M, npm, 3 * n))
+    V = np.empty((M, M, npm, 3 * n))
+    m5 = np.empty((M, M, npm))
+    w = np.empty((M, M, npm))
+    for i in range(M):
+        for j in range(M):
+            for p in range(npm):
+                diff = R_desc[i] - R_desc[j][P[p]]
+                norm = sqrt5 * np.linalg.norm(diff)
+                m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+                m5[i, j, p], w[i, j, p] = 5.0 * m, (sig ** 2 + sig * norm) * m
+                U[i, j, p] = J[i].T @ diff
+                dp = np.empty(D)
+                dp[P[p]] = diff               # P_p^T diff
+                V[i, j, p] = J[j].T @ dp
+    return U, V, m5, w
+
+
+def kernel_matvec_factored(R_desc, R_d_desc, perms, sig, x, records=None):
+    """The operator above regrouped as the GPU's record-factored form evaluates it
+    (kernels_mf.hip k_rec_g / k_rec_fin):
+        c_ijp = 5 m (v_ijp . x_j)          (= 5 m (diff . z_j[P_p]))
+        G_i   = sum_jp w_ijp z_j[P_p]
+        y_i   = sum_jp c_ijp u_ijp - J_i^T G_i      (= J_i^T F_i)
+    Same products as kernel_matvec_matrix_free, other grouping."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    P = np.array([desc_perm(p) for p in np.atleast_2d(perms)])
+    U, V, m5, w = records if records is not None else pair_records(R_desc, R_d_desc, perms, sig)
+    s_at, t_at = np.tril_indices(n, k=-1)
+    X = np.asarray(x, dtype=np.float64).reshape(M, n, 3)
+    z = np.einsum("mdc,mdc->md", R_d_desc, X[:, t_at, :] - X[:, s_at, :])
+    Zt = z[:, P]                                    # M x n_perms x D
+    y = np.empty((M, 3 * n))
+    for i in range(M):
+        c = m5[i] * np.einsum("jpa,ja->jp", V[i], X.reshape(M, 3 * n))
+        G = np.einsum("jp,jpd->d", w[i], Zt)
+        contrib = R_d_desc[i] * G[:, None]
+        jtg = np.zeros((n, 3))
+        np.add.at(jtg, t_at, contrib)
+        np.add.at(jtg, s_at, -contrib)
+        y[i] = np.einsum("jp,jpa->a", c, U[i]) - jtg.reshape(-1)
+    return y.reshape(-1)
+
+
 def kernel_diag(R_desc, R_d_desc, perms, sig, use_E_cstr=False):
     """diag(K) of the assembled sGDML kernel, one diagonal block K[i, i] per training point
     (IterativeCholesky._assemble_kernel_mat_diag, iterative_cholesky.py:241-373, which
