@@ -258,18 +258,30 @@ def test_matfree_ragged_shards(sg, golden_dir, m, world):
 
 
 @pytest.mark.parametrize("name", ["nanotube", "sgdml_ethanol_n270_perms",
-                                  "sgdml_ethanol_n270_nongroup"])
+                                  "sgdml_ethanol_n270_nongroup", "ethanol_m40_perms",
+                                  "ethanol_m40"])
 def test_record_factored_operator_matches_pair_path(sg, golden_dir, name, monkeypatch):
     """The record-factored operator (k_rec_g + k_rec_fin: y = sum c u - J^T G from the
     pair records, the default when they fit) against the five-kernel pair / F / J^T path
     (MLFF_MF_REC=0) on the same operand, one rank and three ranks.  Same products,
-    regrouped: 1e-13 of the largest entry."""
+    regrouped: 1e-13 of the largest entry.  Covers every Zt source of k_rec_g: the LDS x
+    stage (one identity permutation, <= 16 points per rank), the per-permutation gathers
+    (the golden permutation sets) and the Zt table (M = 40: three 16-point groups, with
+    and without permutations)."""
     if name == "nanotube":
         from sgdml_amd import synthetic
 
         ds = synthetic.nanotube_like(3, seed=4)
         Rd, Rdd = sg.sgdml_descriptors(ds["R"])
         perms, sig = np.arange(370)[None, :], 10.0
+    elif name.startswith("ethanol_m40"):
+        from sgdml_amd import synthetic
+
+        ds = synthetic.ethanol_like(40, seed=7)
+        Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+        perms = (load_golden(golden_dir, "sgdml_ethanol_n270_perms")["perms"]
+                 if name.endswith("perms") else np.arange(9)[None, :])
+        sig = 10.0
     else:
         f = load_golden(golden_dir, name)
         Rd, Rdd, perms, sig = f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"])
