@@ -1,0 +1,51 @@
+"""bench.py host logic (no GPU): the defaults the driver relies on, the workload / config
+naming, the PMC-traffic lookup and the CPU-core accounting of the baseline."""
+import json
+import sys
+
+import pytest
+
+import bench
+
+
+def _args(monkeypatch, *argv):
+    monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+    return bench.parse()
+
+
+def test_defaults_are_the_driver_contract(monkeypatch):
+    a = _args(monkeypatch)
+    assert (a.gpus, a.steps, a.warmup) == (1, 50, 5)
+    assert a.n is None and a.k is None          # -> N = 65536, k = 256 in main()
+    assert a.workload == "rbf" and a.storage == "auto"
+    assert a.configs3_n == 131072               # the configs[3] leg rides along on every N
+    a = _args(monkeypatch, "--gpus", "8", "--steps", "20", "--warmup", "5")
+    assert (a.gpus, a.steps, a.warmup) == (8, 20, 5)
+    assert a.n is None                          # value stays the configs[2] problem at N > 1
+
+
+def test_metric_matches_baseline():
+    base = json.loads((bench.REPO / "BASELINE.json").read_text())
+    assert bench.METRIC == base["metric"]
+
+
+def test_reference_step_times_are_baseline_md():
+    # 0.105 s (N = 15540), 2.073 s (~157k), 6.600 s (~505k)
+    assert bench.REF_STEP_S == {15540: 0.105, 156510: 2.073, 505050: 6.600}
+
+
+@pytest.mark.parametrize("key", ["rbf_n65536_nystrom256/sym/gpus1",
+                                 "sgdml_nanotube_n15540_pivchol2701/matfree/gpus1"])
+def test_pmc_traffic_lookup(key):
+    workload, storage, g = key.split("/")
+    v = bench.pmc_traffic(workload, storage, int(g[4:]))
+    assert v is not None and v > 0
+    assert bench.pmc_traffic("no_such_workload", "sym", 1) is None
+
+
+def test_usable_cores_is_consistent():
+    c = bench.usable_cores()
+    assert c["cores"] >= 1
+    assert c["cores"] <= c["affinity_cpus"]
+    if c["cgroup_quota_cpus"] is not None:
+        assert c["cores"] <= max(1, int(c["cgroup_quota_cpus"]))
