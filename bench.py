@@ -526,17 +526,25 @@ def main():
         roof_op["note"] = ("two dependent launches (Zt, G = sum w Zt and J^T G of a pair block in one "
                            "workgroup; the finisher): ~33 MB per application at M = 14, latency- "
                            "not HBM-bound (PMC traffic in profiles/pmc_traffic.json; DESIGN.md 3.2)")
-    # low-rank apply z = sigma_p (r - T^T T r) / lam: T (k x N_loc) read twice + r, z, partials
+    # low-rank apply z = sigma_p (r - T^T T r) / lam.  Two-pass form: T (k x N_loc) read
+    # twice + r, z (16 k N + 24 N).  One-pass form (one rank, rows in registers): T read once
+    # + the row groups' partial vectors written and read (8 k N + 16 G N + 24 N); the
+    # algorithmic bytes are those of the form that ran (the library reports them)
     roof_pre = None
     if tm.get("precon_count"):
         pre_ms = tm["precon_ms"] / tm["precon_count"]
-        pre_bytes = 16.0 * k * nloc + 24.0 * nloc
+        one_pass, pre_bytes = solver.precon_apply_traffic()
         pre_gbs = pre_bytes / (pre_ms * 1e-3) / 1e9
+        two_pass_bytes = 16.0 * k * nloc + 24.0 * nloc
         roof_pre = {"bound": "hbm", "achieved": pre_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": pre_gbs / HBM_PEAK_GBS,
-                    "traffic": pmc_traffic(workload + "/precon", storage, world),
-                    "kernel": "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)",
-                    "bytes_per_launch": pre_bytes, "mean_launch_ms": pre_ms}
+                    "traffic": pmc_traffic(workload + ("/precon1" if one_pass else "/precon"),
+                                           storage, world),
+                    "kernel": ("k_lr_rows + k_lr_fin (one-pass low-rank apply: each panel row "
+                               "read once, t_i kept in its workgroup)" if one_pass else
+                               "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)"),
+                    "bytes_per_launch": pre_bytes, "mean_launch_ms": pre_ms,
+                    "two_pass_equivalent_gbs": two_pass_bytes / (pre_ms * 1e-3) / 1e9}
     # the roofline entry is the kernel group with the larger share of the iteration
     roof_dominant = roof_pre if roof_pre is not None and roof_pre["mean_launch_ms"] > gemv_ms \
         else roof_op

@@ -349,6 +349,18 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   if (const char *e = std::getenv("MLFF_ZSPLIT"))  // sweeps
     ctx->zsplit = (int)std::min<int64_t>(std::max(1, std::atoi(e)), (k + 15) / 16);
   MLFF_HIP(ctx, hipMalloc(&ctx->zpart, sizeof(double) * ctx->zsplit * ctx->blk));
+  // one rank, rows that fit a workgroup's registers and at least 3 rows per workgroup (below
+  // that the G partial vectors cost as much traffic as the second panel pass they replace):
+  // the one-pass apply.  MLFF_LR_ROWS=0 / 1 forces the two-pass / one-pass apply (A/B, tests)
+  if (ctx->lr_zpart != nullptr) {
+    (void)hipFree(ctx->lr_zpart);
+    ctx->lr_zpart = nullptr;
+  }
+  ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && k >= 768;
+  if (const char *e = std::getenv("MLFF_LR_ROWS"))
+    ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && std::atoi(e) != 0;
+  if (ctx->lr_rows)
+    MLFF_HIP(ctx, hipMalloc(&ctx->lr_zpart, sizeof(double) * lr_rows_groups(k) * ctx->blk));
   return MLFF_OK;
 }
 
@@ -773,10 +785,15 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
   const double *zsrc;
   if (lowrank) {
     const size_t pm = mark_begin(ctx, marks);
-    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s,
-                      fold);
-    launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
-                    ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
+    if (ctx->lr_rows) {
+      launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
+                           1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold);
+    } else {
+      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status,
+                        s, fold);
+      launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
+                      ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
+    }
     mark_end(ctx, marks, pm, it, 1);
     zsrc = ctx->z;
   } else {
@@ -944,7 +961,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
                   (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart_base,
-                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->gb})
+                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->lr_zpart, (void *)ctx->gb})
     dev_free(p);
   for (const auto &c : ctx->scratch_chunks) dev_free(c.p);
   ctx->scratch_chunks.clear();
@@ -1389,6 +1406,24 @@ int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out) {
   MLFF_API_END(ctx)
 }
 
+int mlff_precon_apply_traffic(mlff_ctx *ctx, int *one_pass_out, double *bytes_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  const double N = (double)ctx->blk, n = (double)ctx->nrows, k = (double)ctx->k;
+  const bool one = ctx->precon_kind != MLFF_PRECON_NONE && ctx->lr_rows;
+  if (one_pass_out) *one_pass_out = one ? 1 : 0;
+  if (bytes_out) {
+    if (ctx->precon_kind == MLFF_PRECON_NONE)
+      *bytes_out = 0.0;
+    else if (one)
+      *bytes_out = 8.0 * k * N + 16.0 * (double)lr_rows_groups(ctx->k) * N + 24.0 * n;
+    else
+      *bytes_out = 16.0 * k * N + 24.0 * n;
+  }
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
@@ -1405,6 +1440,15 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
     MLFF_HIP(ctx, hipMemcpyAsync(zd, rd, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
   } else {
     ctx->spec_t = false;  // tpart is reused below
+    if (ctx->lr_rows) {
+      launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p,
+                           1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart);
+      MLFF_HIP(ctx, hipGetLastError());
+      if (ctx->nrows > 0)
+        MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
+      MLFF_HIP(ctx, hipStreamSynchronize(s));
+      return MLFF_OK;
+    }
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, rd, ctx->tpart, nullptr, s);
     MLFF_TRY(allreduce(ctx, ctx->tpart, (size_t)(ctx->k * ctx->tsplit)));
     launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, rd, zd, ctx->nrows,

@@ -231,6 +231,8 @@ struct mlff_ctx {
   int tsplit = 1;         // column splits of the T GEMV
   int zsplit = 1;         // row splits of the T^T t GEMV
   double *zpart = nullptr;  // zsplit x blk partials
+  bool lr_rows = false;        // one-pass low-rank apply (launch_lr_apply_rows), one rank
+  double *lr_zpart = nullptr;  // its lr_rows_groups(k) x blk partials
   double *tpart = nullptr;       // = tpart_base + kVecGrid
   double *tpart_base = nullptr;
   bool spec_t = false;           // tpart already holds T r of the current r (merged collective)
@@ -350,6 +352,14 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
                      const double *r, double *z, int64_t n, double sigma_p, double lam_inv,
                      double *rho_part, const int *status, hipStream_t s, double *zpart,
                      int zsplit, StopFold fold = StopFold{});
+// one-pass apply z = sigma_p/lam (r - T^T T r) with rho partials, one rank, for panels whose
+// rows fit a workgroup's registers (lr_rows_fits); zpart: lr_rows_groups(k) x ldt scratch
+bool lr_rows_fits(int64_t ldt);
+int lr_rows_groups(int64_t k);
+void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
+                          int64_t n, double sigma_p, double lam_inv, double *rho_part,
+                          const int *status, hipStream_t s, double *zpart,
+                          StopFold fold = StopFold{});
 // part[ks * ldw + c] = sum_{j in slice ks} W[j, c] * (sum_sp tsrc[sp * tstride + j])
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,

@@ -26,6 +26,8 @@ __device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ 
   return sh[4];
 }
 
+__device__ __forceinline__ bool stop_decide(const StopFold &f, double rr);
+
 // Stop test of iteration f.it (as k_stoptest) at the start of the next iteration's first
 // kernel: every workgroup reduces the same partials in the same order and reaches the
 // same decision; workgroup (0, 0) writes the state.  All threads of the block call it.
@@ -34,6 +36,27 @@ __device__ __forceinline__ bool stop_prologue(const StopFold &f, double *sh) {
   if (f.rr_part == nullptr) return true;
   const double rr = reduce_parts_bcast(f.rr_part, kVecGrid, sh);
   __syncthreads();  // sh is reused by the caller
+  return stop_decide(f, rr);
+}
+
+// The same for a workgroup of any multiple of 256 threads: the first 256 threads reduce
+// the partials exactly as reduce_parts_bcast does (same bits), the rest wait.
+__device__ __forceinline__ bool stop_prologue_wide(const StopFold &f, double *sh) {
+  if (f.rr_part == nullptr) return true;
+  double v = 0.0;
+  if (threadIdx.x < 256)
+    for (int i = threadIdx.x; i < kVecGrid; i += 256) v += f.rr_part[i];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0 && w < 4) sh[w] = v;
+  __syncthreads();
+  const double rr = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();  // sh is reused by the caller
+  return stop_decide(f, rr);
+}
+
+__device__ __forceinline__ bool stop_decide(const StopFold &f, double rr) {
   const double resid = sqrt(rr);
   DevState *st = f.st;
   int dec = ST_RUNNING;
@@ -376,6 +399,199 @@ void launch_precon_z(const double *T, int64_t ldt, int64_t k, int splits, const 
                       panel_cached_rows(k, ldt));
   hipLaunchKernelGGL(k_precon_fin, dim3(kVecGrid), dim3(256), 0, s, zpart, zsplit, ldt, r, z, n,
                      sigma_p, lam_inv, rho_part, status);
+}
+
+// ---------------------------------------------------------------------------
+// One-pass low-rank apply (one rank; panel rows short enough to sit in registers):
+//   z = sigma_p * lam_inv * (r - T^T (T r))          (iterative_cholesky.py:145-148)
+// Workgroup w owns the panel rows [w rpw, (w + 1) rpw).  Row i is loaded into registers
+// once (512 threads, M double2 each, 16-B loads), t_i = T[i, :] . r is formed against r
+// staged in LDS (thread partial -> wave sum -> the 8 wave sums in a fixed order, the same
+// bits in every thread), and zacc += T[i, :] t_i from the same registers.  t_i never
+// leaves the workgroup, so the panel is read ONCE per apply where the two-pass apply
+// (T r, then T^T t) reads it twice; the price is one partial vector per workgroup
+// (G x ldt doubles, 32 MB at the nanotube's k = 2701, N = 15540 instead of 336 MB of
+// panel), summed in a fixed order by k_lr_fin.  Row i + 1 is in flight while row i is
+// reduced (two register buffers, one LDS barrier per row).
+constexpr int kLrThreads = 512;
+constexpr int64_t kLrMaxCols = 16 * 2 * kLrThreads;  // M <= 16 double2 per thread
+
+bool lr_rows_fits(int64_t ldt) { return ldt > 0 && ldt % 2 == 0 && ldt <= kLrMaxCols; }
+int lr_rows_per_wg(int64_t k) { return (int)((k + 255) / 256); }
+int lr_rows_groups(int64_t k) {
+  const int rpw = lr_rows_per_wg(k);
+  return (int)((k + rpw - 1) / rpw);
+}
+
+// row loads through a buffer descriptor of the row: one VGPR offset for all M loads (the
+// m-th at soffset m * 8 KB), and the descriptor's range check returns zeros beyond the row
+// (no bounds test, no 64-bit address per load).  aux 2 = non-temporal.
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+template <int M, int AUX>
+__device__ __forceinline__ void lr_load_row(d2 (&buf)[M], const double *row, int bytes) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(row), 0, bytes, 0x00020000);
+  const int voff = (int)threadIdx.x * 16;
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * kLrThreads * 16, AUX));
+}
+
+// Registers per lane: the row being reduced (cur), the next row in flight (nxt) and r, M
+// double2 each; the partial z of the workgroup's rows lives in LDS slots private to the
+// thread (z_sh[m * kLrThreads + tid]), so no barrier guards them.
+// Row i (in cur): t_i, z_sh += cur t_i; row i + 1 loaded into nxt first (a descriptor of
+// zero bytes past the last row: the loads return zeros and move nothing).
+template <int M, int AUX>
+__device__ __forceinline__ void lr_row_step(d2 (&cur)[M], d2 (&nxt)[M], const d2 (&rv)[M],
+                                            d2 *z_sh, const double *__restrict__ T, int64_t ldt,
+                                            int64_t i, int64_t i0, int64_t i1, double *red) {
+  lr_load_row<M, AUX>(nxt, T + (i + 1 < i1 ? i + 1 : i) * ldt, i + 1 < i1 ? (int)(ldt * 8) : 0);
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    a0 = fma(cur[m].x, rv[m].x, a0);
+    a1 = fma(cur[m].y, rv[m].y, a1);
+  }
+  const double s = wave_sum(a0 + a1);
+  const int p = (int)((i - i0) & 1);  // two slot sets: one barrier per row suffices
+  if ((threadIdx.x & 63) == 0) red[p * 8 + (threadIdx.x >> 6)] = s;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  static_assert(kLrThreads == 512, "eight wave sums per row");
+  const double *q = red + p * 8;
+  const double t = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+#pragma unroll
+  for (int m = 0; m < M; m += 4) {
+#pragma unroll
+    for (int u = 0; u < 4 && m + u < M; ++u) {
+      d2 zv = z_sh[threadIdx.x + kLrThreads * (m + u)];
+      zv.x = fma(cur[m + u].x, t, zv.x);
+      zv.y = fma(cur[m + u].y, t, zv.y);
+      z_sh[threadIdx.x + kLrThreads * (m + u)] = zv;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// the workgroup's rows [i0, i1), all read with one load policy (AUX)
+template <int M, int AUX>
+__device__ __forceinline__ bool lr_rows_loop(const d2 (&rv)[M], d2 *z_sh,
+                                             const double *__restrict__ T, int64_t ldt,
+                                             int64_t i0, int64_t i1, double *red,
+                                             const StopFold &fold) {
+  d2 A[M], B[M];
+  lr_load_row<M, AUX>(A, T + i0 * ldt, i0 < i1 ? (int)(ldt * 8) : 0);
+  // the stop test of the previous iteration while the first row is in flight (every
+  // thread reaches the same decision; false: the solver stopped)
+  if (!stop_prologue_wide(fold, red)) return false;
+#pragma unroll
+  for (int m = 0; m < M; ++m) z_sh[threadIdx.x + kLrThreads * m] = d2{0.0, 0.0};
+  int64_t i = i0;
+  for (; i + 1 < i1; i += 2) {
+    lr_row_step<M, AUX>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
+    lr_row_step<M, AUX>(B, A, rv, z_sh, T, ldt, i + 1, i0, i1, red);
+  }
+  if (i < i1) lr_row_step<M, AUX>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
+  return true;
+}
+
+template <int M>
+__global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict__ T, int64_t ldt,
+                                                        int64_t k, int rpw,
+                                                        const double *__restrict__ r,
+                                                        double *__restrict__ zpart,
+                                                        int cached_wgs,
+                                                        const int *__restrict__ status,
+                                                        StopFold fold) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ d2 z_sh[M * kLrThreads];
+  __shared__ double red[16];
+  const int bytes = (int)(ldt * 8);
+  const int64_t i0 = (int64_t)blockIdx.x * rpw;
+  const int64_t i1 = i0 + rpw < k ? i0 + rpw : k;
+  // r and the first row are requested before the stop test of the previous iteration
+  // (its partials' round trip then overlaps them; a stopped solver drops them unused)
+  d2 rv[M];
+  lr_load_row<M, 0>(rv, r, bytes);  // zeros beyond ldt
+  const bool go = blockIdx.x < cached_wgs ? lr_rows_loop<M, 0>(rv, z_sh, T, ldt, i0, i1, red, fold)
+                                           : lr_rows_loop<M, 2>(rv, z_sh, T, ldt, i0, i1, red, fold);
+  if (!go) return;
+  const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+      zpart + (int64_t)blockIdx.x * ldt, 0, bytes, 0x00020000);
+  const int voff = (int)threadIdx.x * 16;
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + kLrThreads * m]),
+                                           out, voff, m * kLrThreads * 16, 0);
+}
+
+// z[j] = sigma_p lam_inv (r[j] - sum_{g < G} zpart[g, j]) for j < n, the G partials in
+// order (wave w sums its quarter, the quarters in order); rho partials r . z
+// (kVecGrid slots: one per workgroup, the rest zero)
+__global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart, int G, int64_t ldp,
+                                                const double *__restrict__ r,
+                                                double *__restrict__ z, int64_t n, double sigma_p,
+                                                double lam_inv, double *__restrict__ rho_part,
+                                                const int *__restrict__ status) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sh[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const int g0 = (G * w) / 4, g1 = (G * (w + 1)) / 4;
+  double s = 0.0;
+  if (j < n) {
+    // batches of 16 partials in flight, the last one predicated (no serial tail)
+    const double *pj = zpart + j;
+    for (int g = g0; g < g1; g += 16) {
+      double t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = g + u < g1 ? pj[(int64_t)(g + u) * ldp] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += t[u];
+    }
+  }
+  sh[w][lane] = s;
+  __syncthreads();
+  if (w == 0) {
+    double rv = 0.0, zv = 0.0;
+    if (j < n) {
+      const double sv = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+      rv = r[j];
+      zv = sigma_p * (lam_inv * (rv - sv));
+      z[j] = zv;
+    }
+    const double rho = wave_sum(rv * zv);
+    if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = rho;
+  }
+  if (blockIdx.x == 0 && rho_part != nullptr)
+    for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 256) rho_part[i] = 0.0;
+}
+
+void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
+                          int64_t n, double sigma_p, double lam_inv, double *rho_part,
+                          const int *status, hipStream_t s, double *zpart, StopFold fold) {
+  const int64_t n2 = ldt / 2;
+  const int rpw = lr_rows_per_wg(k), G = lr_rows_groups(k);
+  // rows read with default-policy loads stay in the MALL from one iteration to the next:
+  // the panel_cached_rows budget as whole workgroups' rows (one load policy per workgroup);
+  // MLFF_LR_CACHE_WGS overrides (A/B)
+  int cached = panel_streams(k, ldt) ? (int)(panel_cached_rows(k, ldt) / rpw) : G;
+  if (const char *e = std::getenv("MLFF_LR_CACHE_WGS")) cached = std::atoi(e);
+  const dim3 grid((unsigned)G);
+  if (n2 <= 4 * kLrThreads)
+    hipLaunchKernelGGL(k_lr_rows<4>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+  else if (n2 <= 8 * kLrThreads)
+    hipLaunchKernelGGL(k_lr_rows<8>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+  else if (n2 <= 12 * kLrThreads)
+    hipLaunchKernelGGL(k_lr_rows<12>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+  else
+    hipLaunchKernelGGL(k_lr_rows<16>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+  if (n > 0)
+    hipLaunchKernelGGL(k_lr_fin, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, zpart, G, ldt, r, z,
+                       n, sigma_p, lam_inv, rho_part, status);
 }
 
 // ---------------------------------------------------------------------------

@@ -78,6 +78,7 @@ SIGNATURES = {
     "mlff_precon_lowrank": (_int, [_c_ctx, _p_dbl, _i64]),
     "mlff_precon_eig": (_int, [_c_ctx, _i64, _int, _i64, _int, _p_dbl, _p_dbl]),
     "mlff_precon_info": (_int, [_c_ctx, _p_int, _p_i64]),
+    "mlff_precon_apply_traffic": (_int, [_c_ctx, _p_int, _p_dbl]),
     "mlff_precon_apply": (_int, [_c_ctx, _p_dbl, _p_dbl]),
     "mlff_precon_get_panel": (_int, [_c_ctx, _p_dbl, _i64]),
     "mlff_lev_scores": (_int, [_c_ctx, _p_i64, _i64, _dbl, _p_dbl]),

@@ -294,3 +294,41 @@ def test_call_order_and_argument_errors(sg):
         s.precon_pivchol(20)                        # still usable
         res = s.pcg(b, tol=1e-8, maxiter=5 * n)
         assert res.info == 0
+
+
+@pytest.mark.parametrize("n,k", [(1000, 3), (1000, 800), (5000, 1031), (11000, 900),
+                                 (15540, 2701)])
+def test_one_pass_lowrank_apply(sg, monkeypatch, n, k):
+    """The one-pass low-rank apply (k_lr_rows + k_lr_fin: each panel row read once, t_i
+    kept in the workgroup) against the two-pass apply (T r, then T^T t) and NumPy, on
+    every register-tile width (M = 4, 8, 12, 16 double2 per thread), ragged row groups
+    (k = 1031: 207 groups of 5 rows, the last of 1) and k < one row per workgroup.  Then a
+    PCG solve on both applies, held to the chaotic-regime contract of tests/parity.py (a
+    random panel makes a poor preconditioner: the residual curves of two summation orders
+    part after ~15 iterations, as they do on the CPU).
+    Reference: iterative_cholesky.py:145-148 (z = (r - T^T T r) / lam)."""
+    lam = 1.0
+    X, b = _rbf(n)
+    rng = np.random.default_rng(n + k)
+    L = rng.standard_normal((k, n)) * 0.05
+    r = rng.standard_normal(n)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MLFF_LR_ROWS", mode)
+        with sg.KernelSolver(n) as s:
+            s.gen_rbf(X, length_scale=0.2)
+            s.set_operator(1.0, lam)
+            s.precon_lowrank(L)
+            T = s.precon_panel()
+            z = s.precon_apply(r)
+            res = s.pcg(b, tol=1e-8, maxiter=5 * n)
+        out[mode] = (T, z, res)
+    T, z1, res1 = out["1"]
+    _, z0, res0 = out["0"]
+    zref = (r - T.T @ (T @ r)) / lam
+    sgn = np.sign(np.dot(z0, zref))  # sigma_p of the low-rank operator
+    assert np.linalg.norm(z0 - sgn * zref) <= 1e-12 * np.linalg.norm(zref)
+    assert np.linalg.norm(z1 - z0) <= 1e-13 * np.linalg.norm(z0)
+    assert res0.info == res1.info == 0
+    assert_pcg_parity(res1.iters, res1.trace[1:], res1.x, res0.iters, res0.trace[1:], res0.x,
+                      mode="chaotic", x_tol=1e-6)
