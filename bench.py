@@ -540,9 +540,12 @@ def main():
                     "frac": pre_gbs / HBM_PEAK_GBS,
                     "traffic": pmc_traffic(workload + ("/precon1" if one_pass else "/precon"),
                                            storage, world),
-                    "kernel": ("k_lr_rows + k_lr_fin (one-pass low-rank apply: each panel row "
-                               "read once, t_i kept in its workgroup)" if one_pass else
-                               "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)"),
+                    "kernel": {1: "k_lr_rows + k_lr_fin (one-pass low-rank apply: each panel "
+                                  "row read once, t_i kept in its workgroup)",
+                               2: "k_lr_cluster + k_lr_fin (one-pass low-rank apply: each panel "
+                                  "row read once by a cluster of workgroups that hand their "
+                                  "partial t_i to each other)"}.get(
+                        one_pass, "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)"),
                     "bytes_per_launch": pre_bytes, "mean_launch_ms": pre_ms,
                     "two_pass_equivalent_gbs": two_pass_bytes / (pre_ms * 1e-3) / 1e9}
     # the roofline entry is the kernel group with the larger share of the iteration

@@ -254,10 +254,12 @@ int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out);
 /* z_local = M r_local (collective over ranks for the low-rank part) */
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local);
 /* How this rank's low-rank apply (iterative_cholesky.py:145-148 z = (r - T^T T r) / lam)
- * runs: one_pass_out = 1 when each panel row is read once per apply (one rank, rows that
- * fit a workgroup's registers: k_lr_rows + k_lr_fin), 0 for the two-pass T r / T^T t
- * apply; bytes_out = its algorithmic HBM bytes per apply (one pass: 8 k N + 16 G N + 24 N,
- * G = row groups; two passes: 16 k N + 24 N).  No reference counterpart (telemetry). */
+ * runs: one_pass_out = 1 when each panel row is read once per apply by one workgroup (one
+ * rank, rows that fit a workgroup's registers: k_lr_rows + k_lr_fin), 2 when a row is
+ * shared by a cluster of workgroups (longer rows: k_lr_cluster + k_lr_fin), 0 for the
+ * two-pass T r / T^T t apply; bytes_out = its algorithmic HBM bytes per apply (one pass:
+ * 8 k N + 16 G N + 24 N, G = row groups or clusters; two passes: 16 k N + 24 N).  A cluster
+ * hand-off that times out fails the call with MLFF_ERR_HIP.  No reference counterpart. */
 int mlff_precon_apply_traffic(mlff_ctx *ctx, int *one_pass_out, double *bytes_out);
 /* the k x nrows Woodbury panel T (or B / P for Nystrom) of this rank */
 int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out);

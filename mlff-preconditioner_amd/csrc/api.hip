@@ -352,15 +352,34 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   // one rank, rows that fit a workgroup's registers and at least 3 rows per workgroup (below
   // that the G partial vectors cost as much traffic as the second panel pass they replace):
   // the one-pass apply.  MLFF_LR_ROWS=0 / 1 forces the two-pass / one-pass apply (A/B, tests)
-  if (ctx->lr_zpart != nullptr) {
-    (void)hipFree(ctx->lr_zpart);
-    ctx->lr_zpart = nullptr;
+  for (void **p : {(void **)&ctx->lr_zpart, (void **)&ctx->lr_slots, (void **)&ctx->lr_fault})
+    if (*p != nullptr) {
+      (void)hipFree(*p);
+      *p = nullptr;
+    }
+  const char *lr_env = std::getenv("MLFF_LR_ROWS");
+  const bool lr_on = lr_env == nullptr || std::atoi(lr_env) != 0;
+  ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && (lr_env ? lr_on : k >= 768);
+  // longer rows: clusters of workgroups share a row (lr_cluster_count of them resident);
+  // worth it from ~4 rows per cluster (the Q partial vectors against the second pass)
+  ctx->lr_cluster = false;
+  if (ctx->world == 1 && !ctx->lr_rows && lr_on && lr_cluster_fits(ctx->blk)) {
+    ctx->lr_q = lr_cluster_count(ctx->blk, ctx->device);
+    if (const char *e = std::getenv("MLFF_LR_CLUSTERS"))  // A/B: fewer clusters
+      ctx->lr_q = std::min(ctx->lr_q, std::max(1, std::atoi(e)));
+    ctx->lr_cluster = ctx->lr_q >= 1 && k >= 4 * (int64_t)ctx->lr_q;
   }
-  ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && k >= 768;
-  if (const char *e = std::getenv("MLFF_LR_ROWS"))
-    ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && std::atoi(e) != 0;
   if (ctx->lr_rows)
     MLFF_HIP(ctx, hipMalloc(&ctx->lr_zpart, sizeof(double) * lr_rows_groups(k) * ctx->blk));
+  if (ctx->lr_cluster) {
+    const size_t ns = (size_t)k * lr_cluster_members(ctx->blk) * 2;
+    MLFF_HIP(ctx, hipMalloc(&ctx->lr_zpart, sizeof(double) * ctx->lr_q * ctx->blk));
+    MLFF_HIP(ctx, hipMalloc(&ctx->lr_slots, sizeof(unsigned long long) * ns));
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->lr_slots, 0, sizeof(unsigned long long) * ns, ctx->stream));
+    MLFF_HIP(ctx, hipMalloc(&ctx->lr_fault, sizeof(int)));
+    MLFF_HIP(ctx, hipMemsetAsync(ctx->lr_fault, 0, sizeof(int), ctx->stream));
+    ctx->lr_epoch = 0;
+  }
   return MLFF_OK;
 }
 
@@ -788,6 +807,11 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
     if (ctx->lr_rows) {
       launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
                            1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold);
+    } else if (ctx->lr_cluster) {
+      launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, ctx->r, ctx->z, ctx->nrows,
+                              ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s,
+                              ctx->lr_zpart, ctx->lr_slots, ++ctx->lr_epoch, &ctx->st->status,
+                              fold);
     } else {
       launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status,
                         s, fold);
@@ -961,7 +985,7 @@ int mlff_ctx_destroy(mlff_ctx *ctx) {
   for (void *p : {(void *)ctx->K, (void *)ctx->x, (void *)ctx->r, (void *)ctx->z, (void *)ctx->q,
                   (void *)ctx->b, (void *)ctx->p_full, (void *)ctx->xg, (void *)ctx->part,
                   (void *)ctx->st, (void *)ctx->trace, (void *)ctx->T, (void *)ctx->tpart_base,
-                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->lr_zpart, (void *)ctx->gb})
+                  (void *)ctx->perm, (void *)ctx->dwork, (void *)ctx->pivflag, (void *)ctx->prow, (void *)ctx->zpart, (void *)ctx->lr_zpart, (void *)ctx->lr_slots, (void *)ctx->lr_fault, (void *)ctx->gb})
     dev_free(p);
   for (const auto &c : ctx->scratch_chunks) dev_free(c.p);
   ctx->scratch_chunks.clear();
@@ -1410,13 +1434,15 @@ int mlff_precon_apply_traffic(mlff_ctx *ctx, int *one_pass_out, double *bytes_ou
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   const double N = (double)ctx->blk, n = (double)ctx->nrows, k = (double)ctx->k;
-  const bool one = ctx->precon_kind != MLFF_PRECON_NONE && ctx->lr_rows;
-  if (one_pass_out) *one_pass_out = one ? 1 : 0;
+  const bool one = ctx->precon_kind != MLFF_PRECON_NONE && (ctx->lr_rows || ctx->lr_cluster);
+  if (one_pass_out) *one_pass_out = one ? (ctx->lr_cluster ? 2 : 1) : 0;
   if (bytes_out) {
     if (ctx->precon_kind == MLFF_PRECON_NONE)
       *bytes_out = 0.0;
     else if (one)
-      *bytes_out = 8.0 * k * N + 16.0 * (double)lr_rows_groups(ctx->k) * N + 24.0 * n;
+      *bytes_out = 8.0 * k * N +
+                   16.0 * (double)(ctx->lr_cluster ? ctx->lr_q : lr_rows_groups(ctx->k)) * N +
+                   24.0 * n;
     else
       *bytes_out = 16.0 * k * N + 24.0 * n;
   }
@@ -1440,10 +1466,22 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
     MLFF_HIP(ctx, hipMemcpyAsync(zd, rd, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
   } else {
     ctx->spec_t = false;  // tpart is reused below
-    if (ctx->lr_rows) {
-      launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p,
-                           1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart);
+    if (ctx->lr_rows || ctx->lr_cluster) {
+      if (ctx->lr_rows)
+        launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p,
+                             1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart);
+      else
+        launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, rd, zd, ctx->nrows,
+                                ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart,
+                                ctx->lr_slots, ++ctx->lr_epoch, ctx->lr_fault);
       MLFF_HIP(ctx, hipGetLastError());
+      if (ctx->lr_cluster) {
+        int fault = 0;
+        MLFF_HIP(ctx, hipMemcpyAsync(&fault, ctx->lr_fault, sizeof(int), hipMemcpyDeviceToHost, s));
+        MLFF_HIP(ctx, hipStreamSynchronize(s));
+        if (fault != 0)
+          return set_error(ctx, MLFF_ERR_HIP, "one-pass apply: a cluster hand-off timed out");
+      }
       if (ctx->nrows > 0)
         MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
       MLFF_HIP(ctx, hipStreamSynchronize(s));
@@ -1638,6 +1676,8 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
     }
     ctx->pcg_done = ctx->h_st->iters;
   }
+  if (ctx->h_st->status == ST_FAULT)
+    return set_error(ctx, MLFF_ERR_HIP, "PCG: a cluster hand-off of the one-pass apply timed out");
   if (status_out) *status_out = ctx->h_st->status;
   return MLFF_OK;
   MLFF_API_END(ctx)

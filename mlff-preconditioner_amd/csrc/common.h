@@ -26,7 +26,7 @@ __host__ __device__ inline int64_t round_up(int64_t a, int64_t b) { return (a + 
 
 // PCG status values kept on the device (status gating: every kernel of an
 // iteration returns immediately unless status == RUNNING).
-enum : int { ST_RUNNING = 0, ST_RECHECK = 1, ST_CONVERGED = 2, ST_MAXITER = 3 };
+enum : int { ST_RUNNING = 0, ST_RECHECK = 1, ST_CONVERGED = 2, ST_MAXITER = 3, ST_FAULT = 4 };
 
 // Device-resident scalars of the solver.  One instance per context.
 struct DevState {
@@ -232,7 +232,12 @@ struct mlff_ctx {
   int zsplit = 1;         // row splits of the T^T t GEMV
   double *zpart = nullptr;  // zsplit x blk partials
   bool lr_rows = false;        // one-pass low-rank apply (launch_lr_apply_rows), one rank
-  double *lr_zpart = nullptr;  // its lr_rows_groups(k) x blk partials
+  bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
+  int lr_q = 0;                // its clusters
+  double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials
+  unsigned long long *lr_slots = nullptr;  // cluster hand-off granules (k x C x 2)
+  unsigned lr_epoch = 0;       // per cluster launch, never 0 in a launch
+  int *lr_fault = nullptr;     // ST_FAULT when a cluster hand-off timed out (precon_apply)
   double *tpart = nullptr;       // = tpart_base + kVecGrid
   double *tpart_base = nullptr;
   bool spec_t = false;           // tpart already holds T r of the current r (merged collective)
@@ -360,6 +365,16 @@ void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double 
                           int64_t n, double sigma_p, double lam_inv, double *rho_part,
                           const int *status, hipStream_t s, double *zpart,
                           StopFold fold = StopFold{});
+// the one-pass apply for long rows (clusters of lr_cluster_members(ldt) workgroups, one per
+// CU, hand-offs of the per-row partial dots); lr_cluster_count = clusters resident at once
+bool lr_cluster_fits(int64_t ldt);
+int lr_cluster_members(int64_t ldt);
+int lr_cluster_count(int64_t ldt, int device);
+void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, const double *r,
+                             double *z, int64_t n, double sigma_p, double lam_inv,
+                             double *rho_part, const int *status, hipStream_t s, double *zpart,
+                             unsigned long long *slots, unsigned epoch, int *fault,
+                             StopFold fold = StopFold{});
 // part[ks * ldw + c] = sum_{j in slice ks} W[j, c] * (sum_sp tsrc[sp * tstride + j])
 void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *tsrc,
                          int tsplits, int64_t tstride, int ksplit, double *part,

@@ -529,8 +529,9 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
 }
 
 // z[j] = sigma_p lam_inv (r[j] - sum_{g < G} zpart[g, j]) for j < n, the G partials in
-// order (wave w sums its quarter, the quarters in order); rho partials r . z
-// (kVecGrid slots: one per workgroup, the rest zero)
+// order (wave w sums its quarter, the quarters in order); rho partials r . z in kVecGrid
+// slots: a workgroup takes the 64-column blocks blockIdx.x + i gridDim.x (grid <= kVecGrid)
+// and writes one slot, the slots past the grid are zero
 __global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart, int G, int64_t ldp,
                                                 const double *__restrict__ r,
                                                 double *__restrict__ z, int64_t n, double sigma_p,
@@ -539,35 +540,316 @@ __global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
   const int g0 = (G * w) / 4, g1 = (G * (w + 1)) / 4;
-  double s = 0.0;
-  if (j < n) {
-    // batches of 16 partials in flight, the last one predicated (no serial tail)
-    const double *pj = zpart + j;
-    for (int g = g0; g < g1; g += 16) {
-      double t[16];
+  double rho = 0.0;
+  for (int64_t jb = blockIdx.x; jb * 64 < n; jb += gridDim.x) {
+    const int64_t j = jb * 64 + lane;
+    double s = 0.0;
+    if (j < n) {
+      // batches of 16 partials in flight, the last one predicated (no serial tail)
+      const double *pj = zpart + j;
+      for (int g = g0; g < g1; g += 16) {
+        double t[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = g + u < g1 ? pj[(int64_t)(g + u) * ldp] : 0.0;
+        for (int u = 0; u < 16; ++u) t[u] = g + u < g1 ? pj[(int64_t)(g + u) * ldp] : 0.0;
 #pragma unroll
-      for (int u = 0; u < 16; ++u) s += t[u];
+        for (int u = 0; u < 16; ++u) s += t[u];
+      }
+    }
+    __syncthreads();  // sh of the previous block
+    sh[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && j < n) {
+      const double sv = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+      const double rv = r[j];
+      const double zv = sigma_p * (lam_inv * (rv - sv));
+      z[j] = zv;
+      rho = fma(rv, zv, rho);
     }
   }
-  sh[w][lane] = s;
-  __syncthreads();
   if (w == 0) {
-    double rv = 0.0, zv = 0.0;
-    if (j < n) {
-      const double sv = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
-      rv = r[j];
-      zv = sigma_p * (lam_inv * (rv - sv));
-      z[j] = zv;
-    }
-    const double rho = wave_sum(rv * zv);
-    if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = rho;
+    const double tot = wave_sum(rho);
+    if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = tot;
   }
   if (blockIdx.x == 0 && rho_part != nullptr)
     for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 256) rho_part[i] = 0.0;
+}
+
+static unsigned lr_fin_grid(int64_t n) {
+  const int64_t b = (n + 63) / 64;
+  return (unsigned)(b < kVecGrid ? b : kVecGrid);
+}
+
+// ---------------------------------------------------------------------------
+// One-pass low-rank apply for rows longer than one workgroup's registers (one rank,
+// N_loc up to kLcMaxC x 8192 columns: the N = 156510 nanotube system).  A row
+// is split over a CLUSTER of C workgroups (column segments of kLcSeg = 8192 columns, 64 KB:
+// 512 threads x 8 double2 in registers; r's and the partial z's segments in LDS), and the
+// Q = floor(CUs / C) clusters own contiguous row ranges.  Per row each member forms its
+// segment's partial dot (fixed-order block sum) and publishes it as two 8-byte {epoch, 32
+// bits} granules (relaxed agent-scope atomic stores, MI355X "R2" hand-off: the data is the
+// flag); D row-steps later every member's sync wave reads the C granule pairs of that row
+// until every tag equals the launch's epoch, sums the C partials in member order (the same
+// bits in every member) and the members accumulate z_seg += T[i, seg] t_i from the row still
+// held in registers.  D + L + 1 register buffers: row j (consumed), rows j + 1 … j + D - 1
+// (waiting for their partials), j + D (partial formed and published; loaded L steps
+// earlier), rows in flight up to j + D + L (loading): D row-steps of slack for the hand-off,
+// L steps between a row's load and its use.  A member that waits for more than ~1 s writes
+// ST_FAULT to `fault` and leaves (the host reports an error; a cluster can only stall if its
+// members are not all resident, which the host checks with the occupancy query before it
+// chooses this path).
+constexpr int kLcThreads = 512;
+constexpr int kLcSeg = 8192;
+constexpr int kLcM = kLcSeg / (2 * kLcThreads);  // 8 double2 per thread per row
+constexpr int kLcMaxC = 24;  // members per cluster: C = 20 (N = 156510) wins 31 %, C = 62
+                             // (N = 505050) loses 8 % to the two-pass apply (the hand-off of
+                             // the slowest of 62 members sets every step's pace)
+constexpr int kLcD = 2, kLcL = 1;
+
+__device__ __forceinline__ void lc_load(d2 (&buf)[kLcM], const double *T, int64_t ldt,
+                                        int64_t row, int64_t i1, int64_t c0, int segbytes) {
+  const bool ok = row < i1;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double *>(T + (ok ? row : 0) * ldt + c0), 0, ok ? segbytes : 0, 0x00020000);
+  const int voff = (int)threadIdx.x * 16;
+#pragma unroll
+  for (int m = 0; m < kLcM; ++m)
+    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * kLcThreads * 16, 2));
+}
+
+struct LcArgs {
+  const double *T;
+  int64_t ldt, c0;
+  int i0, i1;  // the cluster's rows (32-bit: scalar compares in the row loop)
+  int segbytes, C, c;
+  unsigned long long *slots;  // k x C x 2 granules
+  unsigned epoch;
+  int *fault;
+};
+
+// wave 0: the C partials of row `row` (granule pairs), summed in member order; false on
+// timeout.  x0 / x1: this lane's granules as loaded at the start of the step (before the
+// step's row loads, so the first look does not queue behind them); re-polled until every
+// tag equals the epoch.  Every lane returns the same t.
+__device__ __forceinline__ unsigned long long *lc_granule(const LcArgs &a, int row) {
+  const int lane = threadIdx.x & 63;
+  return a.slots + ((size_t)row * a.C + (lane < a.C ? lane : 0)) * 2;
+}
+
+__device__ __forceinline__ bool lc_consume(const LcArgs &a, int row, unsigned long long x0,
+                                           unsigned long long x1, double &t) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long *g = lc_granule(a, row);
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    const bool ok = lane >= a.C ||
+                    ((unsigned)(x0 >> 32) == a.epoch && (unsigned)(x1 >> 32) == a.epoch);
+    if (__all(ok)) break;
+    if (wall_clock64() - t0 > 100000000ull) return false;  // ~1 s at 100 MHz
+    __builtin_amdgcn_s_sleep(1);
+    if (lane < a.C) {
+      x0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const double v = __builtin_bit_cast(double, (x1 << 32) | (x0 & 0xffffffffull));
+  double s = 0.0;
+  for (int m = 0; m < a.C; ++m) s += __shfl(v, m, 64);
+  t = s;
+  return true;
+}
+
+// One row-step at row j with NB register buffers, split between the two kinds of wave (a
+// wave-uniform branch: both execute one barrier per step).  Row waves (0-7) hold the row
+// segment: b0 = row j (consumed), bp = row j + D (its partial formed), bl = row j + D + L
+// (loading); the rows between wait for their partials or are in flight.  The sync
+// wave (8) polls, sums and publishes: its hand-off loads never queue behind row loads, and
+// the row waves' code holds no hand-off load a counter wait could be charged for.
+template <int D, int L>
+__device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[kLcM],
+                                            d2 (&b2)[kLcM], d2 (&b3)[kLcM], const d2 *r_sh,
+                                            d2 *z_sh, double *red, const double *tsh,
+                                            const int *bail) {
+  const int w = threadIdx.x >> 6;
+  const int jp = j + D;
+  lc_load(b3, a.T, a.ldt, j + D + L, a.i1, a.c0, a.segbytes);
+  if (jp >= a.i0 && jp < a.i1) {
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int m = 0; m < kLcM; ++m) {
+      const d2 rv = r_sh[threadIdx.x + kLcThreads * m];
+      a0 = fma(b2[m].x, rv.x, a0);
+      a1 = fma(b2[m].y, rv.y, a1);
+    }
+    const double sw = wave_sum(a0 + a1);
+    if ((threadIdx.x & 63) == 0) red[(jp & 1) * 8 + w] = sw;
+  }
+  __syncthreads();
+  if (*bail) return false;
+  if (j >= a.i0 && j < a.i1) {
+    const double t = tsh[j & 1];
+#pragma unroll
+    for (int m = 0; m < kLcM; ++m) {
+      d2 zv = z_sh[threadIdx.x + kLcThreads * m];
+      zv.x = fma(b0[m].x, t, zv.x);
+      zv.y = fma(b0[m].y, t, zv.y);
+      z_sh[threadIdx.x + kLcThreads * m] = zv;
+    }
+  }
+  return true;
+}
+
+template <int D>
+__device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const double *red,
+                                             double *tsh, int *bail) {
+  const int lane = threadIdx.x & 63;
+  const int jp = j + D;
+  if (j >= a.i0 && j < a.i1) {
+    unsigned long long x0 = 0, x1 = 0;
+    if (lane < a.C) {
+      unsigned long long *g = lc_granule(a, j);
+      x0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    double t;
+    const bool ok = lc_consume(a, j, x0, x1, t);
+    if (lane == 0) {
+      tsh[j & 1] = t;
+      *bail = ok ? 0 : 1;
+    }
+  }
+  __syncthreads();
+  if (*bail) return false;
+  if (jp >= a.i0 && jp < a.i1 && lane == 0) {
+    const double *q = red + (jp & 1) * 8;
+    const double ps = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+    const unsigned long long bits = __builtin_bit_cast(unsigned long long, ps);
+    unsigned long long *g = a.slots + ((size_t)jp * a.C + a.c) * 2;
+    __hip_atomic_store(g, ((unsigned long long)a.epoch << 32) | (bits & 0xffffffffull),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, ((unsigned long long)a.epoch << 32) | (bits >> 32), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
+template <int D, int L, int U>
+__device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D + L + 1][kLcM],
+                                             const d2 *r_sh, d2 *z_sh, double *red,
+                                             const double *tsh, const int *bail) {
+  constexpr int NB = D + L + 1;
+  if constexpr (U == NB) {
+    return true;
+  } else {
+    if (!lc_row_step<D, L>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh, red,
+                           tsh, bail))
+      return false;
+    return lc_row_steps<D, L, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
+  }
+}
+
+template <int D, int L>
+__global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__restrict__ T, int64_t ldt,
+                                                           int64_t k, int C, int rpc,
+                                                           const double *__restrict__ r,
+                                                           double *__restrict__ zpart,
+                                                           unsigned long long *slots,
+                                                           unsigned epoch, int *fault,
+                                                           const int *__restrict__ status,
+                                                           StopFold fold) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ d2 r_sh[kLcM * kLcThreads];
+  __shared__ d2 z_sh[kLcM * kLcThreads];
+  __shared__ double red[16];
+  __shared__ double tsh[2];
+  __shared__ int bail;
+  LcArgs a;
+  a.T = T;
+  a.ldt = ldt;
+  a.C = C;
+  const int q = blockIdx.x / C;
+  a.c = blockIdx.x % C;
+  a.c0 = (int64_t)a.c * kLcSeg;
+  const int64_t segcols = ldt - a.c0 < kLcSeg ? ldt - a.c0 : kLcSeg;
+  a.segbytes = (int)(segcols * 8);
+  a.i0 = q * rpc;
+  a.i1 = a.i0 + rpc < (int)k ? a.i0 + rpc : (int)k;
+  a.slots = slots;
+  a.epoch = epoch;
+  a.fault = fault;
+  const bool row_wave = threadIdx.x < kLcThreads;
+  constexpr int NB = D + L + 1;
+  if (row_wave) {
+    d2 B[NB][kLcM];
+    d2 rv[kLcM];
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double *>(r + a.c0), 0, a.segbytes, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < kLcM; ++m)
+      rv[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(
+                                         rs, (int)threadIdx.x * 16, m * kLcThreads * 16, 0));
+#pragma unroll
+    for (int t = 0; t < L; ++t)  // rows i0 .. i0 + L - 1 (the steps start at j = i0 - D)
+      lc_load(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
+    if (!stop_prologue_wide(fold, red)) return;
+#pragma unroll
+    for (int m = 0; m < kLcM; ++m) {
+      r_sh[threadIdx.x + kLcThreads * m] = rv[m];
+      z_sh[threadIdx.x + kLcThreads * m] = d2{0.0, 0.0};
+    }
+    __syncthreads();  // bail = 0 (sync wave)
+    bool ok = true;
+    for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
+      ok = lc_row_steps<D, L, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
+    if (!ok) return;
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+        zpart + (int64_t)q * ldt + a.c0, 0, a.segbytes, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < kLcM; ++m)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + kLcThreads * m]),
+                                             out, (int)threadIdx.x * 16, m * kLcThreads * 16, 0);
+  } else {
+    if (!stop_prologue_wide(fold, red)) return;
+    if (threadIdx.x == kLcThreads) bail = 0;
+    __syncthreads();
+    bool ok = true;
+    for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
+      for (int u = 0; u < NB && ok; ++u) ok = lc_sync_step<D>(a, j + u, red, tsh, &bail);
+    if (!ok && threadIdx.x == kLcThreads)
+      __hip_atomic_store(fault, ST_FAULT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+int lr_cluster_members(int64_t ldt) { return (int)((ldt + kLcSeg - 1) / kLcSeg); }
+bool lr_cluster_fits(int64_t ldt) { return ldt > 0 && ldt % 2 == 0 && lr_cluster_members(ldt) <= kLcMaxC; }
+
+// clusters of C members that the device keeps resident all at once (0: none)
+int lr_cluster_count(int64_t ldt, int device) {
+  const int C = lr_cluster_members(ldt);
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lr_cluster<kLcD, kLcL>, kLcThreads + 64, 0) !=
+      hipSuccess)
+    return 0;
+  const int resident = cus * std::min(per_cu, 1);  // one member per CU
+  return resident / C;
+}
+
+void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, const double *r,
+                             double *z, int64_t n, double sigma_p, double lam_inv,
+                             double *rho_part, const int *status, hipStream_t s, double *zpart,
+                             unsigned long long *slots, unsigned epoch, int *fault,
+                             StopFold fold) {
+  const int C = lr_cluster_members(ldt);
+  const int rpc = (int)((k + Q - 1) / Q);
+  // hand-off slack D = 2 steps, load distance L = 1 (D = 1, L = 2: apply 3.95 -> 4.22 ms at
+  // N = 156510; the hand-off, not the load latency, sets the pace)
+  hipLaunchKernelGGL((k_lr_cluster<kLcD, kLcL>), dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), 0, s,
+                     T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, status, fold);
+  if (n > 0)
+    hipLaunchKernelGGL(k_lr_fin, dim3(lr_fin_grid(n)), dim3(256), 0, s, zpart, Q, ldt, r,
+                       z, n, sigma_p, lam_inv, rho_part, status);
 }
 
 void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
@@ -590,7 +872,7 @@ void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double 
   else
     hipLaunchKernelGGL(k_lr_rows<16>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
   if (n > 0)
-    hipLaunchKernelGGL(k_lr_fin, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, zpart, G, ldt, r, z,
+    hipLaunchKernelGGL(k_lr_fin, dim3(lr_fin_grid(n)), dim3(256), 0, s, zpart, G, ldt, r, z,
                        n, sigma_p, lam_inv, rho_part, status);
 }
 

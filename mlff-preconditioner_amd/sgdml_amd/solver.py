@@ -259,11 +259,13 @@ class KernelSolver:
         self._call("mlff_precon_info", ctypes.byref(kind), ctypes.byref(k))
         return kind.value, k.value
 
-    def precon_apply_traffic(self) -> tuple[bool, float]:
-        """(one_pass, algorithmic HBM bytes of one low-rank apply on this rank)."""
+    def precon_apply_traffic(self) -> tuple[int, float]:
+        """(form, algorithmic HBM bytes of one low-rank apply on this rank); form 0 = two
+        passes over the panel, 1 = one pass with a row per workgroup, 2 = one pass with a
+        row per cluster of workgroups."""
         one, b = ctypes.c_int(), ctypes.c_double()
         self._call("mlff_precon_apply_traffic", ctypes.byref(one), ctypes.byref(b))
-        return bool(one.value), b.value
+        return one.value, b.value
 
     def precon_apply(self, r_local: np.ndarray) -> np.ndarray:
         r_local = np.ascontiguousarray(r_local, dtype=np.float64)

@@ -296,13 +296,17 @@ def test_call_order_and_argument_errors(sg):
         assert res.info == 0
 
 
-@pytest.mark.parametrize("n,k", [(1000, 3), (1000, 800), (5000, 1031), (11000, 900),
-                                 (15540, 2701)])
-def test_one_pass_lowrank_apply(sg, monkeypatch, n, k):
+@pytest.mark.parametrize("n,k,clusters", [(1000, 3, 0), (1000, 800, 0), (5000, 1031, 0),
+                                          (11000, 900, 0), (15540, 2701, 0),
+                                          (20000, 400, 0), (40000, 301, 0), (40000, 301, 3),
+                                          (70000, 40, 7)])
+def test_one_pass_lowrank_apply(sg, monkeypatch, n, k, clusters):
     """The one-pass low-rank apply (k_lr_rows + k_lr_fin: each panel row read once, t_i
     kept in the workgroup) against the two-pass apply (T r, then T^T t) and NumPy, on
     every register-tile width (M = 4, 8, 12, 16 double2 per thread), ragged row groups
-    (k = 1031: 207 groups of 5 rows, the last of 1) and k < one row per workgroup.  Then a
+    (k = 1031: 207 groups of 5 rows, the last of 1) and k < one row per workgroup; rows
+    longer than 16384 columns take the cluster form (k_lr_cluster: C = 3, 5, 9 workgroups per
+    row, all resident clusters or MLFF_LR_CLUSTERS of them, ragged row ranges).  Then a
     PCG solve on both applies, held to the chaotic-regime contract of tests/parity.py (a
     random panel makes a poor preconditioner: the residual curves of two summation orders
     part after ~15 iterations, as they do on the CPU).
@@ -313,12 +317,16 @@ def test_one_pass_lowrank_apply(sg, monkeypatch, n, k):
     L = rng.standard_normal((k, n)) * 0.05
     r = rng.standard_normal(n)
     out = {}
+    if clusters:
+        monkeypatch.setenv("MLFF_LR_CLUSTERS", str(clusters))
     for mode in ("0", "1"):
         monkeypatch.setenv("MLFF_LR_ROWS", mode)
         with sg.KernelSolver(n) as s:
             s.gen_rbf(X, length_scale=0.2)
             s.set_operator(1.0, lam)
             s.precon_lowrank(L)
+            form, _ = s.precon_apply_traffic()
+            assert form == (0 if mode == "0" else (1 if n <= 16384 else 2))
             T = s.precon_panel()
             z = s.precon_apply(r)
             res = s.pcg(b, tol=1e-8, maxiter=5 * n)
