@@ -1467,13 +1467,15 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
   } else {
     ctx->spec_t = false;  // tpart is reused below
     if (ctx->lr_rows || ctx->lr_cluster) {
-      if (ctx->lr_rows)
+      if (ctx->lr_rows) {
         launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p,
                              1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart);
-      else
+      } else {
+        MLFF_HIP(ctx, hipMemsetAsync(ctx->lr_fault, 0, sizeof(int), s));
         launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, rd, zd, ctx->nrows,
                                 ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart,
                                 ctx->lr_slots, ++ctx->lr_epoch, ctx->lr_fault);
+      }
       MLFF_HIP(ctx, hipGetLastError());
       if (ctx->lr_cluster) {
         int fault = 0;

@@ -625,6 +625,7 @@ struct LcArgs {
   unsigned long long *slots;  // k x C x 2 granules
   unsigned epoch;
   int *fault;
+  int mute;  // test hook: this member never publishes (its cluster times out)
 };
 
 // wave 0: the C partials of row `row` (granule pairs), summed in member order; false on
@@ -720,7 +721,7 @@ __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const doubl
   }
   __syncthreads();
   if (*bail) return false;
-  if (jp >= a.i0 && jp < a.i1 && lane == 0) {
+  if (jp >= a.i0 && jp < a.i1 && lane == 0 && !a.mute) {
     const double *q = red + (jp & 1) * 8;
     const double ps = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     const unsigned long long bits = __builtin_bit_cast(unsigned long long, ps);
@@ -755,6 +756,7 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
                                                            double *__restrict__ zpart,
                                                            unsigned long long *slots,
                                                            unsigned epoch, int *fault,
+                                                           int mute_block,
                                                            const int *__restrict__ status,
                                                            StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
@@ -777,6 +779,7 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
   a.slots = slots;
   a.epoch = epoch;
   a.fault = fault;
+  a.mute = (int)blockIdx.x == mute_block;
   const bool row_wave = threadIdx.x < kLcThreads;
   constexpr int NB = D + L + 1;
   if (row_wave) {
@@ -845,8 +848,12 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
   const int rpc = (int)((k + Q - 1) / Q);
   // hand-off slack D = 2 steps, load distance L = 1 (D = 1, L = 2: apply 3.95 -> 4.22 ms at
   // N = 156510; the hand-off, not the load latency, sets the pace)
+  // MLFF_LC_TEST_MUTE=<b>: workgroup b never publishes, so its cluster's hand-offs time out
+  // (tests of the ~1 s fault bail-out; never set in production)
+  const char *mute_env = std::getenv("MLFF_LC_TEST_MUTE");
+  const int mute = mute_env ? std::atoi(mute_env) : -1;
   hipLaunchKernelGGL((k_lr_cluster<kLcD, kLcL>), dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), 0, s,
-                     T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, status, fold);
+                     T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, mute, status, fold);
   if (n > 0)
     hipLaunchKernelGGL(k_lr_fin, dim3(lr_fin_grid(n)), dim3(256), 0, s, zpart, Q, ldt, r,
                        z, n, sigma_p, lam_inv, rho_part, status);

@@ -340,3 +340,31 @@ def test_one_pass_lowrank_apply(sg, monkeypatch, n, k, clusters):
     assert res0.info == res1.info == 0
     assert_pcg_parity(res1.iters, res1.trace[1:], res1.x, res0.iters, res0.trace[1:], res0.x,
                       mode="chaotic", x_tol=1e-6)
+
+
+def test_cluster_apply_fault_bails_out(sg, monkeypatch):
+    """A cluster member that never publishes its partial (test hook MLFF_LC_TEST_MUTE) makes
+    its cluster's hand-offs time out: the members leave after ~1 s instead of hanging the GPU,
+    the apply and the PCG fail with an error, and the context stays usable (the next apply,
+    without the hook, is correct)."""
+    n, k, lam = 40000, 301, 1.0
+    X, b = _rbf(n)
+    rng = np.random.default_rng(5)
+    L = rng.standard_normal((k, n)) * 0.05
+    r = rng.standard_normal(n)
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, length_scale=0.2)
+        s.set_operator(1.0, lam)
+        s.precon_lowrank(L)
+        assert s.precon_apply_traffic()[0] == 2
+        T = s.precon_panel()
+        monkeypatch.setenv("MLFF_LC_TEST_MUTE", "3")
+        with pytest.raises(Exception, match="timed out"):
+            s.precon_apply(r)
+        with pytest.raises(Exception, match="timed out"):
+            s.pcg(b, tol=1e-8, maxiter=50)
+        monkeypatch.delenv("MLFF_LC_TEST_MUTE")
+        z = s.precon_apply(r)
+    zref = (r - T.T @ (T @ r)) / lam
+    sgn = np.sign(np.dot(z, zref))
+    assert np.linalg.norm(z - sgn * zref) <= 1e-12 * np.linalg.norm(zref)
