@@ -138,3 +138,41 @@ def test_config4_nanotube_pivchol_rank1024_eight_ranks(sg, nanotube):
     err = np.abs(z - ref[2]).max() / np.abs(ref[2]).max()
     print(f"configs[4] Woodbury apply: max |dz| / max |z| = {err:.3e}")
     assert err <= 1e-11
+
+
+@pytest.mark.timeout(900)
+def test_nanotube_cluster_apply_solve(sg, monkeypatch):
+    """The configs[1] geometry with one more training point (M = 15, N = 16650): its panel
+    rows exceed one workgroup's registers, so the drop-in's default low-rank apply is the
+    cluster one-pass form (k_lr_cluster, C = 3).  The rank-2850 pivoted-Cholesky PCG solve with
+    it converges to 1e-6 with the true residual recomputed by the oracle operator, and takes
+    the iteration count of the two-pass apply to within the chaotic-regime slack (the two
+    applies sum in different orders).  Reference: iterative_cholesky.py:115-150."""
+    from oracle.sgdml import kernel_matvec_matrix_free
+    from sgdml_amd import synthetic
+
+    ds = synthetic.nanotube_like(15, seed=0)
+    Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+    y, _ = synthetic.labels(ds["F"])
+    perms = np.arange(N_ATOMS)[None, :]
+    n, k = y.size, 2850
+    assert n == 16650
+    out = {}
+    for mode in ("0", "default"):
+        if mode == "0":
+            monkeypatch.setenv("MLFF_LR_ROWS", "0")
+        else:
+            monkeypatch.delenv("MLFF_LR_ROWS", raising=False)
+        with sg.KernelSolver(n) as s:
+            s.sgdml_operator(Rd, Rdd, perms, SIG)
+            s.set_operator(-1.0, LAM)
+            s.precon_pivchol(k)
+            form, _ = s.precon_apply_traffic()
+            assert form == (0 if mode == "0" else 2)
+            out[mode] = s.pcg(y, tol=1e-6, maxiter=5 * n)
+    r0, r1 = out["0"], out["default"]
+    assert r0.info == 0 and r1.info == 0
+    assert abs(r1.iters - r0.iters) <= max(3, 0.05 * r0.iters), (r1.iters, r0.iters)
+    Ax = -kernel_matvec_matrix_free(Rd, Rdd, perms, SIG, r1.x) + LAM * r1.x
+    relres = np.linalg.norm(y - Ax) / np.linalg.norm(y)
+    assert relres <= 1.05e-6, relres
