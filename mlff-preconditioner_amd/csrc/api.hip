@@ -318,6 +318,12 @@ int dot_sync(mlff_ctx *ctx, const double *a, const double *b, double *out) {
   return MLFF_OK;
 }
 
+// epoch of the next cluster-apply launch: never 0 (the value of a cleared hand-off slot)
+unsigned next_lr_epoch(mlff_ctx *c) {
+  if (++c->lr_epoch == 0) ++c->lr_epoch;
+  return c->lr_epoch;
+}
+
 double *rho_part(mlff_ctx *c) { return c->part + 0 * kMaxPart; }
 double *pq_part(mlff_ctx *c) { return c->part + 1 * kMaxPart; }
 double *rr_part(mlff_ctx *c) { return c->part + 2 * kMaxPart; }
@@ -810,7 +816,7 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
     } else if (ctx->lr_cluster) {
       launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, ctx->r, ctx->z, ctx->nrows,
                               ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s,
-                              ctx->lr_zpart, ctx->lr_slots, ++ctx->lr_epoch, &ctx->st->status,
+                              ctx->lr_zpart, ctx->lr_slots, next_lr_epoch(ctx), &ctx->st->status,
                               fold);
     } else {
       launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status,
@@ -1474,7 +1480,7 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
         MLFF_HIP(ctx, hipMemsetAsync(ctx->lr_fault, 0, sizeof(int), s));
         launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, rd, zd, ctx->nrows,
                                 ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s, ctx->lr_zpart,
-                                ctx->lr_slots, ++ctx->lr_epoch, ctx->lr_fault);
+                                ctx->lr_slots, next_lr_epoch(ctx), ctx->lr_fault);
       }
       MLFF_HIP(ctx, hipGetLastError());
       if (ctx->lr_cluster) {
