@@ -259,7 +259,9 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local);
  * shared by a cluster of workgroups (longer rows: k_lr_cluster + k_lr_fin), 0 for the
  * two-pass T r / T^T t apply; bytes_out = its algorithmic HBM bytes per apply (one pass:
  * 8 k N + 16 G N + 24 N, G = row groups or clusters; two passes: 16 k N + 24 N).  A cluster
- * hand-off that times out fails the call with MLFF_ERR_HIP.  No reference counterpart. */
+ * whose hand-offs time out (its workgroups not all resident, ~1 s) is abandoned: that apply
+ * (or PCG iteration) is redone with two passes and the context keeps the two-pass form (this
+ * call then reports 0).  No reference counterpart. */
 int mlff_precon_apply_traffic(mlff_ctx *ctx, int *one_pass_out, double *bytes_out);
 /* the k x nrows Woodbury panel T (or B / P for Nystrom) of this rank */
 int mlff_precon_get_panel(mlff_ctx *ctx, double *T_local, int64_t ld_out);

@@ -1487,8 +1487,14 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
         int fault = 0;
         MLFF_HIP(ctx, hipMemcpyAsync(&fault, ctx->lr_fault, sizeof(int), hipMemcpyDeviceToHost, s));
         MLFF_HIP(ctx, hipStreamSynchronize(s));
-        if (fault != 0)
-          return set_error(ctx, MLFF_ERR_HIP, "one-pass apply: a cluster hand-off timed out");
+        if (fault != 0) {  // hand-offs timed out (members not all resident): two passes
+          ctx->lr_cluster = false;
+          ctx->lr_fallbacks += 1;
+          launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, rd, ctx->tpart, nullptr, s);
+          launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, rd, zd, ctx->nrows,
+                          ctx->sigma_p, 1.0 / ctx->lam, nullptr, nullptr, s, ctx->zpart, ctx->zsplit);
+          MLFF_HIP(ctx, hipGetLastError());
+        }
       }
       if (ctx->nrows > 0)
         MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
@@ -1653,6 +1659,16 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
     }
     MLFF_HIP(ctx, hipGetLastError());
     MLFF_TRY(poll_state(ctx));
+    if (ctx->h_st->status == ST_FAULT && ctx->lr_cluster) {
+      // the cluster apply could not complete its hand-offs (its workgroups were not all
+      // resident, e.g. another process's kernels held CUs): nothing of iteration iters + 1
+      // was written past its (idempotent) stop test, so the solve continues from there on
+      // the two-pass apply
+      ctx->lr_cluster = false;
+      ctx->lr_fallbacks += 1;
+      ctx->h_st->status = ST_RUNNING;
+      MLFF_HIP(ctx, hipMemsetAsync(&ctx->st->status, 0, sizeof(int), s));  // ST_RUNNING
+    }
     const int64_t done_now = ctx->h_st->iters;
     if (ctx->timing.on && c0 && c1) {
       for (const GemvMark &mk : marks) {

@@ -238,6 +238,7 @@ struct mlff_ctx {
   unsigned long long *lr_slots = nullptr;  // cluster hand-off granules (k x C x 2)
   unsigned lr_epoch = 0;       // per cluster launch, never 0 in a launch
   int *lr_fault = nullptr;     // ST_FAULT when a cluster hand-off timed out (precon_apply)
+  int lr_fallbacks = 0;        // cluster applies that timed out and fell back to two passes
   double *tpart = nullptr;       // = tpart_base + kVecGrid
   double *tpart_base = nullptr;
   bool spec_t = false;           // tpart already holds T r of the current r (merged collective)

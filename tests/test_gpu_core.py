@@ -342,11 +342,12 @@ def test_one_pass_lowrank_apply(sg, monkeypatch, n, k, clusters):
                       mode="chaotic", x_tol=1e-6)
 
 
-def test_cluster_apply_fault_bails_out(sg, monkeypatch):
+def test_cluster_apply_fault_falls_back(sg, monkeypatch):
     """A cluster member that never publishes its partial (test hook MLFF_LC_TEST_MUTE) makes
     its cluster's hand-offs time out: the members leave after ~1 s instead of hanging the GPU,
-    the apply and the PCG fail with an error, and the context stays usable (the next apply,
-    without the hook, is correct)."""
+    the apply is redone with two passes (correct z), the context stays on the two-pass form;
+    in a PCG solve the faulted iteration is re-run with two passes and the solve converges to
+    the result of a two-pass solve."""
     n, k, lam = 40000, 301, 1.0
     X, b = _rbf(n)
     rng = np.random.default_rng(5)
@@ -356,15 +357,21 @@ def test_cluster_apply_fault_bails_out(sg, monkeypatch):
         s.gen_rbf(X, length_scale=0.2)
         s.set_operator(1.0, lam)
         s.precon_lowrank(L)
-        assert s.precon_apply_traffic()[0] == 2
         T = s.precon_panel()
+        ref = s.pcg(b, tol=1e-8, maxiter=2000)  # cluster form, no fault
         monkeypatch.setenv("MLFF_LC_TEST_MUTE", "3")
-        with pytest.raises(Exception, match="timed out"):
-            s.precon_apply(r)
-        with pytest.raises(Exception, match="timed out"):
-            s.pcg(b, tol=1e-8, maxiter=50)
-        monkeypatch.delenv("MLFF_LC_TEST_MUTE")
+        s.precon_lowrank(L)  # a fresh panel: the cluster form again
+        assert s.precon_apply_traffic()[0] == 2
         z = s.precon_apply(r)
+        assert s.precon_apply_traffic()[0] == 0
+        s.precon_lowrank(L)
+        assert s.precon_apply_traffic()[0] == 2
+        res = s.pcg(b, tol=1e-8, maxiter=2000)
+        assert s.precon_apply_traffic()[0] == 0
+        monkeypatch.delenv("MLFF_LC_TEST_MUTE")
     zref = (r - T.T @ (T @ r)) / lam
     sgn = np.sign(np.dot(z, zref))
     assert np.linalg.norm(z - sgn * zref) <= 1e-12 * np.linalg.norm(zref)
+    assert ref.info == 0 and res.info == 0
+    assert_pcg_parity(res.iters, res.trace[1:], res.x, ref.iters, ref.trace[1:], ref.x,
+                      mode="chaotic", x_tol=1e-6)
