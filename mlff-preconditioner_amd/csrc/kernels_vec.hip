@@ -582,7 +582,7 @@ static unsigned lr_fin_grid(int64_t n) {
 
 // ---------------------------------------------------------------------------
 // One-pass low-rank apply for rows longer than one workgroup's registers (one rank,
-// N_loc up to kLcMaxC x 8192 columns: the N = 156510 nanotube system).  A row
+// N_loc up to kLcMaxC x 8192 columns, e.g. the N = 156510 nanotube system).  A row
 // is split over a CLUSTER of C workgroups (column segments of kLcSeg = 8192 columns, 64 KB:
 // 512 threads x 8 double2 in registers; r's and the partial z's segments in LDS), and the
 // Q = floor(CUs / C) clusters own contiguous row ranges.  Per row each member forms its
@@ -601,9 +601,10 @@ static unsigned lr_fin_grid(int64_t n) {
 constexpr int kLcThreads = 512;
 constexpr int kLcSeg = 8192;
 constexpr int kLcM = kLcSeg / (2 * kLcThreads);  // 8 double2 per thread per row
-constexpr int kLcMaxC = 24;  // members per cluster: C = 20 (N = 156510) wins 31 %, C = 62
-                             // (N = 505050) loses 8 % to the two-pass apply (the hand-off of
-                             // the slowest of 62 members sets every step's pace)
+constexpr int kLcMaxC = 44;  // members per cluster.  Apply time against two passes
+                             // (nanotube, rule-of-thumb k): C = 3..14 -21..-41 %, C = 20
+                             // -31 %, C = 28 -27 %, C = 41 -8 %, C = 62 (N = 505050) +14 %
+                             // (the hand-off of the slowest of C members paces each step)
 constexpr int kLcD = 2, kLcL = 1;
 
 __device__ __forceinline__ void lc_load(d2 (&buf)[kLcM], const double *T, int64_t ldt,
@@ -824,7 +825,13 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
 }
 
 int lr_cluster_members(int64_t ldt) { return (int)((ldt + kLcSeg - 1) / kLcSeg); }
-bool lr_cluster_fits(int64_t ldt) { return ldt > 0 && ldt % 2 == 0 && lr_cluster_members(ldt) <= kLcMaxC; }
+bool lr_cluster_fits(int64_t ldt) {
+  static const int maxc = [] {  // MLFF_LC_MAXC: sweeps of the member cap (at most 64: one wave polls)
+    const char *e = std::getenv("MLFF_LC_MAXC");
+    return e ? std::min(64, std::max(1, std::atoi(e))) : kLcMaxC;
+  }();
+  return ldt > 0 && ldt % 2 == 0 && lr_cluster_members(ldt) <= maxc;
+}
 
 // clusters of C members that the device keeps resident all at once (0: none)
 int lr_cluster_count(int64_t ldt, int device) {
