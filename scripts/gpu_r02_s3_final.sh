@@ -5,7 +5,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out
-L=gpurun_out/r02_s3_final.log
+L=gpurun_out/r02_s3_final${TAG:-}.log
 : > $L
 step() {
   local t=$1 name=$2; shift 2
