@@ -685,7 +685,7 @@ hipEvent_t timing_event(mlff_ctx *ctx) {
   Timing &t = ctx->timing;
   if (t.used >= t.ev.size()) {
     hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, timing_event_flags()) != hipSuccess) return nullptr;
     t.ev.push_back(e);
   }
   return t.ev[t.used++];

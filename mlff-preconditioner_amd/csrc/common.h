@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/mlffpcg.h"
@@ -142,6 +143,15 @@ struct StopFold {
   double *trace = nullptr;
   long long it = 0;
 };
+
+// flags of the timing-only events (stamps read after a stream synchronisation): no
+// system-scope fence, so recording one does not write back and invalidate the caches
+// between the kernels it brackets (MLFF_EVENT_FENCE=1 restores the default, for A/B)
+inline unsigned timing_event_flags() {
+  static const unsigned f = std::getenv("MLFF_EVENT_FENCE") ? hipEventDefault
+                                                            : hipEventDisableSystemFence;
+  return f;
+}
 
 struct Timing {
   bool on = false;

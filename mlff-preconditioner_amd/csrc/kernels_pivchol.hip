@@ -495,7 +495,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   stamps.reserve((size_t)(k / kStampEvery + 2));
   auto stamp = [&]() {
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) == hipSuccess) {
+    if (hipEventCreateWithFlags(&e, timing_event_flags()) == hipSuccess) {
       hipEventRecord(e, s);
       stamps.push_back(e);
     }
