@@ -289,6 +289,9 @@ int mlff_pcg_get_x(mlff_ctx *ctx, double *x_local);
 int mlff_pcg_get_trace(mlff_ctx *ctx, double *trace_out, int64_t n);
 
 /* ---- timing (device time of the hot kernels, hipEvents on the ctx stream) --- */
+/* on = 0: off; 1: every PCG iteration bracketed; n > 1: every n-th iteration only (each
+ * event costs GPU time between the kernels it brackets; the per-kernel averages are over
+ * the bracketed iterations, whose count is the operator count of mlff_timing_read) */
 int mlff_timing_enable(mlff_ctx *ctx, int on);
 /* accumulated milliseconds and launch counts of the K mat-vec (GEMV) and of the
  * whole PCG iteration since the last reset */

@@ -702,7 +702,7 @@ struct GemvMark {
 constexpr size_t kNoMark = (size_t)-1;
 
 size_t mark_begin(mlff_ctx *ctx, std::vector<GemvMark> *marks) {
-  if (!ctx->timing.on || marks == nullptr) return kNoMark;
+  if (!ctx->timing.on || marks == nullptr || !ctx->timing.sample) return kNoMark;
   hipEvent_t e0 = timing_event(ctx);
   if (e0 == nullptr) return kNoMark;
   hipEventRecord(e0, ctx->stream);
@@ -779,6 +779,9 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
                      lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
   }
   if (lowrank) {
+    // the T r half of iteration it + 1's apply: bracketed with that iteration (its
+    // z half, kind 1) so a sampled apply is always timed whole
+    ctx->timing.sample = (it + 1) % ctx->timing.every == 0;
     const size_t tm = mark_begin(ctx, marks);
     launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
     mark_end(ctx, marks, tm, it, 3);
@@ -800,6 +803,9 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
 // test of this iteration runs as its own launch (last iteration of a chunk)
 int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, bool fold_in,
                      bool stop_out) {
+  // events cost GPU time between the kernels they bracket: only every timing.every-th
+  // iteration is bracketed (the averages are over the sampled iterations)
+  ctx->timing.sample = it % ctx->timing.every == 0;
   if (ctx->world > 1) return launch_iteration_ranks(ctx, it, marks, fold_in, stop_out);
   hipStream_t s = ctx->stream;
   const int *status = &ctx->st->status;
@@ -1752,6 +1758,7 @@ int mlff_timing_enable(mlff_ctx *ctx, int on) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);
   ctx->timing.on = on != 0;
+  ctx->timing.every = on > 1 ? on : 1;
   if (ctx->timing.on && ctx->timing.ev.size() < kTimingPool) ctx->timing.ev.reserve(kTimingPool);
   return MLFF_OK;
   MLFF_API_END(ctx)

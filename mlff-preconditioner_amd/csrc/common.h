@@ -155,6 +155,8 @@ inline unsigned timing_event_flags() {
 
 struct Timing {
   bool on = false;
+  int every = 1;        // bracket every `every`-th PCG iteration only (mlff_timing_enable)
+  bool sample = true;   // the iteration being launched is bracketed
   std::vector<hipEvent_t> ev;  // pool, pairs (start, stop)
   size_t used = 0;             // events used in the current chunk
   double gemv_ms = 0.0;

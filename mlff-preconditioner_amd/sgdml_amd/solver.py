@@ -352,8 +352,10 @@ class KernelSolver:
                          early_exit=early, callbacks=callbacks)
 
     # ------------------------------------------------------------------- timing
-    def timing(self, on: bool = True):
-        self._call("mlff_timing_enable", int(bool(on)))
+    def timing(self, on: bool | int = True):
+        """True / 1: bracket every PCG iteration with timing events; n > 1: every n-th
+        iteration only (events cost GPU time); False / 0: off."""
+        self._call("mlff_timing_enable", int(on) if not isinstance(on, bool) else int(on))
 
     def timing_reset(self):
         self._call("mlff_timing_reset")
