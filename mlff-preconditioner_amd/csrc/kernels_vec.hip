@@ -625,7 +625,6 @@ struct LcArgs {
   int segbytes, C, c;
   unsigned long long *slots;  // k x C x 2 granules
   unsigned epoch;
-  int *fault;
   int mute;  // test hook: this member never publishes (its cluster times out)
 };
 
@@ -779,7 +778,6 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
   a.i1 = a.i0 + rpc < (int)k ? a.i0 + rpc : (int)k;
   a.slots = slots;
   a.epoch = epoch;
-  a.fault = fault;
   a.mute = (int)blockIdx.x == mute_block;
   const bool row_wave = threadIdx.x < kLcThreads;
   constexpr int NB = D + L + 1;
