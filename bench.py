@@ -61,6 +61,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 TIMING_EVERY = int(os.environ.get("MLFF_BENCH_TIMING_EVERY", "8"))
 
 
+def timing_every(steps: int) -> int:
+    """Bracket period for a timed region of `steps` iterations: TIMING_EVERY, shortened so
+    that at least 4 of the steps (or all of a shorter run) are bracketed."""
+    return max(1, min(TIMING_EVERY, steps // 4))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -386,7 +392,7 @@ def size_leg(args, rank, world, local, pg, n, k, lam, ell):
                     maxiter=args.warmup + args.steps + 1)
         if args.warmup:
             s.pcg_run(args.warmup, args.warmup)
-        s.timing(TIMING_EVERY)
+        s.timing(timing_every(args.steps))
         s.timing_reset()
         barrier(pg, s)
         t0 = time.perf_counter()
@@ -430,7 +436,7 @@ def solo_profile(args):
                     maxiter=args.warmup + args.steps + 1)
         if args.warmup:
             s.pcg_run(args.warmup, args.warmup)
-        s.timing(TIMING_EVERY)
+        s.timing(timing_every(args.steps))
         s.timing_reset()
         s.synchronize()
         t0 = time.perf_counter()
@@ -493,7 +499,7 @@ def main():
         solver.pcg_run(args.warmup, args.warmup)
     # HIP events on every TIMING_EVERY-th iteration of the timed region (each event costs
     # GPU time between the kernels it brackets; the per-kernel averages are over those)
-    solver.timing(TIMING_EVERY)
+    solver.timing(timing_every(args.steps))
     solver.timing_reset()
     barrier(pg, solver)
     t0 = time.perf_counter()
@@ -621,7 +627,7 @@ def main():
             # with half storage also report against the dense 8 N^2 bytes
             "matvec_gbs_dense_equivalent": dense_equiv,
             "iter_device_ms": iter_ms,
-            "timing_events_every": TIMING_EVERY,
+            "timing_events_every": timing_every(args.steps),
             "rccl": comm,
             "device_memory_used_gb_max_rank": used_gb,
             "iter_gbs_algorithmic": per_iter_bytes / (iter_ms * 1e-3) / 1e9,

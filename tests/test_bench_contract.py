@@ -49,3 +49,15 @@ def test_usable_cores_is_consistent():
     assert c["cores"] <= c["affinity_cpus"]
     if c["cgroup_quota_cpus"] is not None:
         assert c["cores"] <= max(1, int(c["cgroup_quota_cpus"]))
+
+
+def test_timing_every_brackets_some_steps():
+    """The timed region brackets every timing_every(steps)-th iteration: at least 4 (or all)
+    of any run of `steps` consecutive iterations are bracketed, so the per-kernel averages
+    of the line always exist (a 5-step run once divided by zero bracketed iterations)."""
+    for steps in (1, 2, 3, 5, 10, 20, 50, 200):
+        e = bench.timing_every(steps)
+        assert 1 <= e <= bench.TIMING_EVERY
+        for first in range(1, 3 * e + 2):
+            hits = sum(1 for it in range(first, first + steps) if it % e == 0)
+            assert hits >= min(4, steps), (steps, e, first, hits)
