@@ -96,14 +96,14 @@ __global__ __launch_bounds__(256) void k_gemm(int64_t M, int64_t N, int64_t K, d
 // k rows one step reads fall on disjoint bank halves pairwise (2 passes, the minimum).
 // Fixed summation order (k ascending, 4 per instruction): deterministic.
 typedef double v4d __attribute__((ext_vector_type(4)));
-template <int BM, bool TA, bool TB, int NTH = 256, int BK = 16>
+template <int BM, bool TA, bool TB, int NTH = 256>
 __global__ __launch_bounds__(NTH) void k_gemm_mfma(int64_t M, int64_t N, int64_t K, double alpha,
                                                    const double *__restrict__ A, int64_t lda,
                                                    const double *__restrict__ B, int64_t ldb,
                                                    double beta, double *__restrict__ C,
                                                    int64_t ldc, int64_t kchunk,
                                                    int64_t slab_stride, int tri) {
-  constexpr int BN = 128, LP = 144;
+  constexpr int BN = 128, BK = 16, LP = 144;
   if (tri && (int64_t)blockIdx.x * BN >= (int64_t)blockIdx.y * BM + BM) return;
   constexpr int WR = NTH / 128;        // wave rows (two wave columns of 64)
   constexpr int IM = BM / WR / 16, JN = 4;  // 16 x 16 blocks per wave
@@ -187,33 +187,24 @@ __global__ __launch_bounds__(NTH) void k_gemm_mfma(int64_t M, int64_t N, int64_t
       }
 }
 
-template <int BM, int NTH, int BK = 16>
+template <int BM, int NTH>
 static void gemm_mfma_launch_t(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd, double alpha,
                                const double *A, int64_t lda, const double *B, int64_t ldb,
                                double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
                                int64_t slab_stride, hipStream_t s, int tri) {
   dim3 grid((unsigned)((Nc + 127) / 128), (unsigned)((M + BM - 1) / BM), (unsigned)splits);
   if (!ta && !tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, false, false, NTH, BK>), grid, dim3(NTH), 0, s, M, Nc, Kd,
-                       alpha, A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (!ta && tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, false, true, NTH, BK>), grid, dim3(NTH), 0, s, M, Nc, Kd,
-                       alpha, A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
+    hipLaunchKernelGGL((k_gemm_mfma<BM, false, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else if (ta && !tb)
-    hipLaunchKernelGGL((k_gemm_mfma<BM, true, false, NTH, BK>), grid, dim3(NTH), 0, s, M, Nc, Kd,
-                       alpha, A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, false, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
   else
-    hipLaunchKernelGGL((k_gemm_mfma<BM, true, true, NTH, BK>), grid, dim3(NTH), 0, s, M, Nc, Kd,
-                       alpha, A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
-}
-
-// K step of the matrix-core GEMM (MLFF_GEMM_BK = 32 for A/B sweeps: half the barriers per flop)
-static int gemm_bk() {
-  static const int bk = [] {
-    const char *e = std::getenv("MLFF_GEMM_BK");
-    return (e != nullptr && std::atoi(e) == 32) ? 32 : 16;
-  }();
-  return bk;
+    hipLaunchKernelGGL((k_gemm_mfma<BM, true, true, NTH>), grid, dim3(NTH), 0, s, M, Nc, Kd, alpha,
+                       A, lda, B, ldb, beta, C, ldc, kchunk, slab_stride, tri);
 }
 
 // workgroup size of the matrix-core GEMM (MLFF_GEMM_NTH = 256 / 512 for A/B sweeps)
@@ -230,10 +221,7 @@ static void gemm_mfma_launch(bool ta, bool tb, int64_t M, int64_t Nc, int64_t Kd
                              const double *A, int64_t lda, const double *B, int64_t ldb,
                              double beta, double *C, int64_t ldc, int64_t kchunk, int splits,
                              int64_t slab_stride, hipStream_t s, int tri) {
-  if (gemm_nth() == 512 && gemm_bk() == 32)
-    gemm_mfma_launch_t<BM, 512, 32>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
-                                    splits, slab_stride, s, tri);
-  else if (gemm_nth() == 512)
+  if (gemm_nth() == 512)
     gemm_mfma_launch_t<BM, 512>(ta, tb, M, Nc, Kd, alpha, A, lda, B, ldb, beta, C, ldc, kchunk,
                                 splits, slab_stride, s, tri);
   else
