@@ -532,15 +532,17 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
 // order (wave w sums its quarter, the quarters in order); rho partials r . z in kVecGrid
 // slots: a workgroup takes the 64-column blocks blockIdx.x + i gridDim.x (grid <= kVecGrid)
 // and writes one slot, the slots past the grid are zero
-__global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart, int G, int64_t ldp,
-                                                const double *__restrict__ r,
-                                                double *__restrict__ z, int64_t n, double sigma_p,
-                                                double lam_inv, double *__restrict__ rho_part,
-                                                const int *__restrict__ status) {
+template <int NW>  // waves per workgroup, each summing 1/NW of the partials
+__global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ zpart, int G,
+                                                    int64_t ldp, const double *__restrict__ r,
+                                                    double *__restrict__ z, int64_t n,
+                                                    double sigma_p, double lam_inv,
+                                                    double *__restrict__ rho_part,
+                                                    const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sh[4][64];
+  __shared__ double sh[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int g0 = (G * w) / 4, g1 = (G * (w + 1)) / 4;
+  const int g0 = (G * w) / NW, g1 = (G * (w + 1)) / NW;
   double rho = 0.0;
   for (int64_t jb = blockIdx.x; jb * 64 < n; jb += gridDim.x) {
     const int64_t j = jb * 64 + lane;
@@ -560,7 +562,9 @@ __global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart
     sh[w][lane] = s;
     __syncthreads();
     if (w == 0 && j < n) {
-      const double sv = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+      double sv = sh[0][lane];  // the wave sums in wave order
+#pragma unroll
+      for (int q = 1; q < NW; ++q) sv += sh[q][lane];
       const double rv = r[j];
       const double zv = sigma_p * (lam_inv * (rv - sv));
       z[j] = zv;
@@ -572,7 +576,32 @@ __global__ __launch_bounds__(256) void k_lr_fin(const double *__restrict__ zpart
     if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = tot;
   }
   if (blockIdx.x == 0 && rho_part != nullptr)
-    for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 256) rho_part[i] = 0.0;
+    for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 64 * NW) rho_part[i] = 0.0;
+}
+
+// waves of k_lr_fin (MLFF_LR_FIN_WAVES = 4 / 8 / 16 for A/B; nanotube, 2 interleaved rounds:
+// apply 66.3-66.6 us with 4, 65.8-65.9 with 16; k_lr_fin 8.1 -> 7.1 us)
+static int lr_fin_waves() {
+  static const int nw = [] {
+    const char *e = std::getenv("MLFF_LR_FIN_WAVES");
+    const int v = e ? std::atoi(e) : 16;
+    return v == 8 || v == 16 ? v : 4;
+  }();
+  return nw;
+}
+
+static void launch_lr_fin(const double *zpart, int G, int64_t ldp, const double *r, double *z,
+                          int64_t n, double sigma_p, double lam_inv, double *rho_part,
+                          const int *status, hipStream_t s, unsigned grid) {
+  if (lr_fin_waves() == 16)
+    hipLaunchKernelGGL(k_lr_fin<16>, dim3(grid), dim3(1024), 0, s, zpart, G, ldp, r, z, n, sigma_p,
+                       lam_inv, rho_part, status);
+  else if (lr_fin_waves() == 8)
+    hipLaunchKernelGGL(k_lr_fin<8>, dim3(grid), dim3(512), 0, s, zpart, G, ldp, r, z, n, sigma_p,
+                       lam_inv, rho_part, status);
+  else
+    hipLaunchKernelGGL(k_lr_fin<4>, dim3(grid), dim3(256), 0, s, zpart, G, ldp, r, z, n, sigma_p,
+                       lam_inv, rho_part, status);
 }
 
 static unsigned lr_fin_grid(int64_t n) {
@@ -860,8 +889,7 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
   hipLaunchKernelGGL((k_lr_cluster<kLcD, kLcL>), dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), 0, s,
                      T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, mute, status, fold);
   if (n > 0)
-    hipLaunchKernelGGL(k_lr_fin, dim3(lr_fin_grid(n)), dim3(256), 0, s, zpart, Q, ldt, r,
-                       z, n, sigma_p, lam_inv, rho_part, status);
+    launch_lr_fin(zpart, Q, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n));
 }
 
 void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
@@ -884,8 +912,7 @@ void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double 
   else
     hipLaunchKernelGGL(k_lr_rows<16>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
   if (n > 0)
-    hipLaunchKernelGGL(k_lr_fin, dim3(lr_fin_grid(n)), dim3(256), 0, s, zpart, G, ldt, r, z,
-                       n, sigma_p, lam_inv, rho_part, status);
+    launch_lr_fin(zpart, G, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n));
 }
 
 // ---------------------------------------------------------------------------
