@@ -137,11 +137,17 @@ def test_pcg_stable_regime_exact(sg, kind):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
-def test_nystrom_apply(sg, variant):
+@pytest.mark.parametrize("form", ["auto", "one_pass", "cluster"])
+def test_nystrom_apply(sg, monkeypatch, variant, form):
+    """Nystrom applies (both variants, their opposite signs sigma_p) against the oracle, on
+    the apply form the size selects, forced onto the one-pass rows form, and on the cluster
+    form (N = 20000: rows longer than a workgroup)."""
     from oracle.precon import apply_panel, nystrom_panel
     from oracle.rbf import rbf_kernel
 
-    n, k, lam = 1000, 64, 1e-6
+    n, k, lam = (20000, 400, 1e-6) if form == "cluster" else (1000, 64, 1e-6)
+    if form == "one_pass":
+        monkeypatch.setenv("MLFF_LR_ROWS", "1")
     X, _ = _rbf(n)
     K = rbf_kernel(X, 0.2)
     idx = np.sort(np.random.default_rng(5).choice(n, k, replace=False))
@@ -150,6 +156,8 @@ def test_nystrom_apply(sg, variant):
         s.gen_rbf(X, length_scale=0.2)
         s.set_operator(1.0, lam)
         s.precon_nystrom(idx, variant=variant)
+        if form != "auto":
+            assert s.precon_apply_traffic()[0] == (1 if form == "one_pass" else 2)
         z = s.precon_apply(r)
     B, sp = nystrom_panel(K[:, idx], idx, lam, variant=variant)
     zref = apply_panel(B, sp, lam, r)
