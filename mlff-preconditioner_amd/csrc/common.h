@@ -54,9 +54,11 @@ struct SymPack {
   int64_t nb = 0;            // Np / B
   int64_t tiles_per_rank = 0;
   double *P = nullptr;       // slot buffer nb x Np
-  // the last (ntiles - nwhole) tiles of `list` run as 4 quarter-tile workgroups each;
-  // their column partials of quarters 1..3 go to Pq (3 planes of nb x Np)
+  // the last (ntiles - nwhole) tiles of `list` run as 2^lsub sub-unit workgroups each;
+  // their column partials of sub-units 1.. go to Pq (2^lsub - 1 planes of nb x Np)
   int64_t nwhole = 0;
+  int lsub = 2;              // split tiles run as 2^lsub sub-units (row slices) each
+  int64_t pq_planes = 0;     // planes allocated in Pq (2^lsub - 1 needed)
   double *Pq = nullptr;
   unsigned char *split = nullptr;  // nb x nb: tile (I, J) is split
   int *own = nullptr;              // nb x nb owned slots per row block + nb counts (W > 1)

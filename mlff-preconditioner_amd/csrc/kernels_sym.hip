@@ -127,25 +127,25 @@ __device__ __forceinline__ void tile_body(const double *__restrict__ A, int I, i
 
 constexpr int kBatches = B / kRB;  // 8-row batches per tile
 
-// workgroups [0, nwhole): one whole tile each; then 4 workgroups per remaining tile,
-// one quarter (128 rows) each, so the launch ends on quarter-tile units instead of a
+// workgroups [0, nwhole): one whole tile each; then 2^lsub workgroups per remaining tile,
+// one row slice (512 >> lsub rows) each, so the launch ends on sub-tile units instead of a
 // partial round of whole tiles (a lone 2-MB tile streams at one CU's rate)
 __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ tiles,
                                                     const int2 *__restrict__ list,
                                                     const double *__restrict__ v,
                                                     double *__restrict__ P,
                                                     double *__restrict__ Pq, int64_t Np,
-                                                    int nwhole, int nb,
+                                                    int nwhole, int nb, int lsub,
                                                     const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[6 * B + 4 * kRB * 64];
   int tile = blockIdx.x, h = 0, gb0 = 0, gb1 = kBatches;
   if (tile >= nwhole) {
     const int u = tile - nwhole;
-    tile = nwhole + (u >> 2);
-    h = u & 3;
-    gb0 = h * (kBatches / 4);
-    gb1 = gb0 + kBatches / 4;
+    tile = nwhole + (u >> lsub);
+    h = u & ((1 << lsub) - 1);
+    gb0 = h * (kBatches >> lsub);
+    gb1 = gb0 + (kBatches >> lsub);
   }
   const int2 t = list[tile];
   const double *A = tiles + (int64_t)tile * B * B;
@@ -161,8 +161,8 @@ __global__ __launch_bounds__(256) void k_symv_tiles(const double *__restrict__ t
 // finishing a tile (LDS combine + slot stores) a workgroup already has the first batch
 // of its next unit and the next p segment in flight, so the HBM stream of a workgroup
 // slot does not stop at tile boundaries.  The counter is reset by the slot reduction.
-__device__ __forceinline__ void decode_unit(long long u, int nwhole, int &tile, int &h, int &gb0,
-                                            int &gb1) {
+__device__ __forceinline__ void decode_unit(long long u, int nwhole, int lsub, int &tile, int &h,
+                                            int &gb0, int &gb1) {
   if (u < nwhole) {
     tile = (int)u;
     h = 0;
@@ -170,10 +170,10 @@ __device__ __forceinline__ void decode_unit(long long u, int nwhole, int &tile, 
     gb1 = kBatches;
   } else {
     const long long q = u - nwhole;
-    tile = nwhole + (int)(q >> 2);
-    h = (int)(q & 3);
-    gb0 = h * (kBatches / 4);
-    gb1 = gb0 + kBatches / 4;
+    tile = nwhole + (int)(q >> lsub);
+    h = (int)(q & ((1 << lsub) - 1));
+    gb0 = h * (kBatches >> lsub);
+    gb1 = gb0 + (kBatches >> lsub);
   }
 }
 
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
                                                   double *__restrict__ P,
                                                   double *__restrict__ Pq, int64_t Np,
                                                   int nwhole, long long nunits, int nb,
+                                                  int lsub,
                                                   unsigned long long *__restrict__ ticket,
                                                   const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
   long long u = blockIdx.x;
   if (u >= nunits) return;
   int tile, h, gb0, gb1;
-  decode_unit(u, nwhole, tile, h, gb0, gb1);
+  decode_unit(u, nwhole, lsub, tile, h, gb0, gb1);
   int2 t = list[tile];
   const double *A = tiles + (int64_t)tile * B * B;
   d2 pc[4], a[kRB][4];
@@ -275,7 +276,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
     int2 t2 = t;
     const double *A2 = A;
     if (un < nunits) {  // next unit: p segment and first batch in flight during the stores
-      decode_unit(un, nwhole, tile2, h2, gb02, gb12);
+      decode_unit(un, nwhole, lsub, tile2, h2, gb02, gb12);
       t2 = list[tile2];
       A2 = tiles + (int64_t)tile2 * B * B;
       const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)t2.y * B);
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
 }
 
 // column partials of slot t for rows of block bi: tile (t, bi), t > bi; a split tile
-// adds its quarters 1..3 (planes Pq) to quarter 0 (P) in quarter order
+// adds its sub-units 1..nq (planes Pq) to sub-unit 0 (P) in sub-unit order
 constexpr int kOwnSplit = 1 << 24;  // flag bit of an owned-slot entry: the tile is split
 
 // y[i] = sum_{t=0}^{nb-1} P[t, i] over the slots whose tile this rank owns
@@ -327,7 +328,7 @@ template <bool EPI, bool PQ>
 __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P,
                                                     const double *__restrict__ Pq,
                                                     const unsigned char *__restrict__ split,
-                                                    int t_split, int64_t Np, int nb,
+                                                    int t_split, int64_t Np, int nb, int nq,
                                                     int64_t n_out, double *__restrict__ y,
                                                     double sigma, double lam,
                                                     const double *__restrict__ vloc,
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
       for (int u = 0; u < 8; ++u) s += v[u];
     }
     // the remaining slots (split tiles among them) in batches of 8 as well; every slot
-    // value is ((P + Pq0) + Pq1) + Pq2, added in slot order
+    // value is ((P + Pq0) + Pq1) + ... + Pq_{nq-1}, added in slot order
     for (; t < nb; t += 8) {
       double v[8];
 #pragma unroll
@@ -374,11 +375,8 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
         const int tu = t + u;
         if (tu < nb) {
           v[u] = P[(int64_t)tu * Np + i];
-          if (tu > bi && split[(int64_t)tu * nb + bi]) {
-            const double q0 = Pq[(int64_t)tu * Np + i], q1 = Pq[pl + (int64_t)tu * Np + i],
-                         q2 = Pq[2 * pl + (int64_t)tu * Np + i];
-            v[u] = ((v[u] + q0) + q1) + q2;
-          }
+          if (tu > bi && split[(int64_t)tu * nb + bi])
+            for (int hq = 0; hq < nq; ++hq) v[u] += Pq[hq * pl + (int64_t)tu * Np + i];
         }
       }
 #pragma unroll
@@ -412,7 +410,7 @@ template <bool PQ>
 __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__ P,
                                                       const double *__restrict__ Pq,
                                                       const unsigned char *__restrict__ split,
-                                                      int64_t Np,
+                                                      int64_t Np, int nq,
                                                       int nb, int rank,
                                                       const int *__restrict__ own,
                                                       int64_t ld, int64_t blk, int64_t bstride,
@@ -435,7 +433,7 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
     double s = 0.0;
     // this rank's slots of row block bi (own: ascending slots, kOwnSplit marks a split
     // tile; built at setup) in batches of 16 whose loads are all in flight before the
-    // first addition; every slot value is ((P + Pq0) + Pq1) + Pq2, added in
+    // first addition; every slot value is ((P + Pq0) + Pq1) + ... (nq planes), added in
     // slot order
     const int *ol = own + (int64_t)bi * nb;
     const int cnt = own[(int64_t)nb * nb + bi];
@@ -449,7 +447,8 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
           const int e = ol[c + u];
           const int64_t at = (int64_t)(e & (kOwnSplit - 1)) * Np + i;
           v[u] = P[at];
-          if (e & kOwnSplit) v[u] = ((v[u] + Pq[at]) + Pq[pl + at]) + Pq[2 * pl + at];
+          if (e & kOwnSplit)
+            for (int hq = 0; hq < nq; ++hq) v[u] += Pq[hq * pl + at];
         }
       }
 #pragma unroll
@@ -615,15 +614,15 @@ __global__ __launch_bounds__(256) void k_sym_gen_rbf(const int2 *__restrict__ li
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
                  hipStream_t s) {
   if (sp.ntiles == 0) return;
-  const int64_t grid = sp.nwhole + 4 * (sp.ntiles - sp.nwhole);
+  const int64_t grid = sp.nwhole + ((sp.ntiles - sp.nwhole) << sp.lsub);
   if (sp.dyn > 0) {
     hipLaunchKernelGGL(k_symv_dyn, dim3((unsigned)std::min<int64_t>(sp.dyn, grid)), dim3(256), 0, s,
                        sp.tiles, sp.list, v_full, P, sp.Pq, sp.Np, (int)sp.nwhole, (long long)grid,
-                       (int)sp.nb, sp.ticket, status);
+                       (int)sp.nb, sp.lsub, sp.ticket, status);
     return;
   }
   hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)grid), dim3(256), 0, s, sp.tiles, sp.list, v_full,
-                     P, sp.Pq, sp.Np, (int)sp.nwhole, (int)sp.nb, status);
+                     P, sp.Pq, sp.Np, (int)sp.nwhole, (int)sp.nb, sp.lsub, status);
 }
 
 void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogue, double sigma,
@@ -632,18 +631,19 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
   const dim3 grid((unsigned)((n_out + 255) / 256));
   if (epilogue)
     hipLaunchKernelGGL((k_sym_reduce<true, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
-                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y, sigma, lam, vloc,
                        (double *)nullptr, sp.ticket, status);
   else
     hipLaunchKernelGGL((k_sym_reduce<false, false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split,
-                       (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, vloc,
+                       (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y, sigma, lam, vloc,
                        (double *)nullptr, sp.ticket, status);
 }
 
 void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
                           const double *p, double *pq_part, const int *status, hipStream_t s) {
   hipLaunchKernelGGL((k_sym_reduce<true, true>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
-                     sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, n_out, y, sigma, lam, p, pq_part,
+                     sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y, sigma,
+                     lam, p, pq_part,
                      sp.ticket, status);
 }
 
@@ -654,13 +654,13 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
   const dim3 grid(kVecGrid);
   if (p_full == nullptr) {
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
-                       (int)sp.nb, rank,
+                       (1 << sp.lsub) - 1, (int)sp.nb, rank,
                        sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
                        sp.ticket, status);
     return;
   }
   hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
-                     (int)sp.nb, rank,
+                     (1 << sp.lsub) - 1, (int)sp.nb, rank,
                      sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
                      sp.ticket, status);
   hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
@@ -714,6 +714,19 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   // tiles where one-workgroup-per-unit launches took 2.51-2.61 ms (bimodal across runs),
   // equal at 528 / 1035 tiles.  MLFF_SYM_SCHED=static selects the one-workgroup-per-unit
   // launch (k_symv_tiles).
+  // Sub-units per split tile: 4 (quarters).  MLFF_SYM_LSUB=3|4 slices the split tiles
+  // into 8 / 16 row slices instead (the count that would fill the C slots when the nt mod
+  // C tail tiles are few, e.g. 8 of a rank's 1032 at 8 ranks).  Measured on one MI355X
+  // (scripts/gpu_sym_lsub_ab.sh, profiles/final3e): no gain -- the dynamic schedule
+  // already overlaps the tail (k_symv_dyn 323.9 vs 323.6 us at W = 8) while the reduce
+  // reads 15 instead of 3 planes of the split slots (12.7 -> 17.9 us): the step got 1 %
+  // slower at W = 8 / 4, 0.2 % at W = 1.  Kept selectable, not default.
+  int lsub = 2;
+  if (const char *e = std::getenv("MLFF_SYM_LSUB")) {
+    const int v = std::atoi(e);
+    if (v >= 2 && v <= 4) lsub = v;
+  }
+  const int64_t nq = ((int64_t)1 << lsub) - 1;
   int64_t dyn = C;
   if (const char *e = std::getenv("MLFF_SYM_SCHED"))
     if (std::strcmp(e, "static") == 0) dyn = 0;
@@ -721,7 +734,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   // cut at range boundaries -- measured slower at every size on one MI355X: 2.67 vs
   // 2.61 ms at 8256 tiles, 0.366 vs 0.338 ms at 1035: the hardware dispatcher's dynamic
   // whole-tile balance beats a static equal-byte split.)
-  if (sp.tiles == nullptr || sp.ntiles != nt || sp.Np != Np) {
+  if (sp.tiles == nullptr || sp.ntiles != nt || sp.Np != Np || sp.pq_planes != nq) {
     sym_free(sp);
     if (nt > 0) {
       MLFF_HIP(ctx, hipMalloc(&sp.tiles, sizeof(double) * nt * B * B));
@@ -729,8 +742,9 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     }
     MLFF_HIP(ctx, hipMalloc(&sp.P, sizeof(double) * (int64_t)nb * Np));
     MLFF_HIP(ctx, hipMemsetAsync(sp.P, 0, sizeof(double) * (int64_t)nb * Np, s));
-    MLFF_HIP(ctx, hipMalloc(&sp.Pq, sizeof(double) * 3 * (int64_t)nb * Np));
-    MLFF_HIP(ctx, hipMemsetAsync(sp.Pq, 0, sizeof(double) * 3 * (int64_t)nb * Np, s));
+    MLFF_HIP(ctx, hipMalloc(&sp.Pq, sizeof(double) * nq * (int64_t)nb * Np));
+    MLFF_HIP(ctx, hipMemsetAsync(sp.Pq, 0, sizeof(double) * nq * (int64_t)nb * Np, s));
+    sp.pq_planes = nq;
     MLFF_HIP(ctx, hipMalloc(&sp.split, (size_t)nb * nb));
     MLFF_HIP(ctx, hipMalloc(&sp.own, sizeof(int) * (size_t)nb * (nb + 1)));
     MLFF_HIP(ctx, hipMalloc(&sp.ticket, sizeof(unsigned long long)));
@@ -750,6 +764,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   sp.nb = nb;
   sp.tiles_per_rank = tpr;
   sp.nwhole = nwhole;
+  sp.lsub = lsub;
   sp.dyn = dyn;
   {
     std::vector<unsigned char> split((size_t)nb * nb, 0);
@@ -825,6 +840,7 @@ void sym_free(SymPack &sp) {
   sp.yg = nullptr;
   sp.yr = nullptr;
   sp.ntiles = 0;
+  sp.pq_planes = 0;
   sp.ready = false;
 }
 
