@@ -116,6 +116,22 @@ def test_sharded_solve_matches_single_rank(world, precon, storage):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("lsub", ["3", "4"])
+def test_sharded_sym_row_slices(lsub, monkeypatch):
+    """Split tiles as 8 / 16 row slices (MLFF_SYM_LSUB; below one round of resident
+    workgroups every tile is split): the owned-slot reduction sums 7 / 15 partial planes
+    per split slot; the sharded mat-vec and solve must match the single-rank one."""
+    monkeypatch.setenv("MLFF_SYM_LSUB", lsub)
+    n = 1003
+    ref = run_ranks(1, lambda r, w, key: solve_case(r, w, key, n, "nystrom"))[0]
+    outs = run_ranks(3, lambda r, w, key: solve_case(r, w, key, n, "nystrom"))
+    np.testing.assert_allclose(gather(outs, "y"), ref["y"], rtol=1e-13, atol=1e-13)
+    assert outs[0]["info"] == ref["info"] == 0
+    assert_pcg_parity(outs[0]["iters"], outs[0]["trace"][1:], gather(outs, "x"), ref["iters"],
+                      ref["trace"][1:], ref["x"], mode="chaotic", x_tol=1e-7)
+
+
+@pytest.mark.timeout(300)
 def test_sharded_sgdml_assembly_rows():
     import sgdml_amd
     from oracle.sgdml import descriptors

@@ -122,16 +122,18 @@ def test_symtile_sgdml_assembly(sg):
     assert np.max(np.abs(y - ref)) <= 1e-13 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("lsub", ["2", "4"])
 @pytest.mark.parametrize("sched", ["dyn", "static"])
 @pytest.mark.parametrize("n", [16384, 23040])
-def test_symtile_quarter_tail_matches_dense(sg, n, sched, monkeypatch):
+def test_symtile_quarter_tail_matches_dense(sg, n, sched, lsub, monkeypatch):
     """Tile counts past one round of 512 workgroups (528 and 1035 tiles: whole tiles plus
-    quarter-tile units for the remainder), both launch schedules (counter-driven resident
-    workgroups with cross-tile prefetch; one workgroup per unit), against the dense row
-    GEMV."""
+    sub-tile units for the remainder -- quarters, or 16 row slices with MLFF_SYM_LSUB=4),
+    both launch schedules (counter-driven resident workgroups with cross-tile prefetch; one
+    workgroup per unit), against the dense row GEMV."""
     from sgdml_amd import synthetic
 
     monkeypatch.setenv("MLFF_SYM_SCHED", sched)
+    monkeypatch.setenv("MLFF_SYM_LSUB", lsub)
 
     X, _ = synthetic.rbf_points(n, 3, 11)
     v = np.random.default_rng(n).standard_normal(n)
