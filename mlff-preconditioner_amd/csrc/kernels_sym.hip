@@ -717,7 +717,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   // Sub-units per split tile: 4 (quarters).  MLFF_SYM_LSUB=3|4 slices the split tiles
   // into 8 / 16 row slices instead (the count that would fill the C slots when the nt mod
   // C tail tiles are few, e.g. 8 of a rank's 1032 at 8 ranks).  Measured on one MI355X
-  // (scripts/gpu_sym_lsub_ab.sh, profiles/final3e): no gain -- the dynamic schedule
+  // (scripts/gpu_sym_lsub_ab.sh, profiles/r02/final3e): no gain -- the dynamic schedule
   // already overlaps the tail (k_symv_dyn 323.9 vs 323.6 us at W = 8) while the reduce
   // reads 15 instead of 3 planes of the split slots (12.7 -> 17.9 us): the step got 1 %
   // slower at W = 8 / 4, 0.2 % at W = 1.  Kept selectable, not default.
