@@ -20,7 +20,9 @@ iteration (the fp64 mat-vec over the whole N x N matrix + preconditioner apply +
 updates); with several GPUs the rows are sharded and the iteration runs three RCCL
 collectives (allgather of z, reduce-scatter of the partial K p, allreduce of ||r||^2 | T r).
 
-Prints one JSON line (rank 0) with the driver's keys plus
+Prints the JSON line (rank 0) with the driver's keys -- once right after the configs[2] leg,
+and once more, identical plus `configs3_leg`, after the configs[3] leg (the last line is the
+complete one) -- with
   roofline:     algorithmic bytes/launch of the K mat-vec / its mean HIP-event
                 duration, against 8 TB/s; traffic from profiles/ (PMC) or null.  With
                 the symmetric tiled storage (default) the bytes are the stored lower
@@ -162,16 +164,38 @@ def make_solver(n, rank, world, local, pg):
     return sgdml_amd.KernelSolver(n, device=local, rank=rank, world=world, comm_id=comm_id)
 
 
-def pmc_traffic(workload: str, storage: str, world: int):
+def csrc_hash() -> str:
+    """Content hash of the library sources (csrc/ and include/): PMC traffic figures are
+    only valid for the code they were collected on."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(list((REPO / "mlff-preconditioner_amd" / "csrc").glob("*"))
+                   + list((REPO / "include").glob("*.h")))
+    for f in files:
+        if f.is_file():
+            h.update(f.relative_to(REPO).as_posix().encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(key: str):
+    """(HBM bytes per launch from profiles/pmc_traffic.json, None) when the entry was collected
+    on the current sources (scripts/pmc_head.py stamps csrc_sha), else (None, reason)."""
     p = REPO / "profiles" / "pmc_traffic.json"
     if not p.exists():
-        return None
+        return None, "no profiles/pmc_traffic.json"
     try:
-        d = json.loads(p.read_text())
-        e = d.get(f"{workload}/{storage}/gpus{world}")
-        return None if e is None else float(e["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+        e = json.loads(p.read_text()).get(key)
+    except Exception as ex:  # noqa: BLE001
+        return None, f"unreadable profiles/pmc_traffic.json: {ex!r}"
+    if e is None:
+        return None, f"no PMC entry for {key}"
+    sha = csrc_hash()
+    if e.get("csrc_sha") != sha:
+        return None, (f"stale: PMC entry {key} was collected on sources {e.get('csrc_sha')}, "
+                      f"these are {sha} (scripts/pmc_head.py re-collects)")
+    return float(e["hbm_bytes_per_launch"]), None
 
 
 def _cpu_model() -> str:
@@ -300,8 +324,24 @@ def cpu_baseline(solver, X, b, idx, lam, ell, iters, iters_1t):
                  "single_thread": one}, **cpus)
 
 
+def rbf_band():
+    """The measured noise band of the configs[2] generator at N = 8192 (tests/golden/
+    make_rbf_band.py: the CPU oracle in six summation orders) and the oracle's own solve of
+    the full N = 65536 system (iterations to relres 1e-6), when committed."""
+    g = REPO / "tests" / "golden"
+    bd = json.loads((g / "rbf_band_n8192.json").read_text()) if (g / "rbf_band_n8192.json").exists() else None
+    full = None
+    if (g / "rbf_solve_n65536.npz").exists():
+        f = np.load(g / "rbf_solve_n65536.npz", allow_pickle=False)
+        full = {"iters": int(f["iters"]), "info": int(f["info"]),
+                "final_true_relres": float(f["final_relres"]), "x_norm": float(f["x_norm"]),
+                "cpu_seconds": float(f["seconds"])}
+    return bd, full
+
+
 def parity_small(n, k, lam, ell, tol=1e-6):
-    """Same generator at N = 8192: GPU vs CPU-oracle iterations to relres 1e-6."""
+    """Same generator at N = 8192: GPU vs CPU-oracle iterations to relres 1e-6, with the
+    measured noise band of that count (|d iters| <= 2 b_it + 2 is in band, tests/parity.py)."""
     import sgdml_amd
     from sgdml_amd import synthetic
 
@@ -320,9 +360,17 @@ def parity_small(n, k, lam, ell, tol=1e-6):
     B, sp = nystrom_panel(K[:, idx], idx, lam, 0)
     x, info, tr, it = cg_legacy(lambda v: K @ v + lam * v, b, tol=tol, maxiter=min(5 * n, 10000),
                                 psolve=lambda v: apply_panel(B, sp, lam, v))
-    return {"n": n, "k": k, "tol": tol, "gpu_iters": int(r.iters), "cpu_iters": int(it),
-            "gpu_info": int(r.info), "cpu_info": int(info),
-            "rel_dx": float(np.linalg.norm(r.x - x) / np.linalg.norm(x))}
+    out = {"n": n, "k": k, "tol": tol, "gpu_iters": int(r.iters), "cpu_iters": int(it),
+           "gpu_info": int(r.info), "cpu_info": int(info),
+           "rel_dx": float(np.linalg.norm(r.x - x) / np.linalg.norm(x))}
+    bd, _ = rbf_band()
+    if bd is not None and bd["n"] == n and bd["k"] == k and bd["lam"] == lam and bd["ell"] == ell:
+        out["band"] = {"b_iters": bd["band_iters"], "b_rel_dx": bd["band_rel_dx"],
+                       "oracle_orders": {o: v["iters"] for o, v in bd["variants"].items()},
+                       "source": "tests/golden/rbf_band_n8192.json"}
+        out["in_band"] = bool(abs(r.iters - it) <= 2 * bd["band_iters"] + 2
+                              and out["rel_dx"] <= 10 * bd["band_rel_dx"])
+    return out
 
 
 def sgdml_workload(args, rank, world, local, pg):
@@ -372,21 +420,49 @@ def precon_rbf(solver, idx) -> float:
     return solver.precon_nystrom(idx, variant=0)
 
 
+def all_ok(pg, ok: bool) -> bool:
+    """True when every rank reports ok: a collective verdict before any step that would make a
+    rank wait in a barrier or a collective for a peer that has already failed."""
+    if pg is None:
+        return ok
+    import torch
+
+    t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64,
+                     device="cpu" if REHEARSE else "cuda")
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item()) == 0.0
+
+
 def size_leg(args, rank, world, local, pg, n, k, lam, ell):
     """Iterations/s of the rbf workload at size n on all ranks (same generator, Nystrom rank,
     storage and timing as the main leg; no solve, no CPU leg): configs[3] (n = 131072) next
-    to the configs[2] `value`, so each bench line carries both problems' numbers."""
+    to the configs[2] `value`, so each bench line carries both problems' numbers.  Failures
+    are agreed on collectively between the phases, so every rank skips the rest together."""
     from sgdml_amd import synthetic
 
     X, b = synthetic.rbf_points(n, 3, 0)
     idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
-    s = make_solver(n, rank, world, local, pg)
+    s, err = None, None
     try:
+        s = make_solver(n, rank, world, local, pg)
         s.gen_rbf(X, ell)
         s.set_operator(1.0, lam)
-        precon_rbf(s, idx)
-        s.set_storage(args.storage)
-        _, op_bytes = s.storage_info()
+    except Exception as e:  # noqa: BLE001 -- reported in the line
+        err = e
+    if not all_ok(pg, err is None):
+        if s is not None:
+            s.close()
+        return {"n": n, "value": None, "error": repr(err) if err else "failed on another rank"}
+    try:
+        try:
+            precon_rbf(s, idx)
+            s.set_storage(args.storage)
+            _, op_bytes = s.storage_info()
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not all_ok(pg, err is None):
+            return {"n": n, "value": None,
+                    "error": repr(err) if err else "failed on another rank"}
         r0, r1 = s.row_range()
         s.pcg_start(np.ascontiguousarray(b[r0:r1]), tol=0.0,
                     maxiter=args.warmup + args.steps + 1)
@@ -526,13 +602,16 @@ def main():
     per_iter_bytes = op_bytes + 16.0 * k * nloc + 80.0 * nloc
     roof_op = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": achieved / HBM_PEAK_GBS,
-               "traffic": pmc_traffic(workload, storage, world),
+               "traffic": None,
                "kernel": {"sym": "k_symv_dyn + k_sym_reduce (K mat-vec, lower-triangle tiles)",
                           "dense": "k_gemv<4,4,1> (K mat-vec, dense rows)",
                           "matfree": "k_rec_g + k_rec_fin (record-factored matrix-free sGDML "
                                      "operator; k_mf_* when the pair records exceed their cap)"}
                .get(storage, storage),
                "bytes_per_launch": gemv_bytes, "mean_launch_ms": gemv_ms}
+    roof_op["traffic"], why = pmc_traffic(f"{workload}/{storage}/gpus{world}")
+    if why:
+        roof_op["traffic_note"] = why
     if storage == "matfree":
         roof_op["note"] = ("two dependent launches (Zt, G = sum w Zt and J^T G of a pair block in one "
                            "workgroup; the finisher): ~33 MB per application at M = 14, latency- "
@@ -549,8 +628,7 @@ def main():
         two_pass_bytes = 16.0 * k * nloc + 24.0 * nloc
         roof_pre = {"bound": "hbm", "achieved": pre_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": pre_gbs / HBM_PEAK_GBS,
-                    "traffic": pmc_traffic(workload + ("/precon1" if one_pass else "/precon"),
-                                           storage, world),
+                    "traffic": None,
                     "kernel": {1: "k_lr_rows + k_lr_fin (one-pass low-rank apply: each panel "
                                   "row read once, t_i kept in its workgroup)",
                                2: "k_lr_cluster + k_lr_fin (one-pass low-rank apply: each panel "
@@ -559,6 +637,9 @@ def main():
                         one_pass, "k_gemv<4,2,0> + k_colgemv_part + k_precon_fin (low-rank apply)"),
                     "bytes_per_launch": pre_bytes, "mean_launch_ms": pre_ms,
                     "two_pass_equivalent_gbs": two_pass_bytes / (pre_ms * 1e-3) / 1e9}
+        roof_pre["traffic"], why = pmc_traffic(f"{workload}/precon{one_pass}/{storage}/gpus{world}")
+        if why:
+            roof_pre["traffic_note"] = why
     # the roofline entry is the kernel group with the larger share of the iteration
     roof_dominant = roof_pre if roof_pre is not None and roof_pre["mean_launch_ms"] > gemv_ms \
         else roof_op
@@ -572,6 +653,14 @@ def main():
         t_solve = max_over_ranks(pg, time.perf_counter() - t1)
         solve = {"tol": 1e-6, "iters": int(res.iters), "info": int(res.info),
                  "seconds": t_solve, "final_relres": float(res.resid / np.linalg.norm(b))}
+        bd, full = rbf_band()
+        if sg_info is None and n == 65536 and k == 256 and full is not None and bd is not None:
+            # the CPU oracle's solve of this very system (committed fixture, ~2 h of CPU time:
+            # make_rbf_band.py --full), held to the N = 8192 band scaled by the count
+            b_it = int(np.ceil(bd["band_iters"] * full["iters"] / bd["ref_iters"]))
+            solve["cpu_ref"] = dict(full, source="tests/golden/rbf_solve_n65536.npz")
+            solve["band_iters_scaled"] = b_it
+            solve["in_band"] = bool(abs(res.iters - full["iters"]) <= 2 * b_it + 2)
 
     out = None
     if rank == 0:
@@ -639,10 +728,13 @@ def main():
                             storage_pack=t_pack),
         }
     solver.close()
+    if out is not None:
+        # the headline line first: a later leg that fails or hangs cannot take it away
+        print(json.dumps(out), flush=True)
     if args.workload == "rbf" and args.configs3_n and args.configs3_n != n:
         try:
             leg = size_leg(args, rank, world, local, pg, args.configs3_n, k, lam, ell)
-        except Exception as e:  # the configs[2] line above must still be printed
+        except Exception as e:  # the configs[2] line above is already printed
             leg = {"n": args.configs3_n, "value": None, "error": repr(e)}
         if out is not None:
             out["configs3_leg"] = dict(leg, baseline_config=(
@@ -651,8 +743,8 @@ def main():
                     "the configs[3] problem on the same ranks: its value at N GPUs over its "
                     "value in the N=1 bench line is configs[3]'s strong scaling (BASELINE.md "
                     "2: >=6x at 8 GPUs); `value` above is configs[2] (N=65536) on N GPUs"))
-    if out is not None:
-        print(json.dumps(out), flush=True)
+            # the same line again with the configs[3] leg added (the last line supersedes)
+            print(json.dumps(out), flush=True)
     if pg is not None:
         pg.barrier()
         pg.destroy_process_group()

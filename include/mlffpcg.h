@@ -179,6 +179,22 @@ int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out);
 int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha,
                    const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                    double *C, int64_t ldc, int splits);
+/* Iterative._cho_factor_stable (src/sGDML/sgdml/solvers/iterative_solver.py:555-583): the
+ * smallest eigenvalue of the lower triangle of the host m x m matrix M (row-major) --
+ * eigh(M, eigvals_only=True, eigvals=(0, 0)) at :577, computed on the device by Householder
+ * tridiagonalisation and Sturm bisection as LAPACK's dsyevr/dstebz do --, the shift
+ * M +- 1e-15 I (+ when lo_eig <= 0, :578-579) and the Cholesky factor (:580-582).  L_out
+ * (m x m): the lower factor L = U^T of the reference's upper cho_factor (upper triangle
+ * zero); lo_eig_out: the eigenvalue the sign was taken from.  MLFF_ERR_LINALG (-> LinAlgError)
+ * when the shifted matrix is not positive definite.  The Nystrom builds (mlff_precon_nystrom
+ * variant 0, mlff_lev_scores) call the same routine on their device matrices. */
+int mlff_cho_factor_stable(mlff_ctx *ctx, const double *M, int64_t m, double *L_out,
+                           double *lo_eig_out);
+/* The eigenvalue test of mlff_cho_factor_stable alone: lo_eig_out = the smallest eigenvalue of
+ * the lower triangle of M; d_out (m) / e_out (m - 1), optional: the tridiagonal matrix the
+ * device reduction produced (its eigenvalues are M's). */
+int mlff_sym_min_eig(mlff_ctx *ctx, const double *M, int64_t m, double *lo_eig_out,
+                     double *d_out, double *e_out);
 int mlff_sgdml_descriptors(const double *R, int64_t M, int n_atoms, double *R_desc_out,
                            double *R_d_desc_out);
 

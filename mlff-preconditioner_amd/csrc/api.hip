@@ -389,26 +389,18 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   return MLFF_OK;
 }
 
-// _cho_factor_stable (iterative_solver.py:576-583): shift the diagonal by -1e-15
-// when the smallest eigenvalue is positive, +1e-15 otherwise, then Cholesky.  The
-// sign test is done by attempting the factorization: a successful Cholesky of
-// M - 1e-15 I certifies lo_eig > 0 up to rounding; otherwise M + 1e-15 I is used.
-int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k) {
-  ScratchScope scope(ctx);
-  double *tmp = nullptr;
-  MLFF_TRY(scratch_alloc(ctx, &tmp, k * k));
-  MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
-  launch_add_diag(tmp, k, -1e-15, ctx->stream);
-  int rc = potrf_lower(ctx, tmp, k);
-  if (rc == MLFF_ERR_LINALG) {
-    MLFF_HIP(ctx, hipMemcpyAsync(tmp, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
-    launch_add_diag(tmp, k, 1e-15, ctx->stream);
-    rc = potrf_lower(ctx, tmp, k);
-  }
-  if (rc == MLFF_OK)
-    MLFF_HIP(ctx, hipMemcpyAsync(A, tmp, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
-  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return rc;
+// _cho_factor_stable (iterative_solver.py:555-583; :584-618 are unreachable after `if True:`):
+// lo_eig = the smallest eigenvalue of M (eigh of the lower triangle, :577 -- here the
+// device tridiagonalisation + Sturm bisection of kernels_syev.hip), M += (+1e-15 if lo_eig
+// <= 0 else -1e-15) I (:578-579), then the Cholesky factor (:580-582; LinAlgError when it
+// fails).  A (k x k, device) is overwritten with the lower factor; lo_eig_out: the value used.
+int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out) {
+  double lo = 0.0;
+  MLFF_TRY(sym_min_eig(ctx, A, k, &lo, nullptr, nullptr));
+  ctx->last_lo_eig = lo;
+  if (lo_eig_out) *lo_eig_out = lo;
+  launch_add_diag(A, k, lo <= 0.0 ? 1e-15 : -1e-15, ctx->stream);
+  return potrf_lower(ctx, A, k);
 }
 
 // Woodbury panel from a wide factor W = L^T (k x blk) in place:
@@ -486,7 +478,7 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
   MLFF_TRY(allreduce(ctx, Smm, (size_t)(k * k)));
   int rc;
   if (variant == 0) {
-    rc = cho_factor_stable(ctx, Smm, k);          // U^T U = -K_mm (+-1e-15)
+    rc = cho_factor_stable(ctx, Smm, k, nullptr);  // U^T U = -K_mm (+-1e-15)
   } else {
     launch_add_diag(Smm, k, 1e-16, s);            // cholesky(K_mm + 1e-16 I, lower=True)
     rc = potrf_lower(ctx, Smm, k);
@@ -497,7 +489,7 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
   launch_add_diag(G, k, lam, s);
   if (variant == 0)
-    rc = cho_factor_stable(ctx, G, k);
+    rc = cho_factor_stable(ctx, G, k, nullptr);
   else
     rc = potrf_lower(ctx, G, k);
   if (rc != MLFF_OK) return rc;
@@ -1190,6 +1182,37 @@ int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t 
       lda < (ta ? M : K) || ldb < (tb ? K : N) || ldc < N)
     return set_error(ctx, MLFF_ERR_ARG, "test_gemm: bad arguments");
   return test_gemm(ctx, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, splits);
+  MLFF_API_END(ctx)
+}
+
+int mlff_sym_min_eig(mlff_ctx *ctx, const double *M, int64_t m, double *lo_eig_out,
+                     double *d_out, double *e_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (M == nullptr || m < 1 || lo_eig_out == nullptr)
+    return set_error(ctx, MLFF_ERR_ARG, "sym_min_eig: bad arguments");
+  ScratchScope scope(ctx);
+  double *dM = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &dM, (size_t)(m * m)));
+  MLFF_HIP(ctx, hipMemcpyAsync(dM, M, sizeof(double) * m * m, hipMemcpyHostToDevice, ctx->stream));
+  return sym_min_eig(ctx, dM, m, lo_eig_out, d_out, e_out);
+  MLFF_API_END(ctx)
+}
+
+int mlff_cho_factor_stable(mlff_ctx *ctx, const double *M, int64_t m, double *L_out,
+                           double *lo_eig_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (M == nullptr || m < 1 || L_out == nullptr)
+    return set_error(ctx, MLFF_ERR_ARG, "cho_factor_stable: bad arguments");
+  ScratchScope scope(ctx);
+  double *dM = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &dM, (size_t)(m * m)));
+  MLFF_HIP(ctx, hipMemcpyAsync(dM, M, sizeof(double) * m * m, hipMemcpyHostToDevice, ctx->stream));
+  MLFF_TRY(cho_factor_stable(ctx, dM, m, lo_eig_out));
+  MLFF_HIP(ctx, hipMemcpyAsync(L_out, dM, sizeof(double) * m * m, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
   MLFF_API_END(ctx)
 }
 

@@ -253,6 +253,7 @@ struct mlff_ctx {
   unsigned lr_epoch = 0;       // per cluster launch, never 0 in a launch
   int *lr_fault = nullptr;     // ST_FAULT when a cluster hand-off timed out (precon_apply)
   int lr_fallbacks = 0;        // cluster applies that timed out and fell back to two passes
+  double last_lo_eig = 0.0;    // lo_eig of the last _cho_factor_stable (cho_factor_stable)
   double *tpart = nullptr;       // = tpart_base + kVecGrid
   double *tpart_base = nullptr;
   bool spec_t = false;           // tpart already holds T r of the current r (merged collective)
@@ -451,6 +452,11 @@ int gram_wide(mlff_ctx *ctx, const double *A, const double *B, int64_t k, int64_
               int64_t ldw, double *G);
 // in-place lower Cholesky of the k x k matrix A (row-major, ld = k)
 int potrf_lower(mlff_ctx *ctx, double *A, int64_t k);
+// smallest eigenvalue of the lower triangle of a device m x m matrix (kernels_syev.hip:
+// Householder tridiagonalisation + Sturm bisection, the eigh of _cho_factor_stable);
+// d_host / e_host (optional): the tridiagonal
+int sym_min_eig(mlff_ctx *ctx, const double *M, int64_t m, double *lo_eig, double *d_host,
+                double *e_host);
 // W <- L^-1 W, L k x k lower (ld = k), W k x ncols (row stride ldw)
 int trsm_lower_wide(mlff_ctx *ctx, const double *L, int64_t k, double *W, int64_t ncols,
                     int64_t ldw);

@@ -219,6 +219,28 @@ class ShardedKernelSolver:
         r = np.ascontiguousarray(r, dtype=np.float64)
         return self._gather(self._all(lambda q: self.ranks[q].precon_apply(self._local(r, q))))
 
+    # the PCG primitives of KernelSolver over all ranks (global b / x0 / x): the drop-in's
+    # chunked progress / checkpoint loop (solvers/iterative_solver.py _CGStatus) drives these
+    def pcg_start(self, b, x0=None, tol=1e-5, maxiter=None):
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        x0 = None if x0 is None else np.ascontiguousarray(x0, dtype=np.float64)
+        early = self._all(lambda r: self.ranks[r].pcg_start(
+            self._local(b, r), None if x0 is None else self._local(x0, r), tol, maxiter))[0]
+        self._maxiter = self.ranks[0]._maxiter
+        return early
+
+    def pcg_run(self, n_iter, chunk=0):
+        return self._each("pcg_run", n_iter, chunk)[0]
+
+    def pcg_result(self):
+        return self.ranks[0].pcg_result()
+
+    def pcg_x(self):
+        return self._gather(self._each("pcg_x"))
+
+    def pcg_trace(self):
+        return self.ranks[0].pcg_trace()
+
     def pcg(self, b, x0=None, tol=1e-5, maxiter=None, callback=None, cb_every=0, chunk=0):
         """KernelSolver.pcg over all ranks (global b / x0 / x); callback(x, iters, resid)
         sees the gathered iterate."""

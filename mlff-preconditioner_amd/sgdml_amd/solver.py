@@ -279,6 +279,31 @@ class KernelSolver:
         self._call("mlff_precon_get_panel", nat.dptr(T), self.nrows)
         return T
 
+    def cho_factor_stable(self, M: np.ndarray) -> tuple[np.ndarray, float]:
+        """Iterative._cho_factor_stable (iterative_solver.py:555-583) on the device: (L, lo_eig)
+        with L L^T = M +- 1e-15 I (+ when the smallest eigenvalue lo_eig of M's lower triangle
+        is <= 0); LinAlgError when the shifted M is not positive definite."""
+        M = np.ascontiguousarray(M, dtype=np.float64)
+        if M.ndim != 2 or M.shape[0] != M.shape[1]:
+            raise ValueError("M must be square")
+        L = np.empty_like(M)
+        lo = ctypes.c_double()
+        self._call("mlff_cho_factor_stable", nat.dptr(M), M.shape[0], nat.dptr(L), ctypes.byref(lo))
+        return L, lo.value
+
+    def sym_min_eig(self, M: np.ndarray, want_tridiag: bool = False):
+        """Smallest eigenvalue of M's lower triangle (the eigh of _cho_factor_stable,
+        iterative_solver.py:577) on the device; with want_tridiag also the tridiagonal (d, e)."""
+        M = np.ascontiguousarray(M, dtype=np.float64)
+        if M.ndim != 2 or M.shape[0] != M.shape[1]:
+            raise ValueError("M must be square")
+        m = M.shape[0]
+        lo = ctypes.c_double()
+        d = np.empty(m) if want_tridiag else None
+        e = np.empty(max(m - 1, 1)) if want_tridiag else None
+        self._call("mlff_sym_min_eig", nat.dptr(M), m, ctypes.byref(lo), nat.dptr(d), nat.dptr(e))
+        return (lo.value, d, e[: m - 1]) if want_tridiag else lo.value
+
     def lev_scores(self, idx: np.ndarray, lam: float) -> np.ndarray:
         idx = np.ascontiguousarray(idx, dtype=np.int64)
         out = np.empty(self.n)

@@ -26,6 +26,7 @@ What runs where:
 """
 from __future__ import annotations
 
+import collections
 import os
 import timeit
 from functools import partial
@@ -34,7 +35,9 @@ import numpy as np
 
 from .. import _native as nat
 from ..sharded import ShardedKernelSolver
-from ..solver import KernelSolver
+from ..solver import KernelSolver, PCGResult
+
+DONE, NOT_DONE = 1, 0  # sgdml/__init__.py:31-32 (the progress callback's first argument)
 
 LEV_SCORES_KEYS = ["lev_scores", "random_scores", "inverse_lev", "lev_random",
                    "truncated_cholesky", "truncated_cholesky_custom", "rank_k_lev_scores",
@@ -225,15 +228,18 @@ class Iterative(object):
         x0 = None if alphas0_F is None else -np.asarray(alphas0_F, dtype=np.float64)
         # the reference stops the CG after 10 iterations when the spectra are requested (:1002)
         maxiter = 3 * n_atoms * n_train * 5 if not flag_eigvals else 10
-        progress = _Checkpointer(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std,
-                                 inducing_pts_idxs, num_iters0, save_progr_callback)
+        cb = None
+        if self.callback is not None:  # :820-823, :852-853
+            cb = partial(self.callback, disp_str="Initializing solver")
+            cb(NOT_DONE, sec_disp_str=None)
+        status = _CGStatus(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std,
+                           inducing_pts_idxs, num_iters0, n_inducing_pts, save_progr_callback, cb)
         op_storage, op_bytes = solver.storage_info()
         solver.timing(True)
         solver.timing_reset()
         tic = timeit.default_timer()
-        res = solver.pcg(np.asarray(y, dtype=np.float64), x0, tol=float(task["solver_tol"]),
-                         maxiter=maxiter, callback=progress if progress.active else None,
-                         cb_every=progress.every)
+        res = status.run(solver, np.asarray(y, dtype=np.float64), x0, float(task["solver_tol"]),
+                         maxiter)
         total_time_cg = timeit.default_timer() - tic
         t = solver.timing_read()
         alphas = -res.x
@@ -259,6 +265,13 @@ class Iterative(object):
             info.update(info_cholesky)
         if eig_info is not None:
             info.update(eig_info)  # iterative_solver.py:1100-1102
+        if cb is not None:  # :1074-1086
+            cb(DONE, disp_str="Training on {:,} points{}".format(
+                n_train, "" if is_conv else " (NOT CONVERGED)"),
+               sec_disp_str="{:d} iter @ {} iter/s".format(
+                   num_iters, "{:.1f}".format(num_iters / status.avg_tt)
+                   if status.avg_tt > 0 else "--"),
+               done_with_warning=not is_conv)
         train_rmse = resid / np.sqrt(len(y))
         return alphas, num_iters, resid, train_rmse, inducing_pts_idxs, is_conv, info
 
@@ -269,29 +282,132 @@ class Iterative(object):
         return rowlev
 
 
-class _Checkpointer:
-    """The reference's 2-minute checkpoint in _cg_status (iterative_solver.py:919-954):
-    an unconverged model built from -x_k handed to save_progr_callback."""
+class _CGStatus:
+    """The reference's per-iteration CG callback `_cg_status` (iterative_solver.py:874-965)
+    around the chunked device PCG.
+
+    scipy 1.7.3 calls it once per iteration with the iterate x_j (j = 1 ... m; the caller-frame
+    `resid` it reads is the stop-test residual of that iterate, trace[j]).  In it the
+    reference keeps (module globals) num_iters (= num_iters0 + calls so far), the per-call
+    wall time tt, avg_tt = sum tt, and the last CG_STEPS_HIST_LEN = 100 residual steps, and
+      * once per second -- when tt > 0 and num_iters % ceil(1 / tt) == 0 -- calls
+        callback(NOT_DONE, disp_str='Training error (RMSE): forces ...',
+        sec_disp_str='<num_iters> iter @ <1/tt> iter/s [eff: <eff>%] k: <n_inducing_pts>'),
+        eff = (int(100 * ratio) - 50) * 2, ratio = -sum(negative steps) / sum |steps|;
+      * every two minutes -- num_iters % ceil(120 / tt) == 0 -- builds the unconverged model
+        of -x_j (create_model, solver_iters = num_iters + 1, solver_resid = resid), its
+        integration constant c = sum(E_ref - E_pred) / M from a prediction of the training
+        energies with those coefficients (:942-951), and hands it to save_progr_callback.
+    Here the iterations run on the device in chunks that end exactly on the iterations where
+    one of the two conditions holds for the per-iteration time measured over the previous
+    chunk (tt of every call in a chunk = that chunk's average; the first call has tt = 0 as
+    in the reference); the bookkeeping of every call inside a chunk is replayed from the
+    device's residual trace, so eff and num_iters are the reference's.  Without a callback
+    and save_progr_callback the PCG runs in one piece."""
+
+    HIST_LEN = 100          # CG_STEPS_HIST_LEN (iterative_solver.py:57-59)
+    PROGRESS_S = 1.0        # "once per second" (:899)
+    CHECKPOINT_S = 120.0    # "once every 2 minutes" (:919-920)
+    FIRST_CHUNK = 8         # iterations timed before the first planned stop
 
     def __init__(self, it, task, R_desc, R_d_desc, tril_perms_lin, y, y_std, idxs, iters0,
-                 save_progr_callback, period_s=120.0):
+                 n_inducing_pts, save_progr_callback, cb):
         self.it, self.task = it, task
         self.R_desc, self.R_d_desc, self.tpl = R_desc, R_d_desc, tril_perms_lin
-        self.y, self.y_std, self.idxs, self.iters0 = y, y_std, idxs, iters0
-        self.cb = save_progr_callback
-        self.period = period_s
-        self.last = timeit.default_timer()
-        self.active = save_progr_callback is not None and it.gdml_train is not None
-        self.every = 256 if self.active else 0
+        self.y, self.y_std, self.idxs = y, y_std, idxs
+        self.iters0, self.k = int(iters0), int(n_inducing_pts)
+        self.save = save_progr_callback if it.gdml_train is not None else None
+        self.cb = cb
+        self.num_iters = int(iters0)
+        self.resid = 0.0
+        self.avg_tt = 0.0
+        self.calls = 0
+        self.hist = collections.deque(maxlen=self.HIST_LEN)
+        self.eff = 0
+        self.checkpoints = []  # (iterate j, solver_iters) of every model handed over
 
-    def __call__(self, x, iters, resid):
-        now = timeit.default_timer()
-        if now - self.last < self.period:
+    @property
+    def active(self):
+        return self.cb is not None or self.save is not None
+
+    def _period(self, tt, seconds):
+        return int(np.ceil(seconds / tt))
+
+    def _next_stop(self, j, tt, maxiter):
+        """Smallest iterate index > j whose call has num_iters = iters0 + index - 1 divisible
+        by the progress or the checkpoint period (of the per-iteration time tt)."""
+        cand = [maxiter]
+        for sec, on in ((self.PROGRESS_S, self.cb is not None), (self.CHECKPOINT_S, self.save is not None)):
+            if on:
+                P = self._period(tt, sec)
+                base = self.iters0 + j  # num_iters of the call of iterate j + 1
+                cand.append(j + 1 + (-base) % P)
+        return min(cand)
+
+    def _replay(self, trace, j0, j1, tt):
+        """Bookkeeping of the calls of iterates j0 + 1 ... j1 (everything except the displays)."""
+        for j in range(j0 + 1, j1 + 1):
+            t = 0.0 if self.calls == 0 else tt
+            self.avg_tt += t
+            old, self.resid = self.resid, float(trace[j])
+            step = 0.0 if self.num_iters == 0 else self.resid - old
+            self.hist.append(step)
+            h = np.asarray(self.hist)
+            tot = np.abs(h).sum()
+            ratio = (-h.clip(max=0).sum() / tot) if tot > 0 else 1
+            self.eff = 0 if self.num_iters == 0 else (int(100 * ratio) - 50) * 2
+            self.calls += 1
+            if j < j1:
+                self.num_iters += 1
+        # num_iters is now that of the call of iterate j1 (incremented after it by the caller)
+
+    def _at_stop(self, solver, j, tt):
+        if tt <= 0.0:
             return
-        self.last = now
+        if self.cb is not None and self.num_iters % self._period(tt, self.PROGRESS_S) == 0:
+            rmse = self.resid / np.sqrt(len(self.y))
+            self.cb(NOT_DONE, disp_str="Training error (RMSE): forces {:.4f}".format(rmse),
+                    sec_disp_str="{:d} iter @ {} iter/s [eff: {:d}%] k: {:d}".format(
+                        self.num_iters, "{:.1f}".format(1.0 / tt), self.eff, self.k))
+        if self.save is not None and self.num_iters % self._period(tt, self.CHECKPOINT_S) == 0:
+            self.save(self.checkpoint_model(solver.pcg_x(), solver))
+            self.checkpoints.append((j, self.num_iters + 1))
+
+    def checkpoint_model(self, x, solver):
+        """:922-951: the unconverged model of -x and its integration constant."""
+        alphas_F = -np.asarray(x)
         model = self.it.gdml_train.create_model(
-            self.task, "cg", self.R_desc, self.R_d_desc, self.tpl, self.y_std, -x,
-            alphas_E=None, solver_resid=resid, solver_iters=self.iters0 + iters + 1,
+            self.task, "cg", self.R_desc, self.R_d_desc, self.tpl, self.y_std, alphas_F,
+            alphas_E=None, solver_resid=self.resid, solver_iters=self.num_iters + 1,
             norm_y_train=np.linalg.norm(self.y), inducing_pts_idxs=self.idxs)
-        model["c"] = 0.0
-        self.cb(model)
+        _, E = solver.sgdml_energies(alphas_F)  # GDMLPredict with these alphas, c = 0, std 1
+        E_pred = E * self.y_std
+        E_ref = np.squeeze(self.task["E_train"])
+        model["c"] = np.sum(E_ref - E_pred) / E_ref.shape[0]
+        return model
+
+    def run(self, solver, y, x0, tol, maxiter):
+        if not self.active:
+            return solver.pcg(y, x0, tol=tol, maxiter=maxiter)
+        early = solver.pcg_start(y, x0, tol, maxiter)
+        j, status, _, _ = solver.pcg_result()
+        tt = 0.0
+        while status == nat.PCG_RUNNING:
+            stop = min(maxiter, j + self.FIRST_CHUNK) if tt <= 0.0 else \
+                self._next_stop(j, tt, maxiter)
+            t0 = timeit.default_timer()
+            solver.pcg_run(stop - j)
+            el = timeit.default_timer() - t0
+            j1, status, _, _ = solver.pcg_result()
+            tr = solver.pcg_trace()
+            tt_chunk = el / max(j1 - j, 1)
+            if j1 > j:
+                self._replay(tr, j, j1, tt if tt > 0.0 else tt_chunk)
+                if j1 == stop:
+                    self._at_stop(solver, j1, tt)
+                self.num_iters += 1
+            j, tt = j1, tt_chunk
+        it, status, resid, info = solver.pcg_result()
+        return PCGResult(x=solver.pcg_x(), info=info, iters=it, resid=resid,
+                         trace=solver.pcg_trace(), early_exit=early,
+                         callbacks=0 if early else max(it, 1))

@@ -418,6 +418,66 @@ def fx_lev_scores():
          lam=np.float64(1e-10))
 
 
+def fx_cho_stable():
+    """_cho_factor_stable's eigenvalue sign test (iterative_solver.py:555-583) on a nearly
+    singular K_mm: ethanol-like M = 10 plus a copy of geometry 0 moved by `delta` (point 10),
+    27 inducing columns that hold 4 columns of point 0 and the same 4 of its copy.  The
+    smallest eigenvalue of -K_mm then shrinks like delta^2: delta = 3e-7 puts it in
+    (0, 1e-15), where the reference shifts by -1e-15 and its Cholesky fails (LinAlgError from
+    the Nystrom build and from _lev_scores); delta = 1e-6 / 1e-5 put it just above 1e-15 /
+    well above; delta = 0 is an exact duplicate (lo_eig at the rounding level: recorded, not
+    a parity case).  Recorded per delta: the reference's K_mm (from its own column-panel
+    assembly, :112-124), lo_eig of -K_mm (eigh as at :577), the Nystrom variant-0 apply P_op v
+    (:95-322) or its exception, the _lev_scores output (:447-552, the columns forced through
+    idxs_ordered_by_lev_score) or its exception, and the oracle's apply distance to the
+    reference's (the NumPy restatement's own rounding spread)."""
+    if str(REPO) not in sys.path:
+        sys.path.append(str(REPO))
+    from oracle.precon import apply_panel, nystrom_panel
+
+    pairs = [0, 1, 5, 13]
+    other = np.linspace(27, 269, 19).astype(np.int64)
+    idx = np.sort(np.r_[pairs, [270 + i for i in pairs], other]).astype(np.int64)
+    assert idx.size == 27 and np.unique(idx).size == 27
+    out = {"idx": idx, "deltas": np.array([0.0, 3e-7, 1e-6, 1e-5])}
+    for t, delta in enumerate(out["deltas"]):
+        ds = synthetic.ethanol_like(10, seed=3)
+        shift = np.random.default_rng(9).standard_normal(ds["R"][0].shape)
+        for key in ("R", "F", "E"):
+            ds[key] = np.concatenate([ds[key], ds[key][:1]])
+        ds["R"][10] = ds["R"][10] + delta * shift
+        task = make_task(ds)
+        desc, tpl, R_desc, R_d_desc, y, y_std = prepare(task)
+        n = y.size
+        K_nm = gdml_train()._assemble_kernel_mat(R_desc, R_d_desc, tpl, 10, desc, use_E_cstr=False,
+                                                 col_idxs=idx, callback=noop)
+        M = -np.array(K_nm)[idx, :]
+        lo = float(scipy.linalg.eigh(M, eigvals_only=True, eigvals=(0, 0))[0])
+        it, _ = kernel_operator(task, desc, R_desc, R_d_desc, tpl, n)
+        v = np.random.default_rng(31).standard_normal(n)
+        out[f"R_{t}"], out[f"Kmm_{t}"], out[f"lo_eig_{t}"] = ds["R"], M, np.float64(lo)
+        out[f"v_{t}"] = v
+        try:
+            z = _nystrom_apply(it, dict(task, lam=1e-10), R_desc, R_d_desc, tpl, idx, 0, v)
+            out[f"nys0_z_{t}"] = z
+            B, sp = nystrom_panel(-np.array(K_nm), idx, 1e-10, 0)
+            zo = apply_panel(B, sp, 1e-10, v)
+            out[f"nys0_oracle_rel_{t}"] = np.float64(np.linalg.norm(zo - z) / np.linalg.norm(z))
+        except np.linalg.LinAlgError as e:
+            out[f"nys0_error_{t}"] = np.array(type(e).__name__)
+        order = np.r_[np.setdiff1d(np.arange(n), idx), idx]  # the last dim_m = 27 are idx
+        try:
+            lev, _ = it._lev_scores(R_desc, R_d_desc, tpl, 10, 1e-10, False, 4,
+                                    idxs_ordered_by_lev_score=order,
+                                    callback=lambda *a, **k: None)
+            out[f"lev_{t}"] = lev
+        except np.linalg.LinAlgError as e:
+            out[f"lev_error_{t}"] = np.array(type(e).__name__)
+        print(f"  delta={delta:.0e} lo_eig={lo:.3e} nys0={'z' if f'nys0_z_{t}' in out else 'error'} "
+              f"lev={'ok' if f'lev_{t}' in out else 'error'}", flush=True)
+    save("cho_stable_ethanol", **out)
+
+
 def fx_model():
     """GDMLTrain.train end to end for solver 'cg' (train.py:707-970: label normalisation,
     lam = 1e-10, Iterative.solve, create_model :597-702, model.update(info),
@@ -562,6 +622,7 @@ FIXTURES = {
     "sgdml_nanotube_n3330": lambda: fx_sgdml(
         3, "sgdml_nanotube_n3330", ["cholesky", "random_scores"], seed=4, with_K=False,
         none_tol=(), geom="nanotube", k_rows=16),
+    "cho_stable": fx_cho_stable,
     "sgdml_n621": lambda: fx_sgdml(
         23, "sgdml_ethanol_n621", ["cholesky", "random_scores", "truncated_cholesky"], seed=7,
         none_tol=(1e-4,)),

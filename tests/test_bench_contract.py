@@ -34,13 +34,26 @@ def test_reference_step_times_are_baseline_md():
     assert bench.REF_STEP_S == {15540: 0.105, 156510: 2.073, 505050: 6.600}
 
 
-@pytest.mark.parametrize("key", ["rbf_n65536_nystrom256/sym/gpus1",
-                                 "sgdml_nanotube_n15540_pivchol2701/matfree/gpus1"])
-def test_pmc_traffic_lookup(key):
-    workload, storage, g = key.split("/")
-    v = bench.pmc_traffic(workload, storage, int(g[4:]))
-    assert v is not None and v > 0
-    assert bench.pmc_traffic("no_such_workload", "sym", 1) is None
+def test_pmc_traffic_is_refused_when_stale(tmp_path, monkeypatch):
+    """bench.py reports PMC traffic only for entries collected on the current sources
+    (scripts/pmc_head.py stamps csrc_sha); anything else is null with the reason."""
+    key = "rbf_n65536_nystrom256/sym/gpus1"
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "pmc_traffic.json").write_text(json.dumps({
+        key: {"hbm_bytes_per_launch": 1.7e10, "csrc_sha": bench.csrc_hash()},
+        "old/sym/gpus1": {"hbm_bytes_per_launch": 1.0, "csrc_sha": "0123456789abcdef"},
+        "unstamped/sym/gpus1": {"hbm_bytes_per_launch": 1.0}}))
+    real = bench.REPO
+    monkeypatch.setattr(bench, "REPO", tmp_path)
+    (tmp_path / "mlff-preconditioner_amd").symlink_to(real / "mlff-preconditioner_amd")
+    (tmp_path / "include").symlink_to(real / "include")
+    assert bench.pmc_traffic(key) == (1.7e10, None)
+    for k in ("old/sym/gpus1", "unstamped/sym/gpus1"):
+        v, why = bench.pmc_traffic(k)
+        assert v is None and why.startswith("stale")
+    v, why = bench.pmc_traffic("no_such/sym/gpus1")
+    assert v is None and "no PMC entry" in why
 
 
 def test_usable_cores_is_consistent():

@@ -1,0 +1,163 @@
+"""_cho_factor_stable on the GPU (src/sGDML/sgdml/solvers/iterative_solver.py:555-583).
+
+The reference takes the smallest eigenvalue of M (eigh, :577), shifts M by +1e-15 I when it
+is <= 0 and by -1e-15 I otherwise, and Cholesky-factors (LinAlgError when that fails).  The
+device computes lo_eig with the same algorithm class as LAPACK's dsyevr for one eigenvalue
+(Householder tridiagonalisation + Sturm bisection, csrc/kernels_syev.hip).
+
+* sym_min_eig vs scipy's eigh on matrices with prescribed spectra (sizes 1 ... 700, smallest
+  eigenvalue positive, zero-crossing, negative): |d lo_eig| <= 4 m eps ||M|| (both values
+  carry a backward error of that order), the sign wherever |lo_eig| exceeds that bound, and
+  the tridiagonal's full spectrum against eigvalsh.
+* tests/golden/cho_stable_ethanol.npz (make_golden.py fx_cho_stable, the reference run on a
+  nearly singular K_mm: geometry 0 and a copy moved by delta among 27 inducing columns):
+    delta = 3e-7: lo_eig = 1.26e-16 in (0, 1e-15) -> the reference shifts DOWN and its
+      Cholesky fails: the Nystrom build and _lev_scores raise LinAlgError -- here too.  (The
+      round-2 try-factor sign test shifted up and succeeded: VERDICT r2 item 1.)
+    delta = 1e-6 / 1e-5: lo_eig = 1.4e-15 / 1.4e-13 -> shift down, factor succeeds; the GPU's
+      Nystrom apply and leverage scores against the reference's (tolerances below).
+    delta = 0: an exact duplicate, lo_eig = -2e-18 at the rounding level of eigh (~7e-18 =
+      eps ||M||): the sign is noise in the reference itself; only consistency is checked.
+"""
+import numpy as np
+import pytest
+import scipy.linalg
+
+pytestmark = pytest.mark.gpu
+
+EPS = np.finfo(np.float64).eps
+
+
+@pytest.fixture(scope="module")
+def sg():
+    import sgdml_amd
+
+    if sgdml_amd.device_count() < 1:
+        pytest.fail("no GPU visible to libmlffpcg.so")
+    return sgdml_amd
+
+
+def spd_with_spectrum(m, lo, hi, seed, lo_eig=None):
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.standard_normal((m, m)))
+    ev = np.geomspace(lo, hi, m) if lo > 0 else np.linspace(lo, hi, m)
+    if lo_eig is not None:
+        ev[0] = lo_eig
+    M = (Q * ev) @ Q.T
+    # a slightly asymmetric upper triangle: only the lower one may be read (eigh UPLO='L')
+    M[np.triu_indices(m, 1)] += 1e-3 * hi
+    return M
+
+
+CASES = [(1, 0.5, 0.5, None), (2, 1e-3, 1.0, None), (5, 1e-8, 2.0, None),
+         (64, 1e-12, 1.0, None), (100, 1e-10, 3.0, -1e-9), (300, 1e-6, 1.0, -2e-13),
+         (300, 1e-6, 1.0, 3e-13), (700, 1e-9, 10.0, None), (129, -1.0, 1.0, None)]
+
+
+@pytest.mark.parametrize("m,lo,hi,lo_eig", CASES)
+def test_sym_min_eig_vs_lapack(sg, m, lo, hi, lo_eig):
+    M = spd_with_spectrum(m, lo, hi, seed=m, lo_eig=lo_eig)
+    Ml = np.tril(M) + np.tril(M, -1).T
+    ref = scipy.linalg.eigh(M, eigvals_only=True, subset_by_index=[0, 0])[0]
+    with sg.KernelSolver(8) as s:
+        got, d, e = s.sym_min_eig(M, want_tridiag=True)
+    norm = np.linalg.norm(Ml, 2)
+    bound = 4 * m * EPS * norm
+    assert abs(got - ref) <= bound, (got, ref, bound)
+    if abs(ref) > bound:
+        assert np.sign(got) == np.sign(ref)
+    # the tridiagonal is similar to M: all of its eigenvalues
+    ev_t = scipy.linalg.eigvalsh_tridiagonal(d, e) if m > 1 else d
+    np.testing.assert_allclose(ev_t, np.linalg.eigvalsh(Ml), rtol=0, atol=bound)
+
+
+@pytest.mark.parametrize("m,lo_eig,sign", [(40, -5e-16, +1), (40, 3e-15, -1), (200, 5e-12, -1)])
+def test_cho_factor_stable_shift_and_factor(sg, m, lo_eig, sign):
+    """Clear-cut signs (|lo_eig| >> 4 m eps ||M||, ||M|| = 1e-3) that the shift turns positive
+    definite: the shift direction, the sign's eigenvalue, and the factor's backward error
+    against the shifted matrix (cond up to 2e12: the factors themselves agree only to
+    ~cond eps)."""
+    M = spd_with_spectrum(m, 1e-9, 1e-3, seed=7 + m, lo_eig=lo_eig)
+    M = np.tril(M) + np.tril(M, -1).T
+    ref_lo = scipy.linalg.eigh(M, eigvals_only=True, subset_by_index=[0, 0])[0]
+    Ms = M + (1e-15 if ref_lo <= 0 else -1e-15) * np.eye(m)
+    with sg.KernelSolver(8) as s:
+        L, lo = s.cho_factor_stable(M)
+    assert np.sign(lo) == -sign and abs(lo - ref_lo) <= 4 * m * EPS * 1e-3
+    scipy.linalg.cho_factor(Ms, lower=False)  # the reference's factorization succeeds too
+    np.testing.assert_array_equal(np.triu(L, 1), 0.0)
+    assert np.abs(L @ L.T - Ms).max() <= 8 * m * EPS * 1e-3
+
+
+def test_cho_factor_stable_raises_like_the_reference(sg):
+    """lo_eig in (0, 1e-15) with a clear sign: shift -1e-15 -> not positive definite ->
+    LinAlgError (the reference's cho_factor raises at :580-582)."""
+    M = spd_with_spectrum(60, 1e-6, 1e-3, seed=3, lo_eig=4e-16)
+    M = np.tril(M) + np.tril(M, -1).T
+    assert scipy.linalg.eigh(M, eigvals_only=True, subset_by_index=[0, 0])[0] > 0
+    with pytest.raises(np.linalg.LinAlgError):
+        scipy.linalg.cho_factor(M - 1e-15 * np.eye(60))
+    with sg.KernelSolver(8) as s:
+        with pytest.raises(np.linalg.LinAlgError):
+            s.cho_factor_stable(M)
+
+
+def _solver_for(sg, f, t):
+    R = f[f"R_{t}"]
+    M_pts, n_atoms = R.shape[:2]
+    n = 3 * n_atoms * M_pts
+    Rd, Rdd = sg.sgdml_descriptors(R)
+    s = sg.KernelSolver(n)
+    s.sgdml_operator(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
+    s.set_operator(-1.0, 1e-10)
+    return s
+
+
+def test_golden_lo_eig_sign(sg, golden_dir):
+    f = np.load(golden_dir / "cho_stable_ethanol.npz", allow_pickle=False)
+    with sg.KernelSolver(8) as s:
+        for t in range(len(f["deltas"])):
+            M = f[f"Kmm_{t}"]
+            lo_ref = float(f[f"lo_eig_{t}"])
+            lo = s.sym_min_eig(M)
+            print(f"delta index {t}: lo_eig device {lo:.6e} reference {lo_ref:.6e}")
+            bound = 4 * M.shape[0] * EPS * np.linalg.norm(M, 2)
+            assert abs(lo - lo_ref) <= bound, (t, lo, lo_ref, bound)
+            if t >= 1:  # the cases whose sign is above eigh's rounding (fixture docstring)
+                assert np.sign(lo) == np.sign(lo_ref), (t, lo, lo_ref)
+
+
+# Nystrom apply / leverage scores vs the reference on K_mm with cond ~ 4e13 (delta = 1e-6) and
+# ~4e11 (1e-5): the GPU forms K_nm from its own matrix-free columns, so the inputs already
+# differ at the rounding level; measured distances in the file's docstring / DESIGN.md 5.
+NYS_TOL = {2: 1e-6, 3: 1e-8}
+LEV_TOL = {2: 1e-6, 3: 1e-8}
+
+
+@pytest.mark.parametrize("t", [1, 2, 3])
+def test_golden_nystrom_and_lev_scores(sg, golden_dir, t):
+    f = np.load(golden_dir / "cho_stable_ethanol.npz", allow_pickle=False)
+    idx = f["idx"]
+    s = _solver_for(sg, f, t)
+    try:
+        if f"nys0_error_{t}" in f.files:
+            with pytest.raises(np.linalg.LinAlgError):
+                s.precon_nystrom(idx, variant=0)
+        else:
+            s.precon_nystrom(idx, variant=0)
+            z = s.precon_apply(f[f"v_{t}"])
+            zr = f[f"nys0_z_{t}"]
+            rel = np.linalg.norm(z - zr) / np.linalg.norm(zr)
+            print(f"delta index {t}: Nystrom apply rel {rel:.3e}")
+            assert rel <= NYS_TOL[t], (t, rel)
+        if f"lev_error_{t}" in f.files:
+            with pytest.raises(np.linalg.LinAlgError):
+                s.lev_scores(idx, 1e-10)
+        else:
+            lev = s.lev_scores(idx, 1e-10)
+            lr = f[f"lev_{t}"]
+            rel = np.abs(lev - lr).max() / np.abs(lr).max()
+            print(f"delta index {t}: leverage scores rel {rel:.3e}")
+            assert rel <= LEV_TOL[t], (t, rel)
+    finally:
+        s.close()
