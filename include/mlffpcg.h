@@ -267,6 +267,12 @@ int mlff_precon_lowrank(mlff_ctx *ctx, const double *Lt_local, int64_t k);
 int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int build_woodbury,
                     double *evals_out, double *rowlev_out);
 int mlff_precon_info(mlff_ctx *ctx, int *kind_out, int64_t *k_out);
+/* Convergence of the last truncated eigensolve (mlff_precon_eig): converged_out = 1 when every
+ * one of the k leading Ritz pairs met ||S u - theta u|| <= 1e-11 |theta_0|; otherwise the
+ * pairs after the iteration cap were accepted because they met 1e-6 (a slowly decaying
+ * spectrum around k), rel_resid_out = the worst residual / |theta_0|.  The reference's full SVD
+ * (iterative_solver.py:1297-1329) has no such state; the drop-in turns it into a warning. */
+int mlff_eig_info(mlff_ctx *ctx, int *converged_out, double *rel_resid_out);
 /* z_local = M r_local (collective over ranks for the low-rank part) */
 int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local);
 /* How this rank's low-rank apply (iterative_cholesky.py:145-148 z = (r - T^T T r) / lam)

@@ -48,15 +48,33 @@ int api_exception(mlff_ctx *ctx, int code, const char *what) {
   }
 }
 
-ScratchScope::ScratchScope(mlff_ctx *c) : ctx(c), chunk(c->scratch_cur), off(c->scratch_off) {}
+constexpr size_t kScratchChunk = size_t(64) << 20;
 
+ScratchScope::ScratchScope(mlff_ctx *c) : ctx(c), chunk(c->scratch_cur), off(c->scratch_off) {
+  ++ctx->scratch_depth;
+}
+
+// Closing the outermost scope returns every chunk but one standard-size chunk to the device
+// (after the stream has drained the kernels that used them): build temporaries such as the
+// k x k Woodbury Gram, eigensolver panels or split-K slabs do not stay allocated through the
+// PCG that follows.
 ScratchScope::~ScratchScope() {
   ctx->scratch_cur = chunk;
   ctx->scratch_off = off;
+  if (--ctx->scratch_depth != 0) return;
+  auto &ch = ctx->scratch_chunks;
+  const bool keep_first = !ch.empty() && ch[0].size == kScratchChunk;
+  if (ch.size() > (keep_first ? 1u : 0u)) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (size_t i = keep_first ? 1 : 0; i < ch.size(); ++i) (void)hipFree(ch[i].p);
+    ch.resize(keep_first ? 1 : 0);
+  }
+  ctx->scratch_cur = 0;
+  ctx->scratch_off = 0;
 }
 
 int scratch_get(mlff_ctx *ctx, size_t bytes, void **out) {
-  constexpr size_t kAlign = 256, kChunk = size_t(64) << 20;
+  constexpr size_t kAlign = 256, kChunk = kScratchChunk;
   bytes = (bytes + kAlign - 1) / kAlign * kAlign;
   auto &ch = ctx->scratch_chunks;
   while (true) {
@@ -1452,6 +1470,15 @@ int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int 
     ctx->k = k;
     ctx->sigma_p = 1.0;
   }
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
+int mlff_eig_info(mlff_ctx *ctx, int *converged_out, double *rel_resid_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (converged_out) *converged_out = ctx->eig_converged ? 1 : 0;
+  if (rel_resid_out) *rel_resid_out = ctx->eig_rel_resid;
   return MLFF_OK;
   MLFF_API_END(ctx)
 }

@@ -253,7 +253,9 @@ struct mlff_ctx {
   unsigned lr_epoch = 0;       // per cluster launch, never 0 in a launch
   int *lr_fault = nullptr;     // ST_FAULT when a cluster hand-off timed out (precon_apply)
   int lr_fallbacks = 0;        // cluster applies that timed out and fell back to two passes
-  double last_lo_eig = 0.0;    // lo_eig of the last _cho_factor_stable (cho_factor_stable)
+  double last_lo_eig = 0.0;
+  bool eig_converged = true;   // last truncated eigensolve met kEigTol (kernels_eig.hip)
+  double eig_rel_resid = 0.0;  // its worst Ritz residual / |theta_0|    // lo_eig of the last _cho_factor_stable (cho_factor_stable)
   double *tpart = nullptr;       // = tpart_base + kVecGrid
   double *tpart_base = nullptr;
   bool spec_t = false;           // tpart already holds T r of the current r (merged collective)
@@ -277,6 +279,7 @@ struct mlff_ctx {
   };
   std::vector<ScratchChunk> scratch_chunks;
   size_t scratch_cur = 0, scratch_off = 0;
+  int scratch_depth = 0;  // open ScratchScopes
 };
 
 namespace mlff {

@@ -82,6 +82,7 @@ SIGNATURES = {
     "mlff_precon_apply": (_int, [_c_ctx, _p_dbl, _p_dbl]),
     "mlff_precon_get_panel": (_int, [_c_ctx, _p_dbl, _i64]),
     "mlff_lev_scores": (_int, [_c_ctx, _p_i64, _i64, _dbl, _p_dbl]),
+    "mlff_eig_info": (_int, [_c_ctx, _p_int, _p_dbl]),
     "mlff_cho_factor_stable": (_int, [_c_ctx, _p_dbl, _i64, _p_dbl, _p_dbl]),
     "mlff_sym_min_eig": (_int, [_c_ctx, _p_dbl, _i64, _p_dbl, _p_dbl, _p_dbl]),
     "mlff_pcg_start": (_int, [_c_ctx, _p_dbl, _p_dbl, _dbl, _i64, _p_int]),

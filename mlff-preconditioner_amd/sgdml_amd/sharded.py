@@ -182,6 +182,9 @@ class ShardedKernelSolver:
         return self._each("precon_eig", k, mask_mode, dim_i, build_woodbury, want_evals,
                           want_rowlev)[0]
 
+    def eig_info(self):
+        return self.ranks[0].eig_info()
+
     def lev_scores(self, idx, lam):
         return self._each("lev_scores", idx, lam)[0]  # global scores on every rank
 

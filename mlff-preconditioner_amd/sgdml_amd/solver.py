@@ -254,6 +254,12 @@ class KernelSolver:
                    nat.dptr(ev), nat.dptr(rl))
         return ev, rl
 
+    def eig_info(self) -> tuple[bool, float]:
+        """(converged to 1e-11, worst Ritz residual / |theta_0|) of the last precon_eig."""
+        c, r = ctypes.c_int(), ctypes.c_double()
+        self._call("mlff_eig_info", ctypes.byref(c), ctypes.byref(r))
+        return bool(c.value), r.value
+
     def precon_info(self) -> tuple[int, int]:
         kind, k = ctypes.c_int(), ctypes.c_int64()
         self._call("mlff_precon_info", ctypes.byref(kind), ctypes.byref(k))

@@ -29,6 +29,7 @@ from __future__ import annotations
 import collections
 import os
 import timeit
+import warnings
 from functools import partial
 
 import numpy as np
@@ -122,6 +123,7 @@ class Iterative(object):
         mask = {"eigvec_precon": 0, "eigvec_precon_block_diagonal": 1,
                 "eigvec_precon_atomic_interactions": 2}[name]
         solver.precon_eig(k, mask_mode=mask, dim_i=dim_i, build_woodbury=True)
+        _warn_eig(solver)
 
     # --------------------------------------------------------------- solve
     def solve(self, task, R_desc, R_d_desc, tril_perms_lin, y, y_std, save_progr_callback=None,
@@ -279,7 +281,17 @@ class Iterative(object):
         """_rank_k_leverage_scores (iterative_solver.py:1110-1175): ||U[:, :k] row||."""
         k = int(np.max([int(break_percentage * n), 1]))
         _, rowlev = solver.precon_eig(k, mask_mode=0, build_woodbury=False, want_rowlev=True)
+        _warn_eig(solver)
         return rowlev
+
+
+def _warn_eig(solver):
+    """The truncated eigensolver's pairs were accepted at a looser tolerance (mlff_eig_info)."""
+    converged, rel = solver.eig_info()
+    if not converged:
+        warnings.warn(f"truncated eigensolver: the leading Ritz pairs reached a relative residual of "
+                      f"{rel:.1e} (target 1e-11) within the iteration cap; the preconditioner is "
+                      f"built from them", RuntimeWarning, stacklevel=3)
 
 
 class _CGStatus:

@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-3 GPU session: STEPS (space separated) from
+#   suite   driver-exact `pytest -m gpu` (per-test timeout, progress log)
+#   smoke   __graft_entry__.smoke()
+#   bench   default bench line (python bench.py) -> gpurun_out/r03/bench_default.txt
+#   nt      nanotube bench line (configs[1])
+#   lrab    interleaved A/B of the low-rank apply form at configs[2] (cluster vs two passes)
+#   pmc     scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes, rbf + nanotube)
+#   prof    rocprofv3 --kernel-trace --stats of the default bench command
+# every GPU step runs under its own timeout; the first failure ends the script
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r03
+mkdir -p $O
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name $(date +%T)" | tee -a $O/steps.log
+  timeout -k 10 $lim "$@" > $O/$name.txt 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)" | tee -a $O/steps.log
+  if [ $rc -ne 0 ]; then tail -30 $O/$name.txt; exit $rc; fi
+}
+for s in ${STEPS:-suite smoke bench}; do
+  case $s in
+    suite) step suite 1100 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench_default 600 python bench.py ;;
+    nt) step bench_nanotube 300 python bench.py --workload nanotube ;;
+    lrab)
+      for r in 1 2 3; do
+        step lrab_default_$r 200 python bench.py --no-cpu --no-solve --configs3-n 0
+        step lrab_twopass_$r 200 env MLFF_LR_ROWS=0 python bench.py --no-cpu --no-solve --configs3-n 0
+      done ;;
+    pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
+  esac
+done
+echo "== all done $(date +%T)" | tee -a $O/steps.log

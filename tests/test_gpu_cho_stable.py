@@ -129,9 +129,12 @@ def test_golden_lo_eig_sign(sg, golden_dir):
 
 # Nystrom apply / leverage scores vs the reference on K_mm with cond ~ 4e13 (delta = 1e-6) and
 # ~4e11 (1e-5): the GPU forms K_nm from its own matrix-free columns, so the inputs already
-# differ at the rounding level; measured distances in the file's docstring / DESIGN.md 5.
-NYS_TOL = {2: 1e-6, 3: 1e-8}
-LEV_TOL = {2: 1e-6, 3: 1e-8}
+# differ at the rounding level and the factorizations amplify that by up to cond(K_mm).
+# Measured on MI355X (round 3): apply 2.6e-9 / 1.8e-10, leverage scores 5.1e-9 / 4.8e-10;
+# device lo_eig -7.7e-19 / 1.294e-16 / 1.4210e-15 / 1.42111e-13 against the reference's
+# -2.2e-18 / 1.263e-16 / 1.4191e-15 / 1.42111e-13.  Tolerances ~10x the measurement.
+NYS_TOL = {2: 2e-8, 3: 2e-9}
+LEV_TOL = {2: 5e-8, 3: 5e-9}
 
 
 @pytest.mark.parametrize("t", [1, 2, 3])

@@ -291,3 +291,60 @@ def test_rank_failure_aborts_group():
             s.close()
 
     assert run_ranks(2, body, timeout=60) == [True, True]
+
+
+@pytest.mark.timeout(1100)
+def test_configs3_eight_ranks_full_size():
+    """BASELINE configs[3] at its full size: N = 131072 RBF (the bench's generator), rank-256
+    Nystrom, 8 row blocks of 16384 on the symmetric tiles (8.6 GB of tiles per rank, 69 GB in
+    all), as 8 in-process ranks on one GPU.  (a) the sharded mat-vec on 256 sampled rows
+    against rows of K evaluated on the host with the sklearn RBF formula of the reference's
+    generator; (b) 16 PCG iterations against the one-rank run (same rule as the N = 65536
+    rehearsal above: the system is chaotic under summation order); (c) every rank holds the
+    same residual trace; the device memory in use with all 8 ranks resident is printed."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    n, k, lam, ell, iters = 131072, 256, 1e-6, 0.2, 16
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    v = np.random.default_rng(11).standard_normal(n)
+    mem = {}
+
+    def body(rank, world, key):
+        s = sgdml_amd.KernelSolver(n, device=0, rank=rank, world=world,
+                                   comm_id=key if world > 1 else None)
+        try:
+            s.gen_rbf(X, ell)
+            s.set_operator(1.0, lam)
+            s.precon_nystrom(idx, variant=0)
+            mode, op_bytes = s.storage_info()
+            y = s.matvec(v)
+            r0, r1 = s.row_range()
+            res = s.pcg(np.ascontiguousarray(b[r0:r1]), tol=0.0, maxiter=iters)
+            free_b, total_b = s.device_memory()
+            mem[(world, rank)] = (total_b - free_b) / 1e9
+            return mode, (r0, r1), y, res.trace, res.x, op_bytes
+        finally:
+            s.close()
+
+    ref = run_ranks(1, body, timeout=600)[0]
+    outs = run_ranks(8, body, timeout=1000)
+    assert ref[0] == "sym" and all(o[0] == "sym" for o in outs)
+    assert [o[1] for o in outs] == [(r * 16384, (r + 1) * 16384) for r in range(8)]
+    print(f"device memory in use: 1 rank {mem[(1, 0)]:.1f} GB, 8 ranks resident "
+          f"{max(mem[(8, r)] for r in range(8)):.1f} GB; operator bytes per rank "
+          f"{[round(o[5] / 1e9, 2) for o in outs]} GB")
+    y = np.concatenate([o[2] for o in outs])
+    np.testing.assert_allclose(y, ref[2], rtol=1e-12, atol=1e-12 * np.abs(ref[2]).max())
+    rows = np.sort(np.random.default_rng(12).choice(n, 256, replace=False))
+    Xs = X / ell
+    Kr = np.exp(-0.5 * ((Xs[rows, None, :] - Xs[None, :, :]) ** 2).sum(-1))
+    Kr[np.arange(rows.size), rows] = 1.0
+    y_host = Kr @ v + lam * v[rows]
+    np.testing.assert_allclose(y[rows], y_host, rtol=0, atol=1e-11 * np.abs(y_host).max())
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o[3], outs[0][3])
+    np.testing.assert_allclose(outs[0][3], ref[3], rtol=1e-7)
+    x = np.concatenate([o[4] for o in outs])
+    assert np.linalg.norm(x - ref[4]) <= 1e-7 * np.linalg.norm(ref[4])
