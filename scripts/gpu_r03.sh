@@ -22,7 +22,7 @@ step() {
 }
 for s in ${STEPS:-suite smoke bench}; do
   case $s in
-    suite) step suite 1100 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread ;;
+    suite) step suite 1100 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread ${PYTEST_EXTRA:-} ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_default 600 python bench.py ;;
     nt) step bench_nanotube 300 python bench.py --workload nanotube ;;
