@@ -560,7 +560,10 @@ struct RecArgs {
 // Zt table (kZStored: several point groups, where k_mf_z's one pass over Rdd beats a
 // recomputation per group)
 enum { kZGather = 0, kZIdent = 1, kZStored = 2 };
-template <int ZM>
+// CAP: with one identity permutation the query points' Rdd rows are captured from the Zt
+// batches into registers for the epilogue (CAP = false: re-read per epilogue round, fewer
+// registers live across the loop)
+template <int ZM, bool CAP = true>
 __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
                                                int64_t nbp, int64_t ngrp, int64_t nsw8,
                                                const int *__restrict__ status) {
@@ -623,10 +626,11 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   // one identity permutation, point groups aligned to the batches: the query points are
   // training points j = i0 + g0 + k, so their Rdd rows pass through the batches and are
   // kept for the epilogue instead of being read a second time
-  double rg[kRG][3];
+  constexpr int kCap = CAP ? kRG : 1;
+  double rg[kCap][3];
 #pragma unroll
-  for (int k = 0; k < kRG; ++k) rg[k][0] = rg[k][1] = rg[k][2] = 0.0;
-  const bool capture = ZM == kZIdent && a.i0 % kRJ == 0;
+  for (int k = 0; k < kCap; ++k) rg[k][0] = rg[k][1] = rg[k][2] = 0.0;
+  const bool capture = CAP && ZM == kZIdent && a.i0 % kRJ == 0;
   static_assert(8 * 3 * kRB * (kRB + 1) >= kWC * 2 * kRB * 3, "x stage fits in red");
   int64_t jn = 0;  // general permutations: (j, p) of the next batch slot
   int pn = 0;
@@ -682,16 +686,16 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
           rv[u][2] = r[2];
         }
         asm volatile("" ::: "memory");  // the batch's loads are issued together
-        if (capture) {
+        if (CAP && capture) {
           const int64_t off = c0 + jb - (a.i0 + g0);
 #pragma unroll
           for (int h = 0; h < kRG / kRJ; ++h)
             if (off == h * kRJ) {
 #pragma unroll
               for (int u = 0; u < kRJ; ++u) {
-                rg[h * kRJ + u][0] = rv[u][0];
-                rg[h * kRJ + u][1] = rv[u][1];
-                rg[h * kRJ + u][2] = rv[u][2];
+                rg[(h * kRJ + u) % kCap][0] = rv[u][0];
+                rg[(h * kRJ + u) % kCap][1] = rv[u][1];
+                rg[(h * kRJ + u) % kCap][2] = rv[u][2];
               }
             }
         }
@@ -730,25 +734,43 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   // J_i^T G over the block: pair d = (s = aa, t = bb), J[d, t] = +Rdd, J[d, s] = -Rdd;
   // the query points' Rdd rows are loaded together (one round trip), mostly L2 hits
   const int64_t pstride = a.ni * n3;
+  if (CAP && !capture) {
 #pragma unroll
-  for (int k = 0; k < kRG; ++k) {
-    if (!capture && k < ng && valid) {
-      const double *r = a.Rdd + ((a.i0 + g0 + k) * a.D + d) * 3;
-      rg[k][0] = r[0];
-      rg[k][1] = r[1];
-      rg[k][2] = r[2];
+    for (int k = 0; k < kCap; ++k) {
+      if (k < ng && valid) {
+        const double *r = a.Rdd + ((a.i0 + g0 + k) * a.D + d) * 3;
+        rg[k][0] = r[0];
+        rg[k][1] = r[1];
+        rg[k][2] = r[2];
+      }
     }
   }
 #pragma unroll
   for (int k0 = 0; k0 < kRG; k0 += 8) {
     if (k0 >= ng) break;
+    double rr[8][3];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = k0 + kk;
+      if (CAP) {
+        rr[kk][0] = rg[k % kCap][0];
+        rr[kk][1] = rg[k % kCap][1];
+        rr[kk][2] = rg[k % kCap][2];
+      } else {
+        const bool ok = k < ng && valid;
+        const double *r = a.Rdd + ((a.i0 + g0 + (ok ? k : 0)) * a.D + (ok ? d : 0)) * 3;
+        rr[kk][0] = ok ? r[0] : 0.0;
+        rr[kk][1] = ok ? r[1] : 0.0;
+        rr[kk][2] = ok ? r[2] : 0.0;
+      }
+    }
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const int k = k0 + kk;
-      red[kk][0][la][lb] = rg[k][0] * acc[k];
-      red[kk][1][la][lb] = rg[k][1] * acc[k];
-      red[kk][2][la][lb] = rg[k][2] * acc[k];
+      red[kk][0][la][lb] = rr[kk][0] * acc[k];
+      red[kk][1][la][lb] = rr[kk][1] * acc[k];
+      red[kk][2][la][lb] = rr[kk][2] * acc[k];
     }
     __syncthreads();
     // 8 points x (rows of A | columns of B) x 16 atoms x 3 components
@@ -1008,7 +1030,14 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                          mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
       hipLaunchKernelGGL(k_rec_g<kZStored>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     } else if (mf.ident) {
-      hipLaunchKernelGGL(k_rec_g<kZIdent>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+      static const bool nocap = [] {
+        const char *e = std::getenv("MLFF_REC_NOCAP");  // A/B of the epilogue's Rdd rows
+        return e != nullptr && std::atoi(e) != 0;
+      }();
+      if (nocap)
+        hipLaunchKernelGGL((k_rec_g<kZIdent, false>), grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+      else
+        hipLaunchKernelGGL(k_rec_g<kZIdent>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     } else {
       hipLaunchKernelGGL(k_rec_g<kZGather>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     }

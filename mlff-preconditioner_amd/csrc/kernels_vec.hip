@@ -5,6 +5,8 @@
 // Reference semantics: scipy 1.7.3 CGREVCOM + python wrapper as called from
 // src/sGDML/sgdml/solvers/iterative_solver.py:995-1005; preconditioner applies
 // iterative_cholesky.py:145-148, iterative_solver.py:315-318 and :376-379.
+#include <cstring>
+
 #include "common.h"
 
 #include <algorithm>
@@ -882,10 +884,15 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
   const int rpc = (int)((k + Q - 1) / Q);
   // hand-off slack D = 2 steps, load distance L = 1 (D = 1, L = 2: apply 3.95 -> 4.22 ms at
   // N = 156510; the hand-off, not the load latency, sets the pace)
-  // MLFF_LC_TEST_MUTE=<b>: workgroup b never publishes, so its cluster's hand-offs time out
-  // (tests of the ~1 s fault bail-out; never set in production)
-  const char *mute_env = std::getenv("MLFF_LC_TEST_MUTE");
-  const int mute = mute_env ? std::atoi(mute_env) : -1;
+  // MLFF_LC_TEST_MUTE=<b>[@<e>]: workgroup b never publishes (from the launch with epoch e
+  // on, default every launch), so its cluster's hand-offs time out (tests of the ~1 s fault
+  // bail-out, also in the middle of a chunk of PCG iterations; never set in production)
+  int mute = -1;
+  if (const char *mute_env = std::getenv("MLFF_LC_TEST_MUTE")) {
+    const char *at = std::strchr(mute_env, '@');
+    const unsigned from = at ? (unsigned)std::atoi(at + 1) : 0u;
+    if (epoch >= from) mute = std::atoi(mute_env);
+  }
   hipLaunchKernelGGL((k_lr_cluster<kLcD, kLcL>), dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), 0, s,
                      T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, mute, status, fold);
   if (n > 0)

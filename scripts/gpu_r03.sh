@@ -31,6 +31,19 @@ for s in ${STEPS:-suite smoke bench}; do
         step lrab_default_$r 200 python bench.py --no-cpu --no-solve --configs3-n 0
         step lrab_twopass_$r 200 env MLFF_LR_ROWS=0 python bench.py --no-cpu --no-solve --configs3-n 0
       done ;;
+    opexp)  # matrix-free operator with the rank-2701 panel streamed between applications vs a
+            # rank-16 panel (tables stay cached): is the operator bound by cache residency?
+      for r in 1 2; do
+        step opexp_k2701_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step opexp_k16_$r 300 python bench.py --workload nanotube --no-cpu --no-solve --k 16
+      done
+      step opexp_prof 300 rocprofv3 --kernel-trace --stats -d $O/opexp_prof -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --no-solve ;;
+    nocap)  # k_rec_g epilogue rows re-read (MLFF_REC_NOCAP=1) vs captured, interleaved
+      for r in 1 2; do
+        step nocap_default_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step nocap_on_$r 300 env MLFF_REC_NOCAP=1 python bench.py --workload nanotube --no-cpu --no-solve
+      done ;;
+    tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
   esac

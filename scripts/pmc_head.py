@@ -50,7 +50,7 @@ GROUPS = {
 
 def kname(full: str) -> str:
     """'void mlff::k_lr_rows<16>(double const*, ...)' -> 'k_lr_rows<16>'."""
-    s = full.split("(")[0].replace("void ", "").strip()
+    s = full.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
     return s.split("::")[-1]
 
 

@@ -17,7 +17,11 @@ extended-precision products), so the variants are of the matrix-free operator:
   ld        dense K with extended-precision (np.longdouble) products, rounded once
             (N <= 621: near-exact arithmetic)
 
-and the spread against the reference's recorded solve is written to noise_band.json:
+and the spread against the reference's recorded solve is written to noise_band.json
+(plus two cases without a recorded trace: the reference's trained model
+sgdml_model_ethanol_n621 -- iterations and alphas only -- and the multi-rank tests' RBF
+system rbf_n1003/{none,pivchol,nystrom}, whose reference is the oracle's own BLAS-order
+solve, since those tests compare W GPU ranks with one):
 iteration-count differences and the iteration at which the running-minimum residual first
 crosses every half decade.  tests/parity.py holds the GPU to this band (scaled, see there).
 
@@ -209,6 +213,105 @@ def run_case(name, precon, orders):
     return out
 
 
+def run_model_case(orders):
+    """sgdml_model_ethanol_n621: the reference's GDMLTrain.train model (harmonic labels, so the
+    coefficients have prediction-neutral freedom; tol 1e-4, cholesky at the rule-of-thumb
+    rank).  The model keeps no residual curve: the band is on the iteration count and on
+    alphas_F only."""
+    f = np.load(GOLDEN / "sgdml_model_ethanol_n621.npz", allow_pickle=False)
+    Rd, Rdd = descriptors(f["R"])
+    perms = np.atleast_2d(f["perms"])
+    y = f["F"].ravel().copy()
+    y /= np.std(y)
+    n, lam, sig = y.size, 1e-10, float(f["model__sig"])
+    mv0 = kop_variant(Rd, Rdd, perms, sig, "mf")
+    cols = {}
+
+    def col(i):  # columns of -K_op (the reference's get_col, iterative_cholesky.py:152-156)
+        if i not in cols:
+            e = np.zeros(n)
+            e[i] = 1.0
+            cols[i] = -mv0(e) + lam * e
+        return cols[i]
+
+    diag = np.array([-mv0(np.eye(1, n, i)[0])[i] for i in range(n)])
+    k = int(int(f["k_rot"]) / n * n)
+    L, piv = pivoted_cholesky(col, diag, k)
+    T, sp = woodbury_panel(L, lam)
+    a_ref = f["model__alphas_F"]
+    ref_it = int(f["model__solver_iters"])
+    panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7", "mf_pair": "blk512"}
+    out = {"n": n, "ref_iters": ref_it, "variants": {},
+           "pivots_equal_reference": bool(np.array_equal(piv, f["model__index_columns"]))}
+    for order in orders:
+        mvK = kop_variant(Rd, Rdd, perms, sig, order)
+        mvT = make_gemv(T, panel_order[order])
+        mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order[order])
+        x, info, tr, it = cg_legacy(lambda v: -mvK(v) + lam * v, y, tol=1e-4, maxiter=5 * n,
+                                    psolve=lambda r: sp * ((r - mvTt(mvT(r))) / lam))
+        out["variants"][order] = {"iters": int(it), "info": int(info), "d_iters": int(it - ref_it),
+                                  "rel_dalpha": float(np.linalg.norm(-x - a_ref) / np.linalg.norm(a_ref))}
+    v = out["variants"].values()
+    out["band_iters"] = int(max(abs(e["d_iters"]) for e in v))
+    out["band_crossing"] = None
+    out["band_rel_dalpha"] = float(max(e["rel_dalpha"] for e in v))
+    return out
+
+
+def run_rbf_small_cases():
+    """The multi-rank tests' RBF system (tests/test_gpu_multirank.py: N = 1003, x ~ U[0,1)^3
+    default_rng(3), l = 0.2, lam = 0.1, tol 1e-8, rank-150 pivoted Cholesky / Nystrom on
+    default_rng(5) columns / none): the oracle in the dense mat-vec's summation orders,
+    against its own BLAS-order solve (the multi-rank tests compare W ranks with one rank)."""
+    sys.path.insert(0, str(REPO / "mlff-preconditioner_amd"))
+    from oracle.rbf import rbf_kernel
+    from sgdml_amd import synthetic
+
+    n, lam, k = 1003, 1e-1, 150
+    X, b = synthetic.rbf_points(n, 3, 3)
+    K = rbf_kernel(X, 0.2)
+    idx = np.sort(np.random.default_rng(5).choice(n, k, replace=False))
+    res = {}
+    for precon in ("none", "pivchol", "nystrom"):
+        if precon == "pivchol":
+            L, _ = pivoted_cholesky(lambda i: K[:, i], np.diag(K).copy(), k)
+            T, sp = woodbury_panel(L, lam)
+        elif precon == "nystrom":
+            T, sp = nystrom_panel(K[:, idx], idx, lam, 0)
+        else:
+            T, sp = None, 1.0  # no preconditioner
+        runs = {}
+        for order in ("blas", "rev", "blk7", "blk512", "pair"):
+            mvK = make_gemv(K, order)
+            if precon == "none":
+                ps = None
+            else:
+                mvT = make_gemv(T, order)
+                mvTt = make_gemv(np.ascontiguousarray(T.T), order)
+                ps = (lambda mvT, mvTt: (lambda r: sp * ((r - mvTt(mvT(r))) / lam)))(mvT, mvTt)
+            runs[order] = cg_legacy(lambda v: mvK(v) + lam * v, b, tol=1e-8, maxiter=5 * n,
+                                    psolve=ps)
+        x0, _, tr0, it0 = runs["blas"]
+        top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+        cr0 = half_decade_crossings(tr0[1:], top)
+        var = {}
+        for order, (x, info, tr, it) in runs.items():
+            cr = half_decade_crossings(tr[1:], top)
+            dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+            var[order] = {"iters": int(it), "info": int(info), "d_iters": int(it - it0),
+                          "max_d_crossing": int(max(dc) if dc else 0),
+                          "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+        v = var.values()
+        res[f"rbf_n1003/{precon}"] = {
+            "n": n, "ref_iters": int(it0), "variants": var,
+            "band_iters": int(max(abs(e["d_iters"]) for e in v)),
+            "band_crossing": int(max(e["max_d_crossing"] for e in v)),
+            "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v))}
+        print(f"rbf_n1003 {precon:8s} ref {it0}  band it {res[f'rbf_n1003/{precon}']['band_iters']}",
+              flush=True)
+    return res
+
+
 def main():
     res = {}
     for name, precon in CASES:
@@ -221,6 +324,14 @@ def main():
               + " ".join(f"{o}:{e['d_iters']:+d}" for o, e in r["variants"].items())
               + f"  band it {r['band_iters']} cross {r['band_crossing']}  ({time.time() - t0:.1f} s)",
               flush=True)
+    t0 = time.time()
+    r = run_model_case(["mf", "mf_rev", "mf_split", "mf_pair"])
+    res["sgdml_model_ethanol_n621/cholesky"] = r
+    print(f"{'sgdml_model_ethanol_n621':28s} {'cholesky':26s} ref {r['ref_iters']:5d}  "
+          + " ".join(f"{o}:{e['d_iters']:+d}" for o, e in r["variants"].items())
+          + f"  band it {r['band_iters']} dalpha {r['band_rel_dalpha']:.1e}  ({time.time() - t0:.1f} s)",
+          flush=True)
+    res.update(run_rbf_small_cases())
     (GOLDEN / "noise_band.json").write_text(json.dumps(res, indent=1, sort_keys=True))
 
 

@@ -48,14 +48,17 @@ def envelope(trace):
 
 
 def assert_pcg_parity(iters, trace, x, ref_iters, ref_trace, ref_x, mode="chaotic",
-                      head=8, x_tol=1e-6, iter_frac=0.10, case=None):
+                      head=8, x_tol=1e-6, iter_frac=0.10, case=None, band=None):
     """trace / ref_trace: stop-test residuals of iterations 1..m (no r0 entry).
-    case: "fixture/preconditioner" of a golden solve -> its measured noise band."""
+    case: "fixture/preconditioner" of a golden solve -> its measured noise band (whose
+    reference solve is ref_iters); band: a measured band applied to another pair of
+    samples of the same system (e.g. W GPU ranks against one GPU rank)."""
     trace = np.asarray(trace)
     ref_trace = np.asarray(ref_trace)
-    if case is not None:
-        b = noise_band(case)
-        assert b["ref_iters"] == ref_iters, (case, b["ref_iters"], ref_iters)
+    if case is not None or band is not None:
+        b = band if band is not None else noise_band(case)
+        if band is None:
+            assert b["ref_iters"] == ref_iters, (case, b["ref_iters"], ref_iters)
         assert abs(iters - ref_iters) <= 2 * b["band_iters"] + 2, (case, iters, ref_iters, b["band_iters"])
         h = min(head, len(trace), len(ref_trace))
         d = np.abs(np.log10(trace[:h] / ref_trace[:h]))

@@ -18,6 +18,8 @@ configs[4]  nanotube N = 15540, rank-1024 pivoted Cholesky on 8 ranks (in-proces
 import numpy as np
 import pytest
 
+from tests.parity import assert_pcg_parity, noise_band
+
 from tests.test_gpu_golden import load, run_dropin
 from tests.test_gpu_multirank import run_ranks
 
@@ -172,7 +174,16 @@ def test_nanotube_cluster_apply_solve(sg, monkeypatch):
             out[mode] = s.pcg(y, tol=1e-6, maxiter=5 * n)
     r0, r1 = out["0"], out["default"]
     assert r0.info == 0 and r1.info == 0
-    assert abs(r1.iters - r0.iters) <= max(3, 0.05 * r0.iters), (r1.iters, r0.iters)
+    # two summation orders of the same solve: the measured band of the reference's nanotube
+    # cholesky solve (noise_band.json, N = 3330: b_it = 1 of 322 iterations), scaled by the
+    # iteration count, under the tests/parity.py rule
+    b = noise_band("sgdml_nanotube_n3330/cholesky")
+    scale = r0.iters / b["ref_iters"]
+    band = {"band_iters": int(np.ceil(b["band_iters"] * scale)),
+            "band_crossing": int(np.ceil(b["band_crossing"] * scale)),
+            "band_rel_dalpha": b["band_rel_dalpha"]}
+    print(f"cluster vs two-pass apply: {r1.iters} vs {r0.iters} iterations (band {band})")
+    assert_pcg_parity(r1.iters, r1.trace[1:], r1.x, r0.iters, r0.trace[1:], r0.x, band=band)
     Ax = -kernel_matvec_matrix_free(Rd, Rdd, perms, SIG, r1.x) + LAM * r1.x
     relres = np.linalg.norm(y - Ax) / np.linalg.norm(y)
     assert relres <= 1.05e-6, relres

@@ -383,3 +383,39 @@ def test_cluster_apply_fault_falls_back(sg, monkeypatch):
     assert ref.info == 0 and res.info == 0
     assert_pcg_parity(res.iters, res.trace[1:], res.x, ref.iters, ref.trace[1:], ref.x,
                       mode="chaotic", x_tol=1e-6)
+
+
+def test_cluster_apply_fault_mid_chunk(sg, monkeypatch):
+    """The cluster member goes silent only from the 6th apply on (MLFF_LC_TEST_MUTE=3@6), i.e.
+    inside a chunk of PCG iterations whose stop tests are folded into the next iteration's
+    first kernel: iterations 1-5 are the fault-free cluster solve's (residuals bit for bit),
+    iteration 6 faults after its folded prologue already wrote iters / trace / rho1, the host
+    re-runs it with two passes, and the rest of the solve equals a solve that ran the two-pass
+    apply from iteration 6 on (same trace and x within the two-pass/one-pass rounding band)."""
+    n, k, lam = 40000, 301, 1.0
+    X, b = _rbf(n)
+    L = np.random.default_rng(5).standard_normal((k, n)) * 0.05
+    with sg.KernelSolver(n) as s:
+        s.gen_rbf(X, length_scale=0.2)
+        s.set_operator(1.0, lam)
+        s.precon_lowrank(L)
+        ref = s.pcg(b, tol=1e-8, maxiter=2000, chunk=16)  # cluster form throughout
+        monkeypatch.setenv("MLFF_LC_TEST_MUTE", "3@6")
+        s.precon_lowrank(L)
+        assert s.precon_apply_traffic()[0] == 2
+        res = s.pcg(b, tol=1e-8, maxiter=2000, chunk=16)
+        assert s.precon_apply_traffic()[0] == 0  # fell back and stayed on two passes
+        monkeypatch.delenv("MLFF_LC_TEST_MUTE")
+        # the same switch made by hand: 5 cluster iterations, then two passes
+        monkeypatch.setenv("MLFF_LR_ROWS", "0")
+        s.precon_lowrank(L)
+        assert s.precon_apply_traffic()[0] == 0
+        two = s.pcg(b, tol=1e-8, maxiter=2000, chunk=16)
+        monkeypatch.delenv("MLFF_LR_ROWS")
+    assert ref.info == 0 and res.info == 0 and two.info == 0
+    np.testing.assert_array_equal(res.trace[:6], ref.trace[:6])
+    assert np.all(np.isfinite(res.trace)) and res.trace.size == res.iters + 1
+    assert_pcg_parity(res.iters, res.trace[1:], res.x, ref.iters, ref.trace[1:], ref.x,
+                      mode="chaotic", x_tol=1e-6)
+    assert_pcg_parity(res.iters, res.trace[1:], res.x, two.iters, two.trace[1:], two.x,
+                      mode="chaotic", x_tol=1e-6)

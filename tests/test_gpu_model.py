@@ -3,12 +3,16 @@ against the reference's own model (tests/golden/sgdml_model_ethanol_n621: its
 GDMLTrain.train on harmonic-labelled ethanol, cholesky preconditioner, rule-of-thumb
 rank).  This system (forces that integrate exactly, lambda = 1e-10, tol 1e-4) leaves
 large, prediction-neutral freedom in the coefficients: the CPU oracle's own solve (same
-pivots, 260 vs 262 iterations) differs from the reference's by 4.2e-4 in alphas and
-1.3e-5 in the integration constant.  Criteria, at ~5-10x that noise floor: iterations
-within 10 %, ||d alpha|| / ||alpha|| <= 5e-3, constant within 1e-4 relative, identical
-keys / flags / pivots; energies for given coefficients to 1e-12 relative."""
+pivots) differs from the reference's by 4.2e-4 in alphas and 1.3e-5 in the integration
+constant; in 4 summation orders of the reference's operator (tests/golden/noise_band.json,
+"sgdml_model_ethanol_n621/cholesky") by up to 6 iterations and 5.1e-4 in alphas.
+Criteria: the tests/parity.py rule on that band (iterations within 2 b_it + 2, alphas
+within 10 b_dx), constant within 1e-4 relative, identical keys / flags / pivots; energies
+for given coefficients to 1e-12 relative."""
 import numpy as np
 import pytest
+
+from tests.parity import noise_band
 
 pytestmark = pytest.mark.gpu
 
@@ -59,12 +63,18 @@ def test_train_matches_reference_model(fx, devices, tmp_path):
     assert m["use_E"] == bool(f["model__use_E"])
     np.testing.assert_array_equal(m["index_columns"], f["model__index_columns"])
     # the model keeps no residual curve: iteration count and coefficients
+    # measured band of this solve (tests/golden/noise_band.json, make_noise_band.py
+    # run_model_case: the oracle in 4 summation orders moves the count by up to b_it = 6 of
+    # 262 and alphas by up to 5.1e-4); the tests/parity.py rule
+    band = noise_band("sgdml_model_ethanol_n621/cholesky")
     ni, ni_ref = int(m["solver_iters"]), int(f["model__solver_iters"])
-    assert abs(ni - ni_ref) <= max(3, 0.1 * ni_ref), (ni, ni_ref)
+    assert band["ref_iters"] == ni_ref
+    assert abs(ni - ni_ref) <= 2 * band["band_iters"] + 2, (ni, ni_ref, band["band_iters"])
     a, a_ref = m["alphas_F"], f["model__alphas_F"]
-    assert np.linalg.norm(a - a_ref) <= 5e-3 * np.linalg.norm(a_ref)
+    dx = 10 * band["band_rel_dalpha"]
+    assert np.linalg.norm(a - a_ref) <= dx * np.linalg.norm(a_ref)
     np.testing.assert_allclose(m["R_d_desc_alpha"], f["model__R_d_desc_alpha"], rtol=0,
-                               atol=5e-3 * np.abs(f["model__R_d_desc_alpha"]).max())
+                               atol=dx * np.abs(f["model__R_d_desc_alpha"]).max())
     assert abs(m["c"] - float(f["model__c"])) <= 1e-4 * abs(float(f["model__c"]))
     assert m["std"] == float(f["model__std"])
     np.testing.assert_array_equal(m["tril_perms_lin"], f["model__tril_perms_lin"])

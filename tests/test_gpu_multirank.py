@@ -13,7 +13,7 @@ import threading
 import numpy as np
 import pytest
 
-from tests.parity import assert_pcg_parity
+from tests.parity import assert_pcg_parity, noise_band
 
 pytestmark = pytest.mark.gpu
 
@@ -111,8 +111,11 @@ def test_sharded_solve_matches_single_rank(world, precon, storage):
                                atol=1e-9 * np.abs(ref["z"]).max())
     np.testing.assert_allclose(outs[0]["lev"], ref["lev"], rtol=1e-8, atol=1e-12)
     assert outs[0]["info"] == ref["info"] == 0
+    # W ranks vs one rank: two samples of the summation-order distribution whose spread the
+    # oracle measured on this very system (noise_band.json "rbf_n1003/<precon>")
+    band = noise_band(f"rbf_n1003/{'none' if precon == 'none' else precon}")
     assert_pcg_parity(outs[0]["iters"], outs[0]["trace"][1:], gather(outs, "x"), ref["iters"],
-                      ref["trace"][1:], ref["x"], mode="chaotic", x_tol=1e-7)
+                      ref["trace"][1:], ref["x"], band=band)
 
 
 @pytest.mark.timeout(300)
@@ -128,7 +131,7 @@ def test_sharded_sym_row_slices(lsub, monkeypatch):
     np.testing.assert_allclose(gather(outs, "y"), ref["y"], rtol=1e-13, atol=1e-13)
     assert outs[0]["info"] == ref["info"] == 0
     assert_pcg_parity(outs[0]["iters"], outs[0]["trace"][1:], gather(outs, "x"), ref["iters"],
-                      ref["trace"][1:], ref["x"], mode="chaotic", x_tol=1e-7)
+                      ref["trace"][1:], ref["x"], band=noise_band("rbf_n1003/nystrom"))
 
 
 @pytest.mark.timeout(300)
@@ -225,8 +228,8 @@ def test_sharded_x0_matches_single_rank():
     # ||b - A x0|| over the sharded operator (the warm-start residual itself)
     np.testing.assert_allclose(outs[0][2][0], ref[2][0], rtol=1e-12)
     x = np.concatenate([o[0] for o in outs])
-    assert_pcg_parity(outs[0][1], outs[0][2][1:], x, ref[1], ref[2][1:], ref[0], mode="chaotic",
-                      x_tol=1e-7)
+    assert_pcg_parity(outs[0][1], outs[0][2][1:], x, ref[1], ref[2][1:], ref[0],
+                      band=noise_band("rbf_n1003/pivchol"))
 
 
 @pytest.mark.parametrize("n", [1, 2, 63, 513, 1100, 2049])
