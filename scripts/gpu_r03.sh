@@ -43,6 +43,12 @@ for s in ${STEPS:-suite smoke bench}; do
         step nocap_default_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
         step nocap_on_$r 300 env MLFF_REC_NOCAP=1 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
+    rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
+      for W in 2 8; do
+        step rehearse_w$W 400 env MLFF_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node $W --master-addr 127.0.0.1 --master-port $((29500 + W)) \
+          bench.py --gpus $W --steps 10 --warmup 2 --no-solve
+      done ;;
     tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
