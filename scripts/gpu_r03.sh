@@ -43,6 +43,17 @@ for s in ${STEPS:-suite smoke bench}; do
         step nocap_default_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
         step nocap_on_$r 300 env MLFF_REC_NOCAP=1 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
+    oneab)  # k_rec_g one-batch form (default) vs two batches (MLFF_REC_ONE=0), interleaved
+      for r in 1 2 3; do
+        step oneab_on_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step oneab_off_$r 300 env MLFF_REC_ONE=0 python bench.py --workload nanotube --no-cpu --no-solve
+      done ;;
+    rgab)  # k_rec_g point-group size 16 / 8 / 4 (MLFF_REC_RG), interleaved
+      for r in 1 2 3; do
+        for g in 16 8 4; do
+          step rgab_${g}_$r 300 env MLFF_REC_RG=$g python bench.py --workload nanotube --no-cpu --no-solve
+        done
+      done ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
       for W in 2 8; do
         step rehearse_w$W 400 env MLFF_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
