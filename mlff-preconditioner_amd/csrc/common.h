@@ -100,9 +100,8 @@ struct MfData {
   // 5 m (v . x_j) (ni x M n_perms), rpart = J^T G partial rows of every pair block
   // (rblk slots x ni x 3n)
   bool rec = false;
-  bool rec_one = true;    // k_rec_g one-batch form where it applies (MLFF_REC_ONE=0: off)
-  bool rec_nocap = false; // k_rec_g epilogue rows re-read (MLFF_REC_NOCAP=1, A/B)
-  int rec_rg = 16;        // k_rec_g query points per workgroup, identity permutation (MLFF_REC_RG)
+  int rec_rg = 8;         // k_rec_g query points per workgroup, identity permutation (MLFF_REC_RG)
+  bool rec_wc16 = true;   // k_rec_g w / x staged as one 16-slot chunk when MP <= 16 (MLFF_REC_WC16)
   int rblk = 0;
   int64_t ldw = 0;
   double *wt = nullptr, *sv = nullptr, *rpart = nullptr;

@@ -559,21 +559,17 @@ struct RecArgs {
 // LDS-staged x of the block's atoms (kZIdent: one identity permutation), or read from the
 // Zt table (kZStored: several point groups, where k_mf_z's one pass over Rdd beats a
 // recomputation per group)
-// kZOne: kZIdent with every (j, p) of the system in ONE batch of kRJ1 slots (MP <= 16, one
-// point group on rank 0): the batch's Rdd loads are issued with the staging loads, before
-// the first barrier, and the query points' rows are those same registers (j = query point)
-enum { kZGather = 0, kZIdent = 1, kZStored = 2, kZOne = 3 };
-constexpr int kRJ1 = 16;
+enum { kZGather = 0, kZIdent = 1, kZStored = 2 };
 // CAP: with one identity permutation the query points' Rdd rows are captured from the Zt
 // batches into registers for the epilogue (CAP = false: re-read per epilogue round, fewer
 // registers live across the loop)
-template <int ZM, bool CAP = true, int RG = kRG, int RR = 8>
+template <int ZM, bool CAP = true, int RG = kRG, int RR = 8, int WC = kWC>
 __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
                                                int64_t nbp, int64_t ngrp, int64_t nsw8,
                                                const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double red[RR][3][kRB][kRB + 1];
-  __shared__ double sW[kWC][RG];
+  __shared__ double sW[WC][RG];
   const int tid = threadIdx.x;
   const int n3 = 3 * a.n;
   if ((int64_t)blockIdx.x < nsw8) {  // pair scalars: one wave per (local point, j, p)
@@ -626,7 +622,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   const double *rj = a.Rdd + d * 3;
   // identity: x of the chunk's points at the block's 2 x 16 atoms, staged in LDS (in the
   // space of the epilogue's reduction buffer), so a batch loads only its Rdd rows
-  double *sx = &red[0][0][0][0];  // [kWC][2][kRB][3]
+  double *sx = &red[0][0][0][0];  // [WC][2][kRB][3]
   // one identity permutation, point groups aligned to the batches: the query points are
   // training points j = i0 + g0 + k, so their Rdd rows pass through the batches and are
   // kept for the epilogue instead of being read a second time
@@ -636,27 +632,15 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   for (int k = 0; k < kCap; ++k) rg[k][0] = rg[k][1] = rg[k][2] = 0.0;
   const bool capture = CAP && ZM == kZIdent && a.i0 % kRJ == 0;
   static_assert(RG % RR == 0 && RG <= 16, "point groups are whole epilogue rounds");
-  constexpr bool ONE = ZM == kZOne;
-  constexpr bool IDENT = ZM == kZIdent || ZM == kZOne;
-  double r1[ONE ? kRJ1 : 1][3];
-  if (ONE) {  // all of the system's Zt rows for this lane's pair, in flight with the staging
-#pragma unroll
-    for (int u = 0; u < (ONE ? kRJ1 : 1); ++u) {
-      const int64_t jc = u < a.MP ? u : a.MP - 1;
-      const double *r = rj + jc * rs;
-      r1[u][0] = r[0];
-      r1[u][1] = r[1];
-      r1[u][2] = r[2];
-    }
-  }
-  static_assert(RR * 3 * kRB * (kRB + 1) >= kWC * 2 * kRB * 3, "x stage fits in red");
+  constexpr bool IDENT = ZM == kZIdent;
+  static_assert(RR * 3 * kRB * (kRB + 1) >= WC * 2 * kRB * 3, "x stage fits in red");
   int64_t jn = 0;  // general permutations: (j, p) of the next batch slot
   int pn = 0;
-  for (int64_t c0 = 0; c0 < MPp; c0 += kWC) {
+  for (int64_t c0 = 0; c0 < MPp; c0 += WC) {
     // w of the chunk's (j, p) for the group's points, LDS broadcast operands
-    const int cn = (int)((MPp - c0) < kWC ? (MPp - c0) : kWC);
+    const int cn = (int)((MPp - c0) < WC ? (MPp - c0) : WC);
     // (every thread's staging loads issued together, then stored)
-    constexpr int kWL = (kWC * RG + 255) / 256, kXL = kWC * 2 * kRB * 3 / 256;
+    constexpr int kWL = (WC * RG + 255) / 256, kXL = WC * 2 * kRB * 3 / 256;
     double wl[kWL], xl[IDENT ? kXL : 1];
 #pragma unroll
     for (int q = 0; q < kWL; ++q) {
@@ -676,26 +660,15 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kWL; ++q)
-      if (kWC * RG % 256 == 0 || tid + q * 256 < kWC * RG) (&sW[0][0])[tid + q * 256] = wl[q];
+      if (WC * RG % 256 == 0 || tid + q * 256 < WC * RG) (&sW[0][0])[tid + q * 256] = wl[q];
     if (IDENT) {
 #pragma unroll
       for (int q = 0; q < kXL; ++q) sx[tid + q * 256] = xl[q];
     }
     __syncthreads();
-#pragma unroll
-    for (int jb = 0; jb < (ONE ? kRJ1 : cn); jb += kRJ) {
+    for (int jb = 0; jb < cn; jb += kRJ) {
       double z[kRJ];
-      if (ONE) {  // the batch loaded before the staging barrier (same sums as kZIdent)
-#pragma unroll
-        for (int u = 0; u < kRJ; ++u) {
-          const double *xs = sx + (jb + u) * (2 * kRB * 3);
-          double zz = 0.0;
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            zz = fma(r1[(jb + u) % kRJ1][c], xs[kRB * 3 + lb * 3 + c] - xs[la * 3 + c], zz);
-          z[u] = (valid && c0 + jb + u < a.MP) ? zz : 0.0;
-        }
-      } else if (ZM == kZStored) {
+      if (ZM == kZStored) {
         double zv[kRJ];
 #pragma unroll
         for (int u = 0; u < kRJ; ++u) {
@@ -764,7 +737,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   // J_i^T G over the block: pair d = (s = aa, t = bb), J[d, t] = +Rdd, J[d, s] = -Rdd;
   // the query points' Rdd rows are loaded together (one round trip), mostly L2 hits
   const int64_t pstride = a.ni * n3;
-  if (CAP && !capture && !ONE) {
+  if (CAP && !capture) {
 #pragma unroll
     for (int k = 0; k < kCap; ++k) {
       if (k < ng && valid) {
@@ -782,12 +755,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
 #pragma unroll
     for (int kk = 0; kk < RR; ++kk) {
       const int k = k0 + kk;
-      if (ONE) {  // query point k of the group is training point j = g0 + k (rank 0)
-        const bool hi = RG == 8 && g0 != 0;
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          rr[kk][c] = hi ? r1[(8 + k) % kRJ1][c] : r1[k % kRJ1][c];
-      } else if (CAP) {
+      if (CAP) {
         rr[kk][0] = rg[k % kCap][0];
         rr[kk][1] = rg[k % kCap][1];
         rr[kk][2] = rg[k % kCap][2];
@@ -1014,11 +982,10 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
       hipLaunchKernelGGL(k_rec_wt, dim3((unsigned)((mf.ni * MP + 255) / 256)), dim3(256), 0, s,
                          mf.uvk, mf.ni, MP, n, mf.ldw, mf.wt);
       mf.rec = true;
-      const char *e1 = std::getenv("MLFF_REC_ONE"), *e2 = std::getenv("MLFF_REC_NOCAP");  // A/B
-      mf.rec_one = e1 == nullptr || std::atoi(e1) != 0;
-      mf.rec_nocap = e2 != nullptr && std::atoi(e2) != 0;
       const char *e3 = std::getenv("MLFF_REC_RG");
-      mf.rec_rg = e3 != nullptr ? std::atoi(e3) : 16;
+      mf.rec_rg = e3 != nullptr ? std::atoi(e3) : 8;
+      const char *e4 = std::getenv("MLFF_REC_WC16");
+      mf.rec_wc16 = e4 == nullptr || std::atoi(e4) != 0;
     }
   }
   if (mf.ni > 0) {
@@ -1070,25 +1037,24 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                          mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
       hipLaunchKernelGGL(k_rec_g<kZStored>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     } else if (mf.ident) {
-      const bool one = mf.rec_one && ngrp == 1 && mf.i0 == 0 && round_up(MP, kRJ) <= kRJ1;
       if (mf.rec_rg == 8 || mf.rec_rg == 4) {
         // smaller point groups per pair block: more waves (the kernel is latency-bound, with
         // ~1.4 workgroups per CU at 16 points), 4-point epilogue rounds (a third of the LDS),
         // the query points' rows re-read from L2 (registers for 3-4 waves per SIMD)
         const int64_t ng = (mf.ni + mf.rec_rg - 1) / mf.rec_rg;
         const dim3 gridg((unsigned)(nsw8 + nbp8 * ng));
-        if (mf.rec_rg == 8)
+        if (mf.rec_rg == 8 && round_up(MP, kRJ) <= 16 && mf.rec_wc16)  // one 16-slot chunk
+          hipLaunchKernelGGL((k_rec_g<kZIdent, false, 8, 4, 16>), gridg, dim3(256), 0, s, ra, wt, nbp,
+                             ng, nsw8, status);
+        else if (mf.rec_rg == 8)
           hipLaunchKernelGGL((k_rec_g<kZIdent, false, 8, 4>), gridg, dim3(256), 0, s, ra, wt, nbp,
                              ng, nsw8, status);
         else
           hipLaunchKernelGGL((k_rec_g<kZIdent, false, 4, 4>), gridg, dim3(256), 0, s, ra, wt, nbp,
                              ng, nsw8, status);
-      } else if (one)
-        hipLaunchKernelGGL(k_rec_g<kZOne>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
-      else if (mf.rec_nocap)
-        hipLaunchKernelGGL((k_rec_g<kZIdent, false>), grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
-      else
+      } else {  // 16-point groups, rows captured from the Zt batches (MLFF_REC_RG=16)
         hipLaunchKernelGGL(k_rec_g<kZIdent>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
+      }
     } else {
       hipLaunchKernelGGL(k_rec_g<kZGather>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     }

@@ -48,11 +48,12 @@ for s in ${STEPS:-suite smoke bench}; do
         step oneab_on_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
         step oneab_off_$r 300 env MLFF_REC_ONE=0 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
-    rgab)  # k_rec_g point-group size 16 / 8 / 4 (MLFF_REC_RG), interleaved
+    rgab)  # k_rec_g variants, interleaved: default (8-point groups, 16-slot stage) / 32-slot stage /
+           # 16-point groups (the round-2 form)
       for r in 1 2 3; do
-        for g in 16 8 4; do
-          step rgab_${g}_$r 300 env MLFF_REC_RG=$g python bench.py --workload nanotube --no-cpu --no-solve
-        done
+        step rgab_def_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step rgab_wc32_$r 300 env MLFF_REC_WC16=0 python bench.py --workload nanotube --no-cpu --no-solve
+        step rgab_rg16_$r 300 env MLFF_REC_RG=16 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
       for W in 2 8; do

@@ -314,11 +314,12 @@ def test_record_factored_operator_matches_pair_path(sg, golden_dir, name, monkey
 
 
 @pytest.mark.parametrize("M", [3, 14, 16, 17])
-def test_one_batch_record_kernel_bitwise(sg, monkeypatch, M):
-    """k_rec_g's one-batch form (every (j, p) of a system with M <= 16 loaded before the
-    staging barrier, MLFF_REC_ONE) and its 8- / 4-point-group forms (MLFF_REC_RG) compute the same
-    sums in the same order as the two-batch 16-point form: operator outputs and a short PCG
-    are bit-identical.  M = 17 exceeds one point group: every form is the same kernel there."""
+def test_record_kernel_point_groups_bitwise(sg, monkeypatch, M):
+    """k_rec_g with 8-point groups (the default for one identity permutation), 4-point groups
+    and the round-2 16-point groups (MLFF_REC_RG), with the w / x stage as one 16-slot chunk
+    or a 32-slot one (MLFF_REC_WC16), computes the same sums in the same order: operator
+    outputs and a short PCG are bit-identical.  M = 17 exceeds one 16-point group (the Zt-table
+    path, the same kernel for every setting)."""
     from sgdml_amd import synthetic
 
     ds = synthetic.nanotube_like(M, seed=2)
@@ -328,19 +329,18 @@ def test_one_batch_record_kernel_bitwise(sg, monkeypatch, M):
     n = y.size
     v = np.random.default_rng(M).standard_normal(n)
     out = {}
-    for one in ("1", "0", "rg8", "rg4"):
-        monkeypatch.setenv("MLFF_REC_ONE", "1" if one == "1" else "0")
-        # smaller point groups per pair block (rows re-read, 4-point epilogue rounds)
-        monkeypatch.setenv("MLFF_REC_RG", {"rg8": "8", "rg4": "4"}.get(one, "16"))
+    for key, rg, wc16 in (("rg16", "16", "1"), ("rg8", "8", "1"), ("rg4", "4", "1"),
+                          ("rg8wc32", "8", "0")):
+        monkeypatch.setenv("MLFF_REC_RG", rg)
+        monkeypatch.setenv("MLFF_REC_WC16", wc16)
         with sg.KernelSolver(n) as s:
             s.sgdml_operator(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
             s.set_operator(-1.0, 1e-10)
             s.precon_pivchol(max(8, n // 20))
             r = s.pcg(y, tol=0.0, maxiter=12)
-            out[one] = (s.matvec(v), r.trace, r.x)
-    monkeypatch.delenv("MLFF_REC_ONE")
+            out[key] = (s.matvec(v), r.trace, r.x)
     monkeypatch.delenv("MLFF_REC_RG")
-    for a, b, c, d in zip(out["1"], out["0"], out["rg8"], out["rg4"]):
-        np.testing.assert_array_equal(a, b)
-        np.testing.assert_array_equal(c, b)
-        np.testing.assert_array_equal(d, b)
+    monkeypatch.delenv("MLFF_REC_WC16")
+    for key in ("rg8", "rg4", "rg8wc32"):
+        for a, b in zip(out[key], out["rg16"]):
+            np.testing.assert_array_equal(a, b)
