@@ -59,14 +59,27 @@ def matches(full: str, want: str) -> bool:
     return k == want if "<" in want else re.sub(r"<.*", "", k) == want
 
 
+# counters are collected for the measured groups' kernels only (the builds launch ~20k other
+# kernels, each of which a --pmc pass would serialize)
+KERNEL_REGEX = "|".join(sorted({k.split("<")[0] for g in GROUPS.values() for k in g}))
+
+
 def run_pass(wl: str, counter: str, out: Path) -> dict:
+    import time
+
     d = out / f"{wl}_{counter.lower()}"
     d.mkdir(parents=True, exist_ok=True)
-    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "-d", str(d), "-o", "pmc",
+    cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter,
+           "--kernel-include-regex", KERNEL_REGEX, "-d", str(d), "-o", "pmc",
            "--output-format", "csv", "--", sys.executable, str(REPO / "bench.py"), "--steps",
            str(STEPS), "--warmup", str(WARMUP), "--no-cpu", "--no-solve", *WORKLOADS[wl]]
+    t0 = time.time()
     with open(d / "bench_stdout.txt", "w") as fo:
-        rc = subprocess.run(cmd, stdout=fo, stderr=subprocess.STDOUT, cwd=REPO).returncode
+        p = subprocess.Popen(cmd, stdout=fo, stderr=subprocess.STDOUT, cwd=REPO)
+        while p.poll() is None:  # a heartbeat: the pass itself writes its files at the end
+            time.sleep(5)
+            print(f"  {wl} {counter}: {time.time() - t0:.0f} s", flush=True)
+        rc = p.returncode
     if rc != 0:
         raise SystemExit(f"{wl} {counter}: rocprofv3 pass failed (rc {rc}), see {d}")
     lines = [json.loads(x) for x in (d / "bench_stdout.txt").read_text().splitlines()
