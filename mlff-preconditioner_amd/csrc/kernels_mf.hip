@@ -25,6 +25,8 @@
 //   k_mf_pair  c[i, jp] = 5m (diff . Zt[jp])   workgroup per (jp, 16 points)
 //   k_mf_h     F[i, d]                          thread per (d, 16 points)
 //   k_mf_jt    y rows of this rank = J_i^T F_i, epilogue sigma y + lam x
+#include <cstdio>
+
 #include "common.h"
 
 #include <algorithm>
@@ -559,6 +561,21 @@ struct RecArgs {
 // LDS-staged x of the block's atoms (kZIdent: one identity permutation), or read from the
 // Zt table (kZStored: several point groups, where k_mf_z's one pass over Rdd beats a
 // recomputation per group)
+#ifdef MLFF_REC_TRACE
+// phase timestamps of k_rec_g (a variant build, scripts/experiments/gpu_r03_rectrace.sh):
+// per workgroup [start, staged, G loop done, end] of the 100 MHz wall clock, plus the XCC /
+// CU the workgroup ran on
+__device__ unsigned long long g_rec_trace[8192][5];
+#define REC_STAMP(slot)                                                                  \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                           \
+      g_rec_trace[blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
+#else
+#define REC_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
 enum { kZGather = 0, kZIdent = 1, kZStored = 2 };
 // CAP: with one identity permutation the query points' Rdd rows are captured from the Zt
 // batches into registers for the epilogue (CAP = false: re-read per epilogue round, fewer
@@ -567,7 +584,10 @@ template <int ZM, bool CAP = true, int RG = kRG, int RR = 8, int WC = kWC>
 __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
                                                int64_t nbp, int64_t ngrp, int64_t nsw8,
                                                const int *__restrict__ status) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+  REC_STAMP(0);
+  // the status gate is read here and tested once the first loads are in flight (it only has
+  // to hold back the stores of an iteration past convergence)
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double red[RR][3][kRB][kRB + 1];
   __shared__ double sW[WC][RG];
   const int tid = threadIdx.x;
@@ -591,8 +611,10 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
       for (int u = 0; u < 8; ++u) acc = fma(va[u], xa[u], acc);
     }
     for (; t < n3; t += 64) acc = fma(vv[t], xj[t], acc);
+    if (st0 != ST_RUNNING) return;
     acc = wave_sum(acc);
     if ((tid & 63) == 0) a.sv[il * a.MP + jp] = 5.0 * vv[3 * a.n] * acc;  // 5 m (v . x_j)
+    REC_STAMP(3);
     return;
   }
   // XCD-aware order: the point groups of one pair block run on one XCD (workgroup L on
@@ -634,6 +656,22 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   static_assert(RG % RR == 0 && RG <= 16, "point groups are whole epilogue rounds");
   constexpr bool IDENT = ZM == kZIdent;
   static_assert(RR * 3 * kRB * (kRB + 1) >= WC * 2 * kRB * 3, "x stage fits in red");
+  // CAP = false: the query points' Rdd rows of the next epilogue round, prefetched (round 0
+  // during the G loop, round r + 1 during round r)
+  double rn[CAP ? 1 : RR][3];
+  auto load_rows = [&](int k0) {
+    if (!CAP) {
+#pragma unroll
+      for (int kk = 0; kk < (CAP ? 1 : RR); ++kk) {
+        const int k = k0 + kk;
+        const bool ok = k < ng && valid;
+        const double *r = a.Rdd + ((a.i0 + g0 + (ok ? k : 0)) * a.D + (ok ? d : 0)) * 3;
+        rn[kk][0] = ok ? r[0] : 0.0;
+        rn[kk][1] = ok ? r[1] : 0.0;
+        rn[kk][2] = ok ? r[2] : 0.0;
+      }
+    }
+  };
   int64_t jn = 0;  // general permutations: (j, p) of the next batch slot
   int pn = 0;
   for (int64_t c0 = 0; c0 < MPp; c0 += WC) {
@@ -657,6 +695,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
         xl[q] = (jj < cn && j < a.MP && atom < a.n) ? a.xc[j * n3 + 3 * atom + r % 3] : 0.0;
       }
     }
+    if (c0 == 0 && st0 != ST_RUNNING) return;  // uniform: before the first barrier
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kWL; ++q)
@@ -666,6 +705,8 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
       for (int q = 0; q < kXL; ++q) sx[tid + q * 256] = xl[q];
     }
     __syncthreads();
+    REC_STAMP(1);
+    if (!CAP && c0 == 0) load_rows(0);  // the epilogue's first rows arrive during the loop
     for (int jb = 0; jb < cn; jb += kRJ) {
       double z[kRJ];
       if (ZM == kZStored) {
@@ -736,6 +777,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   }
   // J_i^T G over the block: pair d = (s = aa, t = bb), J[d, t] = +Rdd, J[d, s] = -Rdd;
   // the query points' Rdd rows are loaded together (one round trip), mostly L2 hits
+  REC_STAMP(2);
   const int64_t pstride = a.ni * n3;
   if (CAP && !capture) {
 #pragma unroll
@@ -760,13 +802,12 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
         rr[kk][1] = rg[k % kCap][1];
         rr[kk][2] = rg[k % kCap][2];
       } else {
-        const bool ok = k < ng && valid;
-        const double *r = a.Rdd + ((a.i0 + g0 + (ok ? k : 0)) * a.D + (ok ? d : 0)) * 3;
-        rr[kk][0] = ok ? r[0] : 0.0;
-        rr[kk][1] = ok ? r[1] : 0.0;
-        rr[kk][2] = ok ? r[2] : 0.0;
+        rr[kk][0] = rn[kk % (CAP ? 1 : RR)][0];
+        rr[kk][1] = rn[kk % (CAP ? 1 : RR)][1];
+        rr[kk][2] = rn[kk % (CAP ? 1 : RR)][2];
       }
     }
+    if (!CAP && k0 + RR < RG && k0 + RR < ng) load_rows(k0 + RR);
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < RR; ++kk) {
@@ -809,6 +850,15 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
       if (atom < a.n) a.rpart[sl * pstride + (g0 + k0 + kk) * n3 + 3 * atom + c] = v;
     }
   }
+#ifdef MLFF_REC_TRACE
+  __syncthreads();
+  REC_STAMP(3);
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    unsigned hw = 0;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_rec_trace[blockIdx.x][4] = hw;
+  }
+#endif
 }
 
 // rows of this rank: y = sigma (sum_jp s_ijp u_ijp[t] - sum_slots J^T G) + lam x;
@@ -1023,6 +1073,9 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                          (int64_t)0, sigma, lam, x_loc, y_loc, pq_part, status);
     return;
   }
+#ifdef MLFF_REC_TRACE
+  static int rec_launches = 0;
+#endif
   if (mf.rec) {
     const RecArgs ra{mf.Rdd, mf.Zt, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni,
                      MP, mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
@@ -1058,6 +1111,25 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     } else {
       hipLaunchKernelGGL(k_rec_g<kZGather>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     }
+#ifdef MLFF_REC_TRACE
+    static const int trace_at = [] {
+      const char *e = std::getenv("MLFF_REC_TRACE_AT");
+      return e ? std::atoi(e) : 20;
+    }();
+    if (++rec_launches == trace_at) {  // after the build and warmup: one application's phases
+      static unsigned long long h[8192][5];
+      (void)hipStreamSynchronize(s);
+      (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rec_trace), sizeof(h));
+      if (const char *fn = std::getenv("MLFF_REC_TRACE_FILE")) {
+        if (FILE *f = std::fopen(fn, "w")) {
+          for (int i = 0; i < 8192; ++i)
+            if (h[i][0] != 0)
+              std::fprintf(f, "%d %llu %llu %llu %llu %llu\n", i, h[i][0], h[i][1], h[i][2], h[i][3], h[i][4]);
+          std::fclose(f);
+        }
+      }
+    }
+#endif
     // lanes per row: fill the finisher's grid (kVecGrid workgroups with the p.q partials)
     int lg = 0;
     const int64_t threads = (pq_part != nullptr ? (int64_t)kVecGrid : 1024) * 256;

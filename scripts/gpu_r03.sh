@@ -55,6 +55,10 @@ for s in ${STEPS:-suite smoke bench}; do
         step rgab_wc32_$r 300 env MLFF_REC_WC16=0 python bench.py --workload nanotube --no-cpu --no-solve
         step rgab_rg16_$r 300 env MLFF_REC_RG=16 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
+    ntab)  # nanotube bench, 3 runs (operator A/B against the numbers of the previous session)
+      for r in 1 2 3; do
+        step ntab_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+      done ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
       for W in 2 8; do
         step rehearse_w$W 400 env MLFF_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
