@@ -1453,10 +1453,8 @@ int mlff_precon_eig(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, int 
   MLFF_ENTER(ctx);
   if (mask_mode < 0 || mask_mode > 2 || (mask_mode == 2 && (dim_i < 3 || dim_i % 3 != 0)))
     return set_error(ctx, MLFF_ERR_ARG, "eig: bad mask_mode / dim_i");
-  if (mask_mode == 2) {  // the masked matrix is formed from the dense K (one rank)
+  if (mask_mode == 2) {  // the masked matrix is formed from this rank's rows of the dense K
     MLFF_TRY(require_matrix(ctx));
-    if (ctx->world != 1)
-      return set_error(ctx, MLFF_ERR_ARG, "eig atomic_interactions mask needs a single rank");
   } else {
     MLFF_TRY(require_operator(ctx));
   }

@@ -229,16 +229,29 @@ __global__ void k_absmax_part(const double *__restrict__ A, int64_t n_elem,
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
 }
 
-__global__ void k_mask_atomic(double *__restrict__ A, int64_t n, int64_t lda, int64_t dim_i,
-                              const double *__restrict__ part, int np) {
+// rows of this rank (global row = row0 + a), columns in the padded layout (position c -> global
+// column (c / blk) rows_per + c % blk; padding positions hold zeros); the global max|K| is the
+// max of the W per-rank maxima in rmax
+__global__ void k_mask_atomic(double *__restrict__ A, int64_t nrows, int64_t lda, int64_t dim_i,
+                              int64_t row0, int64_t rows_per, int64_t blk,
+                              const double *__restrict__ rmax, int world) {
   double mx = 0.0;
-  for (int t = 0; t < np; ++t) mx = fmax(mx, part[t]);
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n * n;
+  for (int t = 0; t < world; ++t) mx = fmax(mx, rmax[t]);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nrows * lda;
        e += (int64_t)gridDim.x * 256) {
-    const int64_t a = e / n, b = e % n;
+    const int64_t a = row0 + e / lda, c = e % lda;
+    const int64_t b = (c / blk) * rows_per + c % blk;
     const bool same_atom = ((a % dim_i) / 3) == ((b % dim_i) / 3);
-    double &v = A[a * lda + b];
+    double &v = A[e];
     if (!same_atom && fabs(v) < mx) v = 0.0;
+  }
+}
+
+__global__ void k_max_of(const double *__restrict__ part, int np, double *__restrict__ out) {
+  if (threadIdx.x == 0) {
+    double m = 0.0;
+    for (int t = 0; t < np; ++t) m = fmax(m, part[t]);
+    out[0] = m;
   }
 }
 
@@ -345,19 +358,28 @@ int eig_lowrank(mlff_ctx *ctx, int64_t k, int mask_mode, int64_t dim_i, double *
   // operator: S = sigma_K K in its resolved storage, or the masked dense copy (mask 2)
   double *A = nullptr;
   if (mask_mode == 2) {
-    double *part = nullptr;
+    // this rank's rows of the masked S; the mask's threshold max|K| over all ranks (the
+    // per-rank maxima all-gathered)
+    double *part = nullptr, *rmax = nullptr;
     MLFF_TRY(scratch_alloc(ctx, &A, (size_t)blk * ctx->ld));
     MLFF_TRY(scratch_alloc(ctx, &part, 1024));
+    MLFF_TRY(scratch_alloc(ctx, &rmax, (size_t)ctx->world));
     launch_scale_copy(ctx->K, A, blk * ctx->ld, ctx->sigma_K, s);
-    hipLaunchKernelGGL(k_absmax_part, dim3(1024), dim3(256), 0, s, A, n * ctx->ld, part);
-    hipLaunchKernelGGL(k_mask_atomic, dim3(4096), dim3(256), 0, s, A, n, ctx->ld, dim_i, part, 1024);
+    hipLaunchKernelGGL(k_absmax_part, dim3(1024), dim3(256), 0, s, A, nrows * ctx->ld, part);
+    hipLaunchKernelGGL(k_max_of, dim3(1), dim3(64), 0, s, part, 1024, rmax + ctx->rank);
+    MLFF_TRY(comm_allgather(ctx, rmax + ctx->rank, rmax, 1));
+    hipLaunchKernelGGL(k_mask_atomic, dim3(4096), dim3(256), 0, s, A, nrows, ctx->ld, dim_i,
+                       ctx->row0, ctx->rows_per, blk, rmax, ctx->world);
     MLFF_HIP(ctx, hipGetLastError());
   } else {
     MLFF_TRY(operator_prepare(ctx));
   }
   auto apply = [&](const double *x_loc, double *y_loc) -> int {
     if (A == nullptr) return operator_apply_local(ctx, x_loc, y_loc);
-    MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg, x_loc, sizeof(double) * blk, hipMemcpyDeviceToDevice, s));
+    MLFF_HIP(ctx, hipMemcpyAsync(ctx->xg + (int64_t)ctx->rank * blk, x_loc, sizeof(double) * blk,
+                                 hipMemcpyDeviceToDevice, s));
+    if (ctx->world > 1)
+      MLFF_TRY(comm_allgather(ctx, ctx->xg + (int64_t)ctx->rank * blk, ctx->xg, (size_t)blk));
     launch_gemv_rows(A, ctx->ld, nrows, ctx->xg, y_loc, 1.0, 0.0, nullptr, nullptr, s);
     return MLFF_OK;
   };

@@ -175,10 +175,7 @@ class ShardedKernelSolver:
     def precon_eig(self, k, mask_mode=0, dim_i=0, build_woodbury=True, want_evals=False,
                    want_rowlev=False):
         """Truncated eigensolver over all ranks (evals and global row norms from rank 0);
-        mask_mode 2 needs the dense K on one device."""
-        if mask_mode == 2:
-            raise NotImplementedError("the atomic-interactions mask is formed from the dense K "
-                                      "of one device; use a single device")
+        mask_mode 2 masks every rank's rows of the dense K (assemble_sgdml first)."""
         return self._each("precon_eig", k, mask_mode, dim_i, build_woodbury, want_evals,
                           want_rowlev)[0]
 

@@ -22,7 +22,7 @@ What runs where:
     the operator and of the preconditioner panel are sharded over the devices from this
     one process (sgdml_amd.sharded, RCCL), as the reference spreads its GPU operator
     with DataParallel (predict.py:335-341).  The atomic-interactions eigen preconditioner
-    masks the dense K on the first device.
+    masks every device's rows of the dense K (assembled sharded).
 """
 from __future__ import annotations
 
@@ -89,7 +89,7 @@ class Iterative(object):
         otherwise only the matrix-free operator (the reference's K_op) is set up and
         the preconditioner builds fetch their columns through it, as the reference's
         IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory."""
-        if self.devices is not None and not dense:
+        if self.devices is not None:
             s = ShardedKernelSolver(n, self.devices)
         else:
             dev = self.device if self.devices is None else self.devices[0]

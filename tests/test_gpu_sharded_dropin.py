@@ -101,3 +101,42 @@ def test_sharded_solver_gathers(sg):
     assert r3.info == r1.info == 0 and abs(r3.iters - r1.iters) <= 1
     assert np.linalg.norm(r3.x - r1.x) <= 1e-7 * np.linalg.norm(r1.x)
     assert seen and all(s == n for s in seen)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_atomic_interactions_mask(sg, golden_dir, world):
+    """eigvec_precon_atomic_interactions (iterative_solver.py:1238-1253) sharded: every rank
+    masks its rows of the dense K with the global max|K| (the per-rank maxima all-gathered)
+    and the truncated eigensolver runs on the sharded masked operator.  Against one rank: the
+    top-k eigenvalues to 1e-10 and the Woodbury apply to 1e-9; the drop-in solve against the
+    reference's (which stops at 5N iterations on this system, as in
+    test_gpu_golden.py::test_dropin_solve_eigen_masks): the first residuals within 1e-6 in
+    log10."""
+    from tests.test_gpu_golden import EIGMASK
+
+    f = load(golden_dir, EIGMASK)
+    n = f["y"].size
+    k = int(int(f["k_rot"]) / n * n)
+    dim_i = 3 * f["R"].shape[1]
+    v = np.random.default_rng(4).standard_normal(n)
+    out = {}
+    for w in (1, world):
+        s = sg.KernelSolver(n, device=0) if w == 1 else sg.ShardedKernelSolver(n, [0] * w)
+        try:
+            s.assemble_sgdml(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+            s.set_operator(-1.0, float(f["lam"]))
+            ev, _ = s.precon_eig(k, mask_mode=2, dim_i=dim_i, want_evals=True)
+            out[w] = (ev, s.precon_apply(v))
+        finally:
+            s.close()
+    np.testing.assert_allclose(out[world][0], out[1][0], rtol=1e-10)
+    z1, zw = out[1][1], out[world][1]
+    assert np.linalg.norm(zw - z1) <= 1e-9 * np.linalg.norm(z1)
+    precon = "eigvec_precon_atomic_interactions"
+    (alphas, num_iters, resid, rmse, idxs, is_conv, info), (kind, w) = run(
+        f, EIGMASK, precon, [0] * world)
+    assert kind is sg.ShardedKernelSolver and w == world
+    assert is_conv == bool(f[f"{precon}__is_conv"])
+    ref_tr = f[f"{precon}__trace"]
+    assert np.max(np.abs(np.log10(info["resid_trace"][1:9] / ref_tr[:8]))) <= 1e-6
