@@ -625,7 +625,7 @@ static unsigned lr_fin_grid(int64_t n) {
 // held in registers.  D + L + 1 register buffers: row j (consumed), rows j + 1 … j + D - 1
 // (waiting for their partials), j + D (partial formed and published; loaded L steps
 // earlier), rows in flight up to j + D + L (loading): D row-steps of slack for the hand-off,
-// L steps between a row's load and its use.  A member that waits for more than ~1 s writes
+// L steps between a row's load and its use.  A member that waits for more than ~0.1 s writes
 // ST_FAULT to `fault` and leaves (the host reports an error; a cluster can only stall if its
 // members are not all resident, which the host checks with the occupancy query before it
 // chooses this path).
@@ -677,7 +677,10 @@ __device__ __forceinline__ bool lc_consume(const LcArgs &a, int row, unsigned lo
     const bool ok = lane >= a.C ||
                     ((unsigned)(x0 >> 32) == a.epoch && (unsigned)(x1 >> 32) == a.epoch);
     if (__all(ok)) break;
-    if (wall_clock64() - t0 > 100000000ull) return false;  // ~1 s at 100 MHz
+    // ~0.1 s at 100 MHz: far above any hand-off of a resident cluster (the whole apply takes
+    // <= 50 ms at N = 505050), short enough that a cluster starved by another process's
+    // kernels falls back to two passes quickly (the next preconditioner build re-checks)
+    if (wall_clock64() - t0 > 10000000ull) return false;
     __builtin_amdgcn_s_sleep(1);
     if (lane < a.C) {
       x0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -885,7 +888,7 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
   // hand-off slack D = 2 steps, load distance L = 1 (D = 1, L = 2: apply 3.95 -> 4.22 ms at
   // N = 156510; the hand-off, not the load latency, sets the pace)
   // MLFF_LC_TEST_MUTE=<b>[@<e>]: workgroup b never publishes (from the launch with epoch e
-  // on, default every launch), so its cluster's hand-offs time out (tests of the ~1 s fault
+  // on, default every launch), so its cluster's hand-offs time out (tests of the ~0.1 s fault
   // bail-out, also in the middle of a chunk of PCG iterations; never set in production)
   int mute = -1;
   if (const char *mute_env = std::getenv("MLFF_LC_TEST_MUTE")) {

@@ -352,7 +352,7 @@ def test_one_pass_lowrank_apply(sg, monkeypatch, n, k, clusters):
 
 def test_cluster_apply_fault_falls_back(sg, monkeypatch):
     """A cluster member that never publishes its partial (test hook MLFF_LC_TEST_MUTE) makes
-    its cluster's hand-offs time out: the members leave after ~1 s instead of hanging the GPU,
+    its cluster's hand-offs time out: the members leave after ~0.1 s instead of hanging the GPU,
     the apply is redone with two passes (correct z), the context stays on the two-pass form;
     in a PCG solve the faulted iteration is re-run with two passes and the solve converges to
     the result of a two-pass solve."""
