@@ -99,6 +99,14 @@ int mlff_device_count(int *n_out);
 /* RCCL unique id (128 bytes) for a world > 1 context; rank 0 creates it and the
  * caller broadcasts it (torch.distributed / any channel) to the other ranks. */
 int mlff_comm_unique_id(unsigned char id_out[128]);
+/* Test hook: runs the library's RCCL allreduce / allgather (out of place and in place) /
+ * reduce-scatter code on a ONE-rank RCCL communicator over `count` doubles, each between a
+ * producing kernel and a consuming copy on the same stream, and returns the largest
+ * deviation from the expected values (0 when correct, +inf for a poisoned entry).  The
+ * multi-rank data path (sharded_pcg.py / api.hip comm_*) uses exactly these functions; a
+ * one-GPU box can run no larger communicator.  No reference counterpart (torch.distributed
+ * collectives in the reference's sharded callers are what comm_* replaces). */
+int mlff_comm_selftest(int device, int64_t count, double *max_err_out);
 
 /* ---- context --------------------------------------------------------------- */
 /* n_global: kernel size N.  comm_id may be NULL when world == 1.  comm_id is a 128-byte

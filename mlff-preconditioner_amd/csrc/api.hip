@@ -168,6 +168,33 @@ std::shared_ptr<LocalGroup> join_local_group(const std::string &key, int world) 
   return gp;
 }
 
+__global__ void k_selftest_fill(double *p, size_t n, double scale) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = scale * (1.0 + 0.5 * (double)i);
+}
+
+// RCCL transport: the collectives are enqueued on the context's stream, so they are ordered
+// after the kernels that produced `send` and before the ones that read `recv` with no host
+// synchronisation.  Semantics are those of the LOCAL branches below: allreduce in place over
+// n doubles; allgather of `count` doubles per rank into recv[rank*count ...] (in place when
+// send == recv + rank*count); reduce-scatter of world*count doubles into this rank's `count`.
+// mlff_comm_selftest drives these three functions on a one-rank communicator, the only RCCL
+// configuration a one-GPU box can run.
+static int rccl_allreduce(mlff_ctx *ctx, double *buf, size_t n) {
+  MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  return MLFF_OK;
+}
+
+static int rccl_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count) {
+  MLFF_NCCL(ctx, ncclAllGather(send, recv, count, ncclDouble, ctx->comm, ctx->stream));
+  return MLFF_OK;
+}
+
+static int rccl_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t count) {
+  MLFF_NCCL(ctx, ncclReduceScatter(send, recv, count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  return MLFF_OK;
+}
+
 // SOLO transport (comm_id "SOLO:..."): ONE rank of a W-way split runs alone and every
 // collective keeps only this rank's own contribution (no data from peers, no wait).  The
 // numbers are meaningless; the kernels, their sizes and their launch sequence are those of
@@ -175,10 +202,7 @@ std::shared_ptr<LocalGroup> join_local_group(const std::string &key, int world) 
 // iteration without the collectives (bench.py --solo-world).  Profiling only.
 int comm_allreduce(mlff_ctx *ctx, double *buf, size_t n) {
   if (ctx->world <= 1 || n == 0 || ctx->solo) return MLFF_OK;
-  if (ctx->comm != nullptr) {
-    MLFF_NCCL(ctx, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-    return MLFF_OK;
-  }
+  if (ctx->comm != nullptr) return rccl_allreduce(ctx, buf, n);
   LocalGroup &g = *ctx->local;
   std::vector<double> mine(n), sum(n, 0.0);
   MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), buf, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
@@ -208,10 +232,7 @@ int comm_allgather(mlff_ctx *ctx, const double *send, double *recv, size_t count
       MLFF_HIP(ctx, hipMemcpyAsync(own, send, sizeof(double) * count, hipMemcpyDeviceToDevice, ctx->stream));
     return MLFF_OK;
   }
-  if (ctx->comm != nullptr) {
-    MLFF_NCCL(ctx, ncclAllGather(send, recv, count, ncclDouble, ctx->comm, ctx->stream));
-    return MLFF_OK;
-  }
+  if (ctx->comm != nullptr) return rccl_allgather(ctx, send, recv, count);
   LocalGroup &g = *ctx->local;
   std::vector<double> mine(count);
   MLFF_HIP(ctx, hipMemcpyAsync(mine.data(), send, sizeof(double) * count, hipMemcpyDeviceToHost, ctx->stream));
@@ -239,10 +260,7 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
                                  hipMemcpyDeviceToDevice, ctx->stream));
     return MLFF_OK;
   }
-  if (ctx->comm != nullptr) {
-    MLFF_NCCL(ctx, ncclReduceScatter(send, recv, count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-    return MLFF_OK;
-  }
+  if (ctx->comm != nullptr) return rccl_reduce_scatter(ctx, send, recv, count);
   LocalGroup &g = *ctx->local;
   const size_t n = count * (size_t)g.world;
   std::vector<double> mine(n), out(count, 0.0);
@@ -913,6 +931,76 @@ int mlff_comm_unique_id(unsigned char id_out[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   std::memcpy(id_out, &id, 128);
   return MLFF_OK;
+  MLFF_API_END(nullptr)
+}
+
+int mlff_comm_selftest(int device, int64_t count, double *max_err_out) {
+  MLFF_API_BEGIN
+  if (max_err_out == nullptr || count < 1) return set_error(nullptr, MLFF_ERR_ARG, "bad arguments");
+  *max_err_out = -1.0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return set_error(nullptr, MLFF_ERR_ARG, "bad device id");
+  mlff_ctx *ctx = new mlff_ctx();
+  ctx->device = device;
+  ctx->rank = 0;
+  ctx->world = 1;
+  double *a = nullptr, *b = nullptr;
+  auto done = [&](int rc) {
+    dev_free(a);
+    dev_free(b);
+    mlff_ctx_destroy(ctx);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+    return done(set_error(nullptr, MLFF_ERR_HIP, "stream create failed"));
+  ncclUniqueId id;
+  ncclResult_t e = ncclGetUniqueId(&id);
+  if (e == ncclSuccess) e = ncclCommInitRank(&ctx->comm, 1, id, 0);
+  if (e != ncclSuccess) {
+    ctx->comm = nullptr;
+    return done(set_error(nullptr, MLFF_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e)));
+  }
+  const size_t n = (size_t)count;
+  if (hipMalloc(&a, sizeof(double) * n) != hipSuccess || hipMalloc(&b, sizeof(double) * n) != hipSuccess)
+    return done(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
+  std::vector<double> h(n);
+  double worst = 0.0;
+  // every collective sits between a producing kernel and a consuming copy on the same stream
+  // (no host synchronisation in between), so a transport that ran off-stream would read the
+  // input before it is written or leave the poisoned output in place
+  auto check = [&](const double *src, double scale) -> int {
+    MLFF_HIP(ctx, hipMemcpyAsync(h.data(), src, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+    MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < n; ++i) {
+      const double d = std::fabs(h[i] - scale * (1.0 + 0.5 * (double)i));
+      worst = std::isfinite(d) ? std::max(worst, d) : INFINITY;
+    }
+    return MLFF_OK;
+  };
+  auto fill = [&](double *p, double scale) {
+    hipLaunchKernelGGL(k_selftest_fill, dim3(256), dim3(256), 0, ctx->stream, p, n, scale);
+  };
+  auto poison = [&](double *p) { return hipMemsetAsync(p, 0xff, sizeof(double) * n, ctx->stream); };
+  // allreduce in place
+  fill(a, 1.0);
+  if (int rc = rccl_allreduce(ctx, a, n)) return done(rc);
+  if (int rc = check(a, 1.0)) return done(rc);
+  // allgather out of place, then in place (send == recv + rank * count)
+  fill(a, 2.0);
+  MLFF_HIP(ctx, poison(b));
+  if (int rc = rccl_allgather(ctx, a, b, n)) return done(rc);
+  if (int rc = check(b, 2.0)) return done(rc);
+  fill(b, 3.0);
+  if (int rc = rccl_allgather(ctx, b, b, n)) return done(rc);
+  if (int rc = check(b, 3.0)) return done(rc);
+  // reduce-scatter out of place
+  fill(b, 4.0);
+  MLFF_HIP(ctx, poison(a));
+  if (int rc = rccl_reduce_scatter(ctx, b, a, n)) return done(rc);
+  if (int rc = check(a, 4.0)) return done(rc);
+  *max_err_out = worst;
+  return done(MLFF_OK);
   MLFF_API_END(nullptr)
 }
 

@@ -47,6 +47,7 @@ SIGNATURES = {
     "mlff_version": (_int, []),
     "mlff_device_count": (_int, [_p_int]),
     "mlff_comm_unique_id": (_int, [ctypes.c_char_p]),
+    "mlff_comm_selftest": (_int, [_int, _i64, ctypes.POINTER(ctypes.c_double)]),
     "mlff_ctx_create": (_int, [_int, _int, _int, ctypes.c_char_p, _i64, ctypes.POINTER(_c_ctx)]),
     "mlff_ctx_destroy": (_int, [_c_ctx]),
     "mlff_last_error": (ctypes.c_char_p, [_c_ctx]),
@@ -176,3 +177,11 @@ def comm_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     check(lib.mlff_comm_unique_id(buf), None, "mlff_comm_unique_id")
     return buf.raw
+
+
+def comm_selftest(device: int = 0, count: int = 1 << 20) -> float:
+    """RCCL transport self-test on a one-rank communicator (include/mlffpcg.h)."""
+    lib = load_library()
+    err = ctypes.c_double(-1.0)
+    check(lib.mlff_comm_selftest(int(device), int(count), ctypes.byref(err)), None, "mlff_comm_selftest")
+    return err.value

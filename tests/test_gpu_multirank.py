@@ -351,3 +351,16 @@ def test_configs3_eight_ranks_full_size():
     np.testing.assert_allclose(outs[0][3], ref[3], rtol=1e-7)
     x = np.concatenate([o[4] for o in outs])
     assert np.linalg.norm(x - ref[4]) <= 1e-7 * np.linalg.norm(ref[4])
+
+
+@pytest.mark.parametrize("count", [1, 3, 1000003, 1 << 22])
+def test_rccl_transport_one_rank(count):
+    """The RCCL branches of comm_allreduce / comm_allgather / comm_reduce_scatter
+    (api.hip rccl_*), the transport the 8-GPU bench and drop-in run on, driven on a
+    one-rank communicator: in-place and out-of-place forms, odd and multi-chunk counts,
+    each collective between a producing kernel and a consuming copy on the context's
+    stream.  A one-rank sum or gather is the identity, so any deviation is a count,
+    datatype, buffer or stream-ordering error in the call itself."""
+    from sgdml_amd import _native
+
+    assert _native.comm_selftest(0, count) == 0.0
