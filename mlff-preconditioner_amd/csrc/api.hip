@@ -641,10 +641,10 @@ int resolve_storage(mlff_ctx *ctx) {
 // pq_part: also the v_loc . y_loc partials of the CG step (kVecGrid, k_dot_part's layout;
 // fused into the last operator kernel where it can be)
 int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const double *v_loc,
-                    const int *status, double *pq_part = nullptr) {
+                    const int *status, double *pq_part = nullptr, const PFuse *pf = nullptr) {
   hipStream_t s = ctx->stream;
   if (ctx->use_mf) {
-    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part);
+    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part, pf);
     return MLFF_OK;
   }
   if (!ctx->use_sym) {
@@ -826,6 +826,15 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   return MLFF_OK;
 }
 
+// MLFF_FUSE_XR=0: k_update_xr as its own launch every iteration (A/B)
+bool xr_fold_enabled() {
+  static const bool on = [] {
+    const char *e = std::getenv("MLFF_FUSE_XR");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // one PCG iteration (ITER = it), all launches status gated.  fold_in: the stop test of
 // iteration it - 1 runs in this iteration's first kernel (StopFold); stop_out: the stop
 // test of this iteration runs as its own launch (last iteration of a chunk)
@@ -841,12 +850,25 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
   const bool lowrank = ctx->precon_kind != MLFF_PRECON_NONE;
   StopFold fold;
   if (fold_in) fold = StopFold{rr_part(ctx), ctx->st, ctx->trace, it - 1};
+  // matrix-free operator (default form): p = z + beta p formed inside the operator kernels;
+  // with the one-pass apply also k_update_xr of iteration it - 1 folded into this
+  // iteration's apply (x, r, rr partials written by k_lr_fin) and its stop test into the
+  // operator's first kernel: 4 launches per iteration instead of 6
+  const bool fuse_p = ctx->use_mf && mf_can_fuse_p(ctx);
+  const bool fuse_xr = fuse_p && lowrank && ctx->lr_rows && xr_fold_enabled();
+  XrFold xf;
+  StopFold fold_op;
+  if (fuse_xr && fold_in) {  // iteration it - 1 left its x, r update to this iteration
+    xf = XrFold{ctx->x, ctx->r, p_loc, ctx->q, pq_part(ctx), rr_part(ctx), ctx->st};
+    fold_op = fold;
+    fold = StopFold{};
+  }
   const double *zsrc;
   if (lowrank) {
     const size_t pm = mark_begin(ctx, marks);
     if (ctx->lr_rows) {
       launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
-                           1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold);
+                           1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold, xf);
     } else if (ctx->lr_cluster) {
       launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, ctx->r, ctx->z, ctx->nrows,
                               ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s,
@@ -864,7 +886,8 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
     launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s, fold);
     zsrc = ctx->r;
   }
-  launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
+  const PFuse pf{zsrc, rho_part(ctx), ctx->st, it, fold_op};
+  if (!fuse_p) launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
   const size_t e0 = mark_begin(ctx, marks);
   if (ctx->use_sym) {
     // q = sigma K p + lam p and the p.q partials from the slot reduction (no dot launch)
@@ -873,11 +896,13 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
                          pq_part(ctx), status, s);
     mark_end(ctx, marks, e0, it);
   } else {
-    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx)));
+    MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx),
+                             fuse_p ? &pf : nullptr));
     mark_end(ctx, marks, e0, it);
   }
-  launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
-                   status, s);
+  if (!fuse_xr || stop_out)  // else: done by iteration it + 1 (same chunk, fold_in)
+    launch_update_xr(ctx->x, ctx->r, p_loc, ctx->q, ctx->nrows, pq_part(ctx), rr_part(ctx), ctx->st,
+                     status, s);
   if (stop_out) launch_stoptest(rr_part(ctx), ctx->st, ctx->trace, it, s);
   return MLFF_OK;
 }
@@ -1835,10 +1860,18 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
         ctx->timing.iter_count += done_now - ctx->pcg_done;
       }
     }
+    static const bool dbg = std::getenv("MLFF_PCG_DEBUG") != nullptr;
+    if (dbg)
+      std::fprintf(stderr, "pcg chunk [%lld, %lld]: status %d iters %lld resid %.17g atol %.17g\n",
+                   (long long)first, (long long)last, ctx->h_st->status, ctx->h_st->iters,
+                   ctx->h_st->resid, ctx->h_st->atol);
     while (ctx->h_st->status == ST_RECHECK) {
       MLFF_TRY(do_recheck(ctx));
       MLFF_TRY(poll_state(ctx));
       ctx->spec_t = false;  // r was recomputed: the speculative T r is stale
+      if (dbg)
+        std::fprintf(stderr, "  recheck: status %d iters %lld resid %.17g\n", ctx->h_st->status,
+                     ctx->h_st->iters, ctx->h_st->resid);
     }
     ctx->pcg_done = ctx->h_st->iters;
   }

@@ -42,6 +42,7 @@ struct DevState {
   double sqrt_piv;     // its sqrt(pivot)
   double best_val;     // argmax of this rank
   long long best_pos;
+  double rho_new;      // fused p update: rho of the iteration, published by k_rec_g for k_rec_fin
 };
 
 // Lower-block-triangle tiles of K owned by this rank (kernels_sym.hip).
@@ -148,6 +149,19 @@ struct StopFold {
   long long it = 0;
 };
 
+// The CG update of the previous iteration (k_update_xr: alpha = rho / (p.q); x += alpha p;
+// r -= alpha q; rr partials) folded into this iteration's one-pass low-rank apply: k_lr_rows
+// forms r - alpha q on the fly, k_lr_fin writes x, r and the rr partials (x == nullptr: none)
+struct XrFold {
+  double *x = nullptr;
+  double *r = nullptr;
+  const double *p = nullptr;
+  const double *q = nullptr;
+  const double *pq_part = nullptr;
+  double *rr_part = nullptr;
+  DevState *st = nullptr;
+};
+
 // flags of the timing-only events (stamps read after a stream synchronisation): no
 // system-scope fence, so recording one does not write back and invalidate the caches
 // between the kernels it brackets (MLFF_EVENT_FENCE=1 restores the default, for A/B)
@@ -191,6 +205,74 @@ __device__ __forceinline__ double block_sum256(double v, double *sh) {
   double t = 0.0;
   if (threadIdx.x == 0) t = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   return t;
+}
+
+// Deterministic sum of np partials, broadcast to every thread of the block.
+__device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ part, int np,
+                                                     double *sh) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) v += part[i];
+  v = block_sum256(v, sh);
+  __syncthreads();
+  if (threadIdx.x == 0) sh[4] = v;
+  __syncthreads();
+  return sh[4];
+}
+
+// scipy's stop test of iteration f.it on the summed rr partials (k_stoptest); block (0, 0)
+// writes the state.  True: the solver continues.
+__device__ __forceinline__ bool stop_decide(const StopFold &f, double rr) {
+  const double resid = sqrt(rr);
+  DevState *st = f.st;
+  int dec = ST_RUNNING;
+  if (resid <= st->atol)
+    dec = f.it > 1 ? ST_RECHECK : ST_CONVERGED;
+  else if (f.it >= st->maxiter)
+    dec = ST_MAXITER;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    st->rr = rr;
+    st->resid = resid;
+    st->iters = f.it;
+    f.trace[f.it] = resid;
+    if (dec != ST_RUNNING)
+      st->status = dec;
+    else
+      st->rho1 = st->rho;
+  }
+  return dec == ST_RUNNING;
+}
+
+// reduce_parts_bcast for a workgroup of any multiple of 256 threads: the first 256 threads
+// reduce the partials exactly as reduce_parts_bcast does (same bits), every thread gets it
+__device__ __forceinline__ double reduce_parts_bcast_wide(const double *__restrict__ part, int np,
+                                                          double *sh) {
+  double v = 0.0;
+  if (threadIdx.x < 256)
+    for (int i = threadIdx.x; i < np; i += 256) v += part[i];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0 && w < 4) sh[w] = v;
+  __syncthreads();
+  const double t = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();  // sh is reused by the caller
+  return t;
+}
+
+// The same sum in two halves, so the loads can be issued long before the reduction:
+// parts_thread_sum is the thread's share (the loop of reduce_parts_bcast), parts_bcast the
+// block reduction of those shares (same bits as reduce_parts_bcast)
+__device__ __forceinline__ double parts_thread_sum(const double *__restrict__ part, int np) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) v += part[i];
+  return v;
+}
+__device__ __forceinline__ double parts_bcast(double v, double *sh) {
+  v = block_sum256(v, sh);
+  __syncthreads();
+  if (threadIdx.x == 0) sh[4] = v;
+  __syncthreads();
+  return sh[4];
 }
 
 }  // namespace mlff
@@ -385,7 +467,7 @@ int lr_rows_groups(int64_t k);
 void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
                           int64_t n, double sigma_p, double lam_inv, double *rho_part,
                           const int *status, hipStream_t s, double *zpart,
-                          StopFold fold = StopFold{});
+                          StopFold fold = StopFold{}, XrFold xf = XrFold{});
 // the one-pass apply for long rows (clusters of lr_cluster_members(ldt) workgroups, one per
 // CU, hand-offs of the per-row partial dots); lr_cluster_count = clusters resident at once
 bool lr_cluster_fits(int64_t ldt);
@@ -540,9 +622,19 @@ int comm_reduce_scatter(mlff_ctx *ctx, const double *send, double *recv, size_t 
 int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_t M, int n_atoms,
              const int32_t *perms, int n_perms, double sig);
 // pq_part != nullptr: also the x_loc . y_loc partials (kVecGrid, as launch_dot_part)
+// the search-direction update p = z + (rho / rho1) p (k_update_p) fused into the
+// matrix-free operator of a PCG iteration (x_full = x_loc = p_old on one rank)
+struct PFuse {
+  const double *z;
+  const double *rho_part;
+  DevState *st;
+  long long it;
+  StopFold sf;  // the previous iteration's stop test (after a folded k_update_xr), or none
+};
+bool mf_can_fuse_p(const mlff_ctx *ctx);
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
                         const double *x_loc, const int *status, double sigma, double lam,
-                        double *pq_part = nullptr);
+                        double *pq_part = nullptr, const PFuse *pf = nullptr);
 int mf_diag(mlff_ctx *ctx, double *out);
 // sigma K_op columns through the single-column path (mf.uvk); false when it is not set up
 bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double sigma,

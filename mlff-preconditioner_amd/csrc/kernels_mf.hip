@@ -552,7 +552,24 @@ struct RecArgs {
   int n, n_perms, nblk;
   double *rpart;       // nblk x ni x 3n
   double *sv;          // ni x MP
+  // fused search-direction update (one rank, PCG iteration): the operand is
+  // p = z + (rho / rho1) p_old (p = z at ITER 1) formed on the fly from xc = p_old and pz,
+  // rho the fixed-order sum of rho_part (k_update_p's arithmetic, the same bits); k_rec_fin
+  // writes p.  pz == nullptr: xc is the operand itself
+  const double *pz = nullptr;
+  const double *rho_part = nullptr;
+  DevState *st = nullptr;
+  long long it = 0;
+  // the stop test of the previous iteration (its rr partials written by k_lr_fin's folded
+  // k_update_xr), done by workgroup 0; beta's rho1 is then the state's rho (the stop test
+  // copies it into rho1 in this same launch)
+  StopFold sf;
 };
+
+// the operand entry of a fused update (k_update_p: p = fma(beta, p_old, z), p = z at ITER 1)
+__device__ __forceinline__ double fused_p(double pold, double z, double beta, bool first) {
+  return first ? z : fma(beta, pold, z);
+}
 
 // wt: w transposed, round_up(MP, kRJ) rows of ldw = ngrp kRG entries, zero padded, so
 // the accumulation runs unguarded over whole batches and point groups
@@ -580,7 +597,8 @@ enum { kZGather = 0, kZIdent = 1, kZStored = 2 };
 // CAP: with one identity permutation the query points' Rdd rows are captured from the Zt
 // batches into registers for the epilogue (CAP = false: re-read per epilogue round, fewer
 // registers live across the loop)
-template <int ZM, bool CAP = true, int RG = kRG, int RR = 8, int WC = kWC>
+// FP: the fused search-direction update (RecArgs::pz; identity permutation)
+template <int ZM, bool CAP = true, int RG = kRG, int RR = 8, int WC = kWC, bool FP = false>
 __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restrict__ wt,
                                                int64_t nbp, int64_t ngrp, int64_t nsw8,
                                                const int *__restrict__ status) {
@@ -590,27 +608,49 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
   const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double red[RR][3][kRB][kRB + 1];
   __shared__ double sW[WC][RG];
+  __shared__ double shp[8];
   const int tid = threadIdx.x;
   const int n3 = 3 * a.n;
+  static_assert(!FP || ZM == kZIdent, "fused p: identity permutation");
+  // fused p: rho1 and this thread's share of the rho partials, requested first
+  const bool first = FP && a.it <= 1;
+  const bool sfold = FP && a.sf.rr_part != nullptr;
+  const double rho1 = FP ? (sfold ? a.st->rho : a.st->rho1) : 1.0;
+  const double rshare = FP ? parts_thread_sum(a.rho_part, kVecGrid) : 0.0;
   if ((int64_t)blockIdx.x < nsw8) {  // pair scalars: one wave per (local point, j, p)
+    // (fused p: beta first, by all four waves; the scalar waves are off the critical path)
+    const double rho = FP ? parts_bcast(rshare, shp) : 0.0;
+    const double beta = rho / rho1;
+    if (FP && blockIdx.x == 0 && tid == 0) a.st->rho_new = rho;  // for k_rec_fin
+    // the previous iteration's stop test (gated like k_stoptest: a solver stopped before this
+    // iteration keeps its state); uniform in block 0, whose thread 0 writes the state
+    if (sfold && blockIdx.x == 0 && st0 == ST_RUNNING)
+      stop_decide(a.sf, reduce_parts_bcast(a.sf.rr_part, kVecGrid, shp));
     const int64_t q = (int64_t)blockIdx.x * 4 + (tid >> 6);
     if (q >= a.ni * a.MP) return;
     const int64_t il = q / a.MP, jp = q % a.MP, j = jp / a.n_perms;
     const double *vv = a.uvk + q * (int64_t)(6 * a.n + 2) + n3;
     const double *xj = a.xc + j * n3;
+    const double *zj = FP ? a.pz + j * n3 : xj;
     double acc = 0.0;
     int t = tid & 63;
     for (; t + 7 * 64 < n3; t += 8 * 64) {  // 16 loads in flight, summed in t order
-      double va[8], xa[8];
+      double va[8], xa[8], za[FP ? 8 : 1];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         va[u] = vv[t + u * 64];
         xa[u] = xj[t + u * 64];
+        if (FP) za[u % (FP ? 8 : 1)] = zj[t + u * 64];
+      }
+      if (FP) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) xa[u] = fused_p(xa[u], za[u % (FP ? 8 : 1)], beta, first);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc = fma(va[u], xa[u], acc);
     }
-    for (; t < n3; t += 64) acc = fma(vv[t], xj[t], acc);
+    for (; t < n3; t += 64)
+      acc = fma(vv[t], FP ? fused_p(xj[t], zj[t], beta, first) : xj[t], acc);
     if (st0 != ST_RUNNING) return;
     acc = wave_sum(acc);
     if ((tid & 63) == 0) a.sv[il * a.MP + jp] = 5.0 * vv[3 * a.n] * acc;  // 5 m (v . x_j)
@@ -679,7 +719,7 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
     const int cn = (int)((MPp - c0) < WC ? (MPp - c0) : WC);
     // (every thread's staging loads issued together, then stored)
     constexpr int kWL = (WC * RG + 255) / 256, kXL = WC * 2 * kRB * 3 / 256;
-    double wl[kWL], xl[IDENT ? kXL : 1];
+    double wl[kWL], xl[IDENT ? kXL : 1], zl[FP ? kXL : 1];
 #pragma unroll
     for (int q = 0; q < kWL; ++q) {
       const int e = tid + q * 256;
@@ -692,10 +732,17 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
         const int jj = e / (2 * kRB * 3), r = e % (2 * kRB * 3);
         const int atom = (r < kRB * 3 ? A : B) * kRB + (r % (kRB * 3)) / 3;
         const int64_t j = c0 + jj;
-        xl[q] = (jj < cn && j < a.MP && atom < a.n) ? a.xc[j * n3 + 3 * atom + r % 3] : 0.0;
+        const bool ok = jj < cn && j < a.MP && atom < a.n;
+        xl[q] = ok ? a.xc[j * n3 + 3 * atom + r % 3] : 0.0;
+        if (FP) zl[q % (FP ? kXL : 1)] = ok ? a.pz[j * n3 + 3 * atom + r % 3] : 0.0;
       }
     }
     if (c0 == 0 && st0 != ST_RUNNING) return;  // uniform: before the first barrier
+    if (FP) {  // the operand at the block's atoms: p = z + beta p_old (every load in flight)
+      const double beta = parts_bcast(rshare, shp) / rho1;
+#pragma unroll
+      for (int q = 0; q < kXL; ++q) xl[q] = fused_p(xl[q], zl[q % (FP ? kXL : 1)], beta, first);
+    }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kWL; ++q)
@@ -866,6 +913,16 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
 // 2^lg lanes per row (a lane sums every 2^lg-th term of both series, then a butterfly
 // over the group: every lane of it holds the same bits), so the few rows of a small
 // system still spread over the whole grid.
+// fused search-direction update (k_rec_g FP): the operand rows are p = z + beta p_old,
+// written back to p here (after k_rec_g has read p_old), rho stored in the state
+struct FinFuse {
+  const double *z = nullptr;  // nullptr: not fused
+  const double *rho_part = nullptr;
+  DevState *st = nullptr;
+  long long it = 0;
+  double *p = nullptr;        // = xloc
+};
+
 template <bool PQ>
 __global__ __launch_bounds__(256) void k_rec_fin(const double *__restrict__ uvk,
                                                  const double *__restrict__ sv,
@@ -875,9 +932,17 @@ __global__ __launch_bounds__(256) void k_rec_fin(const double *__restrict__ uvk,
                                                  double lam, const double *__restrict__ xloc,
                                                  double *__restrict__ y,
                                                  double *__restrict__ pq_part, int lg,
-                                                 const int *__restrict__ status) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+                                                 const int *__restrict__ status, FinFuse ff) {
+  // the status word only gates the stores: tested once the row's loads are issued
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double sh[8];
+  const bool fp = ff.z != nullptr, first = ff.it <= 1;
+  double beta = 0.0;
+  if (fp) {  // rho as k_rec_g summed it, rho1 as its stop test left it: the same beta bits
+    const double rho = ff.st->rho_new, rho1 = ff.st->rho1;
+    beta = rho / rho1;
+    if (st0 == ST_RUNNING && blockIdx.x == 0 && threadIdx.x == 0) ff.st->rho = rho;
+  }
   const int64_t n3 = 3 * (int64_t)n, stride = 6 * (int64_t)n + 2, pstride = ni * n3;
   const int G = 1 << lg, sub = threadIdx.x & (G - 1);
   const int64_t pass = (int64_t)gridDim.x * (256 >> lg);
@@ -905,17 +970,22 @@ __global__ __launch_bounds__(256) void k_rec_fin(const double *__restrict__ uvk,
       for (int e = 0; e < 4; ++e) sl += pp[e];
     }
     for (; q < nblk; q += G) sl += rpart[q * pstride + pr];
+    double xv = xloc != nullptr ? xloc[r] : 0.0;
+    if (fp) xv = fused_p(xv, ff.z[r], beta, first);
+    if (st0 != ST_RUNNING) return;  // uniform
     for (int m = G >> 1; m > 0; m >>= 1) {
       acc += __shfl_xor(acc, m, G);
       sl += __shfl_xor(sl, m, G);
     }
     if (sub == 0) {
       double yv = sigma * (acc - sl);
-      if (xloc != nullptr) yv += lam * xloc[r];
+      if (xloc != nullptr) yv += lam * xv;
       y[r] = yv;
-      if (PQ) pq = fma(xloc[r], yv, pq);
+      if (fp) ff.p[r] = xv;
+      if (PQ) pq = fma(xv, yv, pq);
     }
   }
+  if (st0 != ST_RUNNING) return;  // uniform (a block without rows)
   if (PQ) {
     const double t = block_sum256(pq, sh);
     if (threadIdx.x == 0) pq_part[blockIdx.x] = t;
@@ -1053,9 +1123,22 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   return MLFF_OK;
 }
 
+// the fused p update runs in the default record-factored form only: one rank, one identity
+// permutation, <= 16 local points, w in one 16-slot chunk (the nanotube configs[1] system)
+bool mf_can_fuse_p(const mlff_ctx *ctx) {
+  static const bool on = [] {
+    const char *e = std::getenv("MLFF_FUSE_P");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  const MfData &mf = ctx->mf;
+  return on && ctx->world == 1 && mf.rec && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
+         mf.rec_rg == 8 && round_up(mf.M * mf.n_perms, kRJ) <= 16 && mf.rec_wc16 &&
+         ctx->nrows == ctx->N;
+}
+
 void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc,
                         const double *x_loc, const int *status, double sigma, double lam,
-                        double *pq_part) {
+                        double *pq_part, const PFuse *pf) {
   const MfData &mf = ctx->mf;
   hipStream_t s = ctx->stream;
   const int64_t MP = mf.M * mf.n_perms;
@@ -1077,8 +1160,17 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   static int rec_launches = 0;
 #endif
   if (mf.rec) {
-    const RecArgs ra{mf.Rdd, mf.Zt, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni,
-                     MP, mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
+    RecArgs ra{mf.Rdd, mf.Zt, xc, mf.Pt, mf.ps, mf.pt, mf.uvk, mf.M, mf.D, mf.i0, mf.ni,
+               MP, mf.ldw, (int)mf.n, (int)mf.n_perms, mf.rblk, mf.rpart, mf.sv};
+    FinFuse ff;
+    if (pf != nullptr) {  // mf_can_fuse_p(ctx) holds (the caller checked)
+      ra.pz = pf->z;
+      ra.rho_part = pf->rho_part;
+      ra.st = pf->st;
+      ra.it = pf->it;
+      ra.sf = pf->sf;
+      ff = FinFuse{pf->z, pf->rho_part, pf->st, pf->it, const_cast<double *>(x_loc)};
+    }
     const int64_t nbp = (int64_t)mf.rblk * (mf.rblk + 1) / 2, ngrp = (mf.ni + kRG - 1) / kRG;
     const int64_t nbp8 = (nbp + 7) / 8 * 8, nsw8 = (mf.ni * MP + 31) / 32 * 8;
     const dim3 grid((unsigned)(nsw8 + nbp8 * ngrp));
@@ -1096,7 +1188,10 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
         // the query points' rows re-read from L2 (registers for 3-4 waves per SIMD)
         const int64_t ng = (mf.ni + mf.rec_rg - 1) / mf.rec_rg;
         const dim3 gridg((unsigned)(nsw8 + nbp8 * ng));
-        if (mf.rec_rg == 8 && round_up(MP, kRJ) <= 16 && mf.rec_wc16)  // one 16-slot chunk
+        if (pf != nullptr)  // one 16-slot chunk, the p update fused
+          hipLaunchKernelGGL((k_rec_g<kZIdent, false, 8, 4, 16, true>), gridg, dim3(256), 0, s, ra, wt,
+                             nbp, ng, nsw8, status);
+        else if (mf.rec_rg == 8 && round_up(MP, kRJ) <= 16 && mf.rec_wc16)  // one 16-slot chunk
           hipLaunchKernelGGL((k_rec_g<kZIdent, false, 8, 4, 16>), gridg, dim3(256), 0, s, ra, wt, nbp,
                              ng, nsw8, status);
         else if (mf.rec_rg == 8)
@@ -1137,12 +1232,12 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     if (pq_part != nullptr) {
       hipLaunchKernelGGL(k_rec_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.uvk, mf.sv, mf.rpart,
                          mf.rblk, MP, (int)mf.n, mf.i0, mf.ni, ctx->row0, ctx->nrows, sigma, lam,
-                         x_loc, y_loc, pq_part, lg, status);
+                         x_loc, y_loc, pq_part, lg, status, ff);
     } else if (ctx->nrows > 0) {
       const int64_t nb = std::min<int64_t>((ctx->nrows << lg) / 256 + 1, 1024);
       hipLaunchKernelGGL(k_rec_fin<false>, dim3((unsigned)nb), dim3(256), 0, s, mf.uvk, mf.sv,
                          mf.rpart, mf.rblk, MP, (int)mf.n, mf.i0, mf.ni, ctx->row0, ctx->nrows,
-                         sigma, lam, x_loc, y_loc, (double *)nullptr, lg, status);
+                         sigma, lam, x_loc, y_loc, (double *)nullptr, lg, status, FinFuse{});
     }
     return;
   }

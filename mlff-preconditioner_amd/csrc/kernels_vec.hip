@@ -16,20 +16,6 @@ namespace mlff {
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 
-// Deterministic sum of np partials, broadcast to every thread of the block.
-__device__ __forceinline__ double reduce_parts_bcast(const double *__restrict__ part, int np,
-                                                     double *sh) {
-  double v = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) v += part[i];
-  v = block_sum256(v, sh);
-  __syncthreads();
-  if (threadIdx.x == 0) sh[4] = v;
-  __syncthreads();
-  return sh[4];
-}
-
-__device__ __forceinline__ bool stop_decide(const StopFold &f, double rr);
-
 // Stop test of iteration f.it (as k_stoptest) at the start of the next iteration's first
 // kernel: every workgroup reduces the same partials in the same order and reaches the
 // same decision; workgroup (0, 0) writes the state.  All threads of the block call it.
@@ -56,27 +42,6 @@ __device__ __forceinline__ bool stop_prologue_wide(const StopFold &f, double *sh
   const double rr = (sh[0] + sh[1]) + (sh[2] + sh[3]);
   __syncthreads();  // sh is reused by the caller
   return stop_decide(f, rr);
-}
-
-__device__ __forceinline__ bool stop_decide(const StopFold &f, double rr) {
-  const double resid = sqrt(rr);
-  DevState *st = f.st;
-  int dec = ST_RUNNING;
-  if (resid <= st->atol)
-    dec = f.it > 1 ? ST_RECHECK : ST_CONVERGED;
-  else if (f.it >= st->maxiter)
-    dec = ST_MAXITER;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    st->rr = rr;
-    st->resid = resid;
-    st->iters = f.it;
-    f.trace[f.it] = resid;
-    if (dec != ST_RUNNING)
-      st->status = dec;
-    else
-      st->rho1 = st->rho;
-  }
-  return dec == ST_RUNNING;
 }
 
 // ---------------------------------------------------------------------------
@@ -507,7 +472,7 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
                                                         double *__restrict__ zpart,
                                                         int cached_wgs,
                                                         const int *__restrict__ status,
-                                                        StopFold fold) {
+                                                        StopFold fold, XrFold xf) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ d2 z_sh[M * kLrThreads];
   __shared__ double red[16];
@@ -518,6 +483,24 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
   // (its partials' round trip then overlaps them; a stopped solver drops them unused)
   d2 rv[M];
   lr_load_row<M, 0>(rv, r, bytes);  // zeros beyond ldt
+  if (xf.x != nullptr) {
+    // the residual of the previous iteration, r - alpha q (k_update_xr's arithmetic), before
+    // the first row is requested (q, r and a row in registers at once would spill)
+    d2 qv[M];
+    lr_load_row<M, 0>(qv, xf.q, bytes);
+    const double rho = xf.st->rho;
+    const double pq = reduce_parts_bcast_wide(xf.pq_part, kVecGrid, red);
+    const double alpha = rho / pq;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // k_update_xr's state; k_lr_fin reads alpha
+      xf.st->pq = pq;
+      xf.st->alpha = alpha;
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      rv[m].x = fma(-alpha, qv[m].x, rv[m].x);
+      rv[m].y = fma(-alpha, qv[m].y, rv[m].y);
+    }
+  }
   const bool go = blockIdx.x < cached_wgs ? lr_rows_loop<M, 0>(rv, z_sh, T, ldt, i0, i1, red, fold)
                                            : lr_rows_loop<M, 2>(rv, z_sh, T, ldt, i0, i1, red, fold);
   if (!go) return;
@@ -540,15 +523,28 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
                                                     double *__restrict__ z, int64_t n,
                                                     double sigma_p, double lam_inv,
                                                     double *__restrict__ rho_part,
-                                                    const int *__restrict__ status) {
+                                                    const int *__restrict__ status, XrFold xf) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g0 = (G * w) / NW, g1 = (G * (w + 1)) / NW;
-  double rho = 0.0;
+  double rho = 0.0, rr = 0.0;
+  const bool fx = xf.x != nullptr;
+  // k_update_xr of the previous iteration: alpha = rho / (p.q) as k_lr_rows formed it
+  const double alpha = fx ? xf.st->alpha : 0.0;
   for (int64_t jb = blockIdx.x; jb * 64 < n; jb += gridDim.x) {
     const int64_t j = jb * 64 + lane;
     double s = 0.0;
+    // wave 0's row operands, requested before the partials
+    double rv = 0.0, qj = 0.0, pj = 0.0, xj = 0.0;
+    if (w == 0 && j < n) {
+      rv = r[j];
+      if (fx) {
+        qj = xf.q[j];
+        pj = xf.p[j];
+        xj = xf.x[j];
+      }
+    }
     if (j < n) {
       // batches of 16 partials in flight, the last one predicated (no serial tail)
       const double *pj = zpart + j;
@@ -567,7 +563,12 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
       double sv = sh[0][lane];  // the wave sums in wave order
 #pragma unroll
       for (int q = 1; q < NW; ++q) sv += sh[q][lane];
-      const double rv = r[j];
+      if (fx) {  // x += alpha p; r -= alpha q (k_update_xr), rr partials of that residual
+        xf.x[j] = fma(alpha, pj, xj);
+        rv = fma(-alpha, qj, rv);
+        xf.r[j] = rv;
+        rr = fma(rv, rv, rr);
+      }
       const double zv = sigma_p * (lam_inv * (rv - sv));
       z[j] = zv;
       rho = fma(rv, zv, rho);
@@ -576,9 +577,15 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
   if (w == 0) {
     const double tot = wave_sum(rho);
     if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = tot;
+    if (fx) {
+      const double tr = wave_sum(rr);
+      if (lane == 0) xf.rr_part[blockIdx.x] = tr;
+    }
   }
   if (blockIdx.x == 0 && rho_part != nullptr)
     for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 64 * NW) rho_part[i] = 0.0;
+  if (blockIdx.x == 0 && fx)
+    for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 64 * NW) xf.rr_part[i] = 0.0;
 }
 
 // waves of k_lr_fin (MLFF_LR_FIN_WAVES = 4 / 8 / 16 for A/B; nanotube, 2 interleaved rounds:
@@ -594,16 +601,16 @@ static int lr_fin_waves() {
 
 static void launch_lr_fin(const double *zpart, int G, int64_t ldp, const double *r, double *z,
                           int64_t n, double sigma_p, double lam_inv, double *rho_part,
-                          const int *status, hipStream_t s, unsigned grid) {
+                          const int *status, hipStream_t s, unsigned grid, XrFold xf = XrFold{}) {
   if (lr_fin_waves() == 16)
     hipLaunchKernelGGL(k_lr_fin<16>, dim3(grid), dim3(1024), 0, s, zpart, G, ldp, r, z, n, sigma_p,
-                       lam_inv, rho_part, status);
+                       lam_inv, rho_part, status, xf);
   else if (lr_fin_waves() == 8)
     hipLaunchKernelGGL(k_lr_fin<8>, dim3(grid), dim3(512), 0, s, zpart, G, ldp, r, z, n, sigma_p,
-                       lam_inv, rho_part, status);
+                       lam_inv, rho_part, status, xf);
   else
     hipLaunchKernelGGL(k_lr_fin<4>, dim3(grid), dim3(256), 0, s, zpart, G, ldp, r, z, n, sigma_p,
-                       lam_inv, rho_part, status);
+                       lam_inv, rho_part, status, xf);
 }
 
 static unsigned lr_fin_grid(int64_t n) {
@@ -904,7 +911,8 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
 
 void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double *r, double *z,
                           int64_t n, double sigma_p, double lam_inv, double *rho_part,
-                          const int *status, hipStream_t s, double *zpart, StopFold fold) {
+                          const int *status, hipStream_t s, double *zpart, StopFold fold,
+                          XrFold xf) {
   const int64_t n2 = ldt / 2;
   const int rpw = lr_rows_per_wg(k), G = lr_rows_groups(k);
   // rows read with default-policy loads stay in the MALL from one iteration to the next:
@@ -914,15 +922,15 @@ void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double 
   if (const char *e = std::getenv("MLFF_LR_CACHE_WGS")) cached = std::atoi(e);
   const dim3 grid((unsigned)G);
   if (n2 <= 4 * kLrThreads)
-    hipLaunchKernelGGL(k_lr_rows<4>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+    hipLaunchKernelGGL(k_lr_rows<4>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
   else if (n2 <= 8 * kLrThreads)
-    hipLaunchKernelGGL(k_lr_rows<8>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+    hipLaunchKernelGGL(k_lr_rows<8>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
   else if (n2 <= 12 * kLrThreads)
-    hipLaunchKernelGGL(k_lr_rows<12>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+    hipLaunchKernelGGL(k_lr_rows<12>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
   else
-    hipLaunchKernelGGL(k_lr_rows<16>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold);
+    hipLaunchKernelGGL(k_lr_rows<16>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
   if (n > 0)
-    launch_lr_fin(zpart, G, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n));
+    launch_lr_fin(zpart, G, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n), xf);
 }
 
 // ---------------------------------------------------------------------------

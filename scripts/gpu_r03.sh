@@ -7,6 +7,7 @@
 #   lrab    interleaved A/B of the low-rank apply form at configs[2] (cluster vs two passes)
 #   pmc     scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes, rbf + nanotube)
 #   prof    rocprofv3 --kernel-trace --stats of the default bench command
+#   preab   k_rec_g first-batch prefetch A/B (nanotube); fpab  fused p update A/B;  ntprof  rocprof stats of the nanotube bench
 # every GPU step runs under its own timeout; the first failure ends the script
 set -u
 export TMPDIR=/tmp
@@ -65,6 +66,19 @@ for s in ${STEPS:-suite smoke bench}; do
           --nproc-per-node $W --master-addr 127.0.0.1 --master-port $((29500 + W)) \
           bench.py --gpus $W --steps 10 --warmup 2 --no-solve
       done ;;
+    preab)  # k_rec_g: Rdd of the first batch issued with the staging loads (default) vs after
+      for r in 1 2; do
+        step preab_on_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step preab_off_$r 300 env MLFF_REC_PRE=0 python bench.py --workload nanotube --no-cpu --no-solve
+      done ;;
+    fpab)  # the CG vector updates folded into the nanotube iteration (default: 4 launches) vs
+           # k_update_xr on its own (5) vs k_update_p and k_update_xr on their own (6), interleaved
+      for r in 1 2; do
+        step fpab_on_$r 300 python bench.py --workload nanotube --no-cpu --no-solve
+        step fpab_xr0_$r 300 env MLFF_FUSE_XR=0 python bench.py --workload nanotube --no-cpu --no-solve
+        step fpab_off_$r 300 env MLFF_FUSE_P=0 python bench.py --workload nanotube --no-cpu --no-solve
+      done ;;
+    ntprof) step ntprof 300 rocprofv3 --kernel-trace --stats -d $O/ntprof -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --no-solve ;;
     tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
