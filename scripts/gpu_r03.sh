@@ -78,6 +78,12 @@ for s in ${STEPS:-suite smoke bench}; do
         step fpab_xr0_$r 300 env MLFF_FUSE_XR=0 python bench.py --workload nanotube --no-cpu --no-solve
         step fpab_off_$r 300 env MLFF_FUSE_P=0 python bench.py --workload nanotube --no-cpu --no-solve
       done ;;
+    lrg)  # one-pass apply workgroups (partial vectors): 256 (default) / 192 / 128, interleaved
+      for r in 1 2; do
+        for g in 256 192 128; do
+          step lrg_${g}_$r 300 env MLFF_LR_GROUPS=$g python bench.py --workload nanotube --no-cpu --no-solve
+        done
+      done ;;
     ntprof) step ntprof 300 rocprofv3 --kernel-trace --stats -d $O/ntprof -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --no-solve ;;
     tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
