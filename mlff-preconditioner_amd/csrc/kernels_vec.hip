@@ -384,19 +384,7 @@ constexpr int kLrThreads = 512;
 constexpr int64_t kLrMaxCols = 16 * 2 * kLrThreads;  // M <= 16 double2 per thread
 
 bool lr_rows_fits(int64_t ldt) { return ldt > 0 && ldt % 2 == 0 && ldt <= kLrMaxCols; }
-// rows per workgroup: ~kLrGroups workgroups (MLFF_LR_GROUPS overrides, A/B)
-static int lr_target_groups() {
-  static const int g = [] {
-    const char *e = std::getenv("MLFF_LR_GROUPS");
-    const int v = e ? std::atoi(e) : 256;
-    return v >= 16 ? v : 256;
-  }();
-  return g;
-}
-int lr_rows_per_wg(int64_t k) {
-  const int g = lr_target_groups();
-  return (int)((k + g - 1) / g);
-}
+int lr_rows_per_wg(int64_t k) { return (int)((k + 255) / 256); }
 int lr_rows_groups(int64_t k) {
   const int rpw = lr_rows_per_wg(k);
   return (int)((k + rpw - 1) / rpw);
