@@ -826,15 +826,6 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   return MLFF_OK;
 }
 
-// MLFF_FUSE_XR=0: k_update_xr as its own launch every iteration (A/B)
-bool xr_fold_enabled() {
-  static const bool on = [] {
-    const char *e = std::getenv("MLFF_FUSE_XR");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return on;
-}
-
 // one PCG iteration (ITER = it), all launches status gated.  fold_in: the stop test of
 // iteration it - 1 runs in this iteration's first kernel (StopFold); stop_out: the stop
 // test of this iteration runs as its own launch (last iteration of a chunk)
@@ -855,7 +846,7 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
   // iteration's apply (x, r, rr partials written by k_lr_fin) and its stop test into the
   // operator's first kernel: 4 launches per iteration instead of 6
   const bool fuse_p = ctx->use_mf && mf_can_fuse_p(ctx);
-  const bool fuse_xr = fuse_p && lowrank && ctx->lr_rows && xr_fold_enabled();
+  const bool fuse_xr = fuse_p && lowrank && ctx->lr_rows && ctx->fuse_xr;
   XrFold xf;
   StopFold fold_op;
   if (fuse_xr && fold_in) {  // iteration it - 1 left its x, r update to this iteration
@@ -1048,6 +1039,11 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (device < 0 || device >= ndev) return set_error(nullptr, MLFF_ERR_ARG, "bad device id");
   mlff_ctx *ctx = new mlff_ctx();
   ctx->device = device;
+  for (auto [name, flag] : {std::pair<const char *, bool *>{"MLFF_FUSE_P", &ctx->fuse_p},
+                            std::pair<const char *, bool *>{"MLFF_FUSE_XR", &ctx->fuse_xr}}) {
+    const char *e = std::getenv(name);
+    *flag = e == nullptr || std::atoi(e) != 0;
+  }
   ctx->rank = rank;
   ctx->world = world;
   ctx->N = n_global;

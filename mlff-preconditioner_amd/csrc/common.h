@@ -330,6 +330,9 @@ struct mlff_ctx {
   int zsplit = 1;         // row splits of the T^T t GEMV
   double *zpart = nullptr;  // zsplit x blk partials
   bool lr_rows = false;        // one-pass low-rank apply (launch_lr_apply_rows), one rank
+  // CG vector updates folded into the matrix-free nanotube iteration; read from
+  // MLFF_FUSE_P / MLFF_FUSE_XR (=0: separate launches) when the context is created
+  bool fuse_p = true, fuse_xr = true;
   bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
   int lr_q = 0;                // its clusters
   double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials

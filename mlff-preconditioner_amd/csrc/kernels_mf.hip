@@ -1126,12 +1126,8 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
 // the fused p update runs in the default record-factored form only: one rank, one identity
 // permutation, <= 16 local points, w in one 16-slot chunk (the nanotube configs[1] system)
 bool mf_can_fuse_p(const mlff_ctx *ctx) {
-  static const bool on = [] {
-    const char *e = std::getenv("MLFF_FUSE_P");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
   const MfData &mf = ctx->mf;
-  return on && ctx->world == 1 && mf.rec && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
+  return ctx->fuse_p && ctx->world == 1 && mf.rec && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
          mf.rec_rg == 8 && round_up(mf.M * mf.n_perms, kRJ) <= 16 && mf.rec_wc16 &&
          ctx->nrows == ctx->N;
 }
