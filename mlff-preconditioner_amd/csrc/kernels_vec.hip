@@ -547,11 +547,11 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
     }
     if (j < n) {
       // batches of 16 partials in flight, the last one predicated (no serial tail)
-      const double *pj = zpart + j;
+      const double *zp = zpart + j;
       for (int g = g0; g < g1; g += 16) {
         double t[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) t[u] = g + u < g1 ? pj[(int64_t)(g + u) * ldp] : 0.0;
+        for (int u = 0; u < 16; ++u) t[u] = g + u < g1 ? zp[(int64_t)(g + u) * ldp] : 0.0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) s += t[u];
       }
