@@ -914,10 +914,10 @@ __global__ __launch_bounds__(256) void k_rec_g(RecArgs a, const double *__restri
 // over the group: every lane of it holds the same bits), so the few rows of a small
 // system still spread over the whole grid.
 // fused search-direction update (k_rec_g FP): the operand rows are p = z + beta p_old,
-// written back to p here (after k_rec_g has read p_old), rho stored in the state
+// written back to p here (after k_rec_g has read p_old), with k_rec_g's rho (st->rho_new)
+// and rho1; rho stored in the state
 struct FinFuse {
   const double *z = nullptr;  // nullptr: not fused
-  const double *rho_part = nullptr;
   DevState *st = nullptr;
   long long it = 0;
   double *p = nullptr;        // = xloc
@@ -1165,7 +1165,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
       ra.st = pf->st;
       ra.it = pf->it;
       ra.sf = pf->sf;
-      ff = FinFuse{pf->z, pf->rho_part, pf->st, pf->it, const_cast<double *>(x_loc)};
+      ff = FinFuse{pf->z, pf->st, pf->it, const_cast<double *>(x_loc)};
     }
     const int64_t nbp = (int64_t)mf.rblk * (mf.rblk + 1) / 2, ngrp = (mf.ni + kRG - 1) / kRG;
     const int64_t nbp8 = (nbp + 7) / 8 * 8, nsw8 = (mf.ni * MP + 31) / 32 * 8;
