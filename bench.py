@@ -615,7 +615,10 @@ def main():
     if storage == "matfree":
         roof_op["note"] = ("two dependent launches (Zt, G = sum w Zt and J^T G of a pair block in one "
                            "workgroup; the finisher): ~33 MB per application at M = 14, latency- "
-                           "not HBM-bound (PMC traffic in profiles/pmc_traffic.json; DESIGN.md 3.2)")
+                           "not HBM-bound (PMC traffic in profiles/pmc_traffic.json; DESIGN.md 3.2); "
+                           "in the one-rank PCG iteration the two launches also form the search "
+                           "direction p = z + beta p and the first one runs the previous "
+                           "iteration's stop test (DESIGN.md 3.7), inside this time")
     # low-rank apply z = sigma_p (r - T^T T r) / lam.  Two-pass form: T (k x N_loc) read
     # twice + r, z (16 k N + 24 N).  One-pass form (one rank, rows in registers): T read once
     # + the row groups' partial vectors written and read (8 k N + 16 G N + 24 N); the
