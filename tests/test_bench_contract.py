@@ -1,6 +1,8 @@
 """bench.py host logic (no GPU): the defaults the driver relies on, the workload / config
 naming, the PMC-traffic lookup and the CPU-core accounting of the baseline."""
+import csv
 import json
+import statistics
 import sys
 
 import pytest
@@ -74,3 +76,27 @@ def test_timing_every_brackets_some_steps():
         for first in range(1, 3 * e + 2):
             hits = sum(1 for it in range(first, first + steps) if it % e == 0)
             assert hits >= min(4, steps), (steps, e, first, hits)
+
+
+def test_pmc_head_medians_optional_kernels(tmp_path):
+    """scripts/pmc_head.py folds the last STEPS dispatches of every kernel of a group; a kernel
+    marked '?' (k_mf_z: launched only where Zt is stored) may be absent."""
+    sys.path.insert(0, str(bench.REPO / "scripts"))
+    import pmc_head
+
+    d = tmp_path / "pass"
+    d.mkdir()
+    names = ["void mlff::(anonymous namespace)::k_rec_g<1, false, 8, 4, 16, true>(RecArgs)",
+             "void mlff::(anonymous namespace)::k_rec_fin<true>(double const*, int)"]
+    with open(d / "x_counter_collection.csv", "w", newline="") as fo:
+        w = csv.writer(fo)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Value"])
+        for i in range(10):
+            w.writerow([2 * i, names[0], 100 + i])
+            w.writerow([2 * i + 1, names[1], 10 + i])
+    m = pmc_head.medians(d, pmc_head.GROUPS["matfree"])
+    assert set(m) == {"k_rec_g", "k_rec_fin"}              # k_mf_z? absent: skipped
+    steps = pmc_head.STEPS
+    assert m["k_rec_g"] == (statistics.median(range(110 - steps, 110)), steps)
+    with pytest.raises(SystemExit):
+        pmc_head.medians(d, ["k_symv_dyn"])                 # a required kernel must be there
