@@ -1856,18 +1856,10 @@ int mlff_pcg_run(mlff_ctx *ctx, int64_t n_iter, int64_t chunk, int *status_out) 
         ctx->timing.iter_count += done_now - ctx->pcg_done;
       }
     }
-    static const bool dbg = std::getenv("MLFF_PCG_DEBUG") != nullptr;
-    if (dbg)
-      std::fprintf(stderr, "pcg chunk [%lld, %lld]: status %d iters %lld resid %.17g atol %.17g\n",
-                   (long long)first, (long long)last, ctx->h_st->status, ctx->h_st->iters,
-                   ctx->h_st->resid, ctx->h_st->atol);
     while (ctx->h_st->status == ST_RECHECK) {
       MLFF_TRY(do_recheck(ctx));
       MLFF_TRY(poll_state(ctx));
       ctx->spec_t = false;  // r was recomputed: the speculative T r is stale
-      if (dbg)
-        std::fprintf(stderr, "  recheck: status %d iters %lld resid %.17g\n", ctx->h_st->status,
-                     ctx->h_st->iters, ctx->h_st->resid);
     }
     ctx->pcg_done = ctx->h_st->iters;
   }

@@ -21,14 +21,12 @@ print(json.dumps({"iters": int(it), "trace": [float(v) for v in info["resid_trac
 
 out = {}
 for v in ("0", "1"):
-    env = dict(os.environ, MLFF_FUSE_XR=v, MLFF_PCG_DEBUG="1")
+    env = dict(os.environ, MLFF_FUSE_XR=v)
     p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True)
     line = [l for l in p.stdout.splitlines() if l.startswith("{")]
     if not line:
         print(p.stdout[-2000:], p.stderr[-3000:])
         sys.exit(1)
-    dbg = [l for l in p.stderr.splitlines() if "pcg chunk" in l or "recheck" in l]
-    print("==", v, "\n" + "\n".join(dbg[-12:]))
     out[v] = json.loads(line[-1])
 a, b = np.array(out["0"]["trace"]), np.array(out["1"]["trace"])
 print("iters", out["0"]["iters"], out["1"]["iters"], "len", a.size, b.size)
