@@ -96,3 +96,53 @@ def test_fused_dropin_recheck_matches(sg, nanotube):
     assert t4.shape == t6.shape
     assert np.max(np.abs(t4 - t6) / np.abs(t6)) <= 1e-12
     assert np.linalg.norm(a4 - a6) <= 1e-12 * np.linalg.norm(a6)
+
+
+def test_fused_dropin_checkpoints(sg, nanotube, monkeypatch):
+    """The drop-in's progress / checkpoint chunking (iterative_solver.py:874-965) on the fused
+    iteration: chunks end on the checkpoint iterations, where the last iteration keeps its own
+    k_update_xr + stop test.  Every checkpoint's alphas are -x_j of an independent solve stopped
+    at j (bit for bit, with its stop-test residual), and the final model equals the one of a
+    solve without callbacks."""
+    from sgdml_amd import model as mdl
+    from sgdml_amd.solvers import iterative_solver as its
+
+    f, (Rd, Rdd) = nanotube
+    M = f["R"].shape[0]
+    task = {"type": "t", "dataset_name": "nanotube", "dataset_theory": "synthetic", "z": f["z"],
+            "R_train": f["R"], "F_train": f["F"], "E_train": f["E"], "idxs_train": np.arange(M),
+            "md5_train": "0", "idxs_valid": np.arange(0), "md5_valid": "0", "sig": 10,
+            "lam": 1e-15, "use_E": True, "use_E_cstr": False, "use_sym": False,
+            "use_cprsn": False, "solver_name": "cg", "solver_tol": 1e-4,
+            "n_inducing_pts_init": 25, "interact_cut_off": None, "perms": f["perms"],
+            "truncated_cholesky": 1500}
+    monkeypatch.setattr(its._CGStatus, "CHECKPOINT_S", 2e-3)
+    monkeypatch.setattr(its._CGStatus, "PROGRESS_S", 5e-4)
+    n = f["y"].size
+    k = int(f["k_rot"])
+    saved = []
+    m = mdl.train(task, save_progr_callback=lambda mod: saved.append(dict(mod)),
+                  callback=lambda *a, **kw: None, break_percentage=k / n,
+                  str_preconditioner="cholesky")
+    m_plain = mdl.train(task, break_percentage=k / n, str_preconditioner="cholesky")
+    np.testing.assert_array_equal(m["alphas_F"], m_plain["alphas_F"])
+    assert m["solver_iters"] == m_plain["solver_iters"]
+    assert len(saved) >= 2, len(saved)
+
+    y = f["F"].ravel().copy()
+    y /= np.std(y)
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, np.atleast_2d(f["perms"]), 10.0)
+        s.set_operator(-1.0, 1e-10)
+        s.precon_pivchol(k)
+        assert s.precon_apply_traffic()[0] == 1  # the rows apply: the fused iteration runs
+        last = 0
+        for mod in saved:
+            j = int(mod["solver_iters"])
+            assert j > last
+            last = j
+            s.pcg_start(y, None, 1e-4, 5 * n)
+            s.pcg_run(j)
+            assert s.pcg_result()[0] == j
+            np.testing.assert_array_equal(mod["alphas_F"], -s.pcg_x())
+            assert mod["solver_resid"] == s.pcg_trace()[j]
