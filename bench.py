@@ -151,6 +151,15 @@ def max_over_ranks(pg, v: float) -> float:
     return float(t.item())
 
 
+def iteration_bytes(op_bytes: float, precon_bytes: float, nloc: int) -> float:
+    """Algorithmic HBM bytes of one PCG iteration on a rank: the operator application in the
+    storage and form that ran, the low-rank apply in the form that ran (its r in / z out
+    included: mlff_precon_apply_traffic), and the other CG vector streams -- rho / p.q / ||r||
+    reads, the p, x and r updates -- 7 N-vectors of 8 bytes (SURVEY 8(d)'s 80 N per iteration
+    counts the apply's r, z streams too)."""
+    return op_bytes + precon_bytes + 56.0 * nloc
+
+
 def make_solver(n, rank, world, local, pg):
     import sgdml_amd
 
@@ -599,7 +608,6 @@ def main():
     gemv_bytes = op_bytes  # algorithmic bytes of this rank's operator launch
     achieved = gemv_bytes / (gemv_ms * 1e-3) / 1e9
     dense_equiv = (8.0 * nloc * n + 16.0 * nloc) / (gemv_ms * 1e-3) / 1e9
-    per_iter_bytes = op_bytes + 16.0 * k * nloc + 80.0 * nloc
     roof_op = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "frac": achieved / HBM_PEAK_GBS,
                "traffic": None,
@@ -643,6 +651,7 @@ def main():
         roof_pre["traffic"], why = pmc_traffic(f"{workload}/precon{one_pass}/{storage}/gpus{world}")
         if why:
             roof_pre["traffic_note"] = why
+    per_iter_bytes = iteration_bytes(op_bytes, pre_bytes if roof_pre is not None else 0.0, nloc)
     # the roofline entry is the kernel group with the larger share of the iteration
     roof_dominant = roof_pre if roof_pre is not None and roof_pre["mean_launch_ms"] > gemv_ms \
         else roof_op

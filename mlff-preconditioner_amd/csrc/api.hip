@@ -957,29 +957,34 @@ int mlff_comm_selftest(int device, int64_t count, double *max_err_out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
     return set_error(nullptr, MLFF_ERR_ARG, "bad device id");
-  mlff_ctx *ctx = new mlff_ctx();
+  // every exit (error returns of the MLFF_HIP checks, exceptions caught by MLFF_API_END)
+  // releases the buffers, the communicator, the stream and the context
+  struct Owned {
+    mlff_ctx *ctx = new mlff_ctx();
+    double *a = nullptr, *b = nullptr;
+    ~Owned() {
+      dev_free(a);
+      dev_free(b);
+      mlff_ctx_destroy(ctx);
+    }
+  } own;
+  mlff_ctx *ctx = own.ctx;
   ctx->device = device;
   ctx->rank = 0;
   ctx->world = 1;
-  double *a = nullptr, *b = nullptr;
-  auto done = [&](int rc) {
-    dev_free(a);
-    dev_free(b);
-    mlff_ctx_destroy(ctx);
-    return rc;
-  };
+  double *&a = own.a, *&b = own.b;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
-    return done(set_error(nullptr, MLFF_ERR_HIP, "stream create failed"));
+    return set_error(nullptr, MLFF_ERR_HIP, "stream create failed");
   ncclUniqueId id;
   ncclResult_t e = ncclGetUniqueId(&id);
   if (e == ncclSuccess) e = ncclCommInitRank(&ctx->comm, 1, id, 0);
   if (e != ncclSuccess) {
     ctx->comm = nullptr;
-    return done(set_error(nullptr, MLFF_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e)));
+    return set_error(nullptr, MLFF_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(e));
   }
   const size_t n = (size_t)count;
   if (hipMalloc(&a, sizeof(double) * n) != hipSuccess || hipMalloc(&b, sizeof(double) * n) != hipSuccess)
-    return done(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
+    return set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed");
   std::vector<double> h(n);
   double worst = 0.0;
   // every collective sits between a producing kernel and a consuming copy on the same stream
@@ -1000,23 +1005,23 @@ int mlff_comm_selftest(int device, int64_t count, double *max_err_out) {
   auto poison = [&](double *p) { return hipMemsetAsync(p, 0xff, sizeof(double) * n, ctx->stream); };
   // allreduce in place
   fill(a, 1.0);
-  if (int rc = rccl_allreduce(ctx, a, n)) return done(rc);
-  if (int rc = check(a, 1.0)) return done(rc);
+  if (int rc = rccl_allreduce(ctx, a, n)) return rc;
+  if (int rc = check(a, 1.0)) return rc;
   // allgather out of place, then in place (send == recv + rank * count)
   fill(a, 2.0);
   MLFF_HIP(ctx, poison(b));
-  if (int rc = rccl_allgather(ctx, a, b, n)) return done(rc);
-  if (int rc = check(b, 2.0)) return done(rc);
+  if (int rc = rccl_allgather(ctx, a, b, n)) return rc;
+  if (int rc = check(b, 2.0)) return rc;
   fill(b, 3.0);
-  if (int rc = rccl_allgather(ctx, b, b, n)) return done(rc);
-  if (int rc = check(b, 3.0)) return done(rc);
+  if (int rc = rccl_allgather(ctx, b, b, n)) return rc;
+  if (int rc = check(b, 3.0)) return rc;
   // reduce-scatter out of place
   fill(b, 4.0);
   MLFF_HIP(ctx, poison(a));
-  if (int rc = rccl_reduce_scatter(ctx, b, a, n)) return done(rc);
-  if (int rc = check(a, 4.0)) return done(rc);
+  if (int rc = rccl_reduce_scatter(ctx, b, a, n)) return rc;
+  if (int rc = check(a, 4.0)) return rc;
   *max_err_out = worst;
-  return done(MLFF_OK);
+  return MLFF_OK;
   MLFF_API_END(nullptr)
 }
 

@@ -929,7 +929,8 @@ __global__ __launch_bounds__(256) void k_rec_fin(const double *__restrict__ uvk,
                                                  const double *__restrict__ rpart, int nblk,
                                                  int64_t MP, int n, int64_t i0, int64_t ni,
                                                  int64_t row0, int64_t nrows, double sigma,
-                                                 double lam, const double *__restrict__ xloc,
+                                                 double lam,
+                                                 const double *xloc,  // = ff.p when fused: no restrict
                                                  double *__restrict__ y,
                                                  double *__restrict__ pq_part, int lg,
                                                  const int *__restrict__ status, FinFuse ff) {

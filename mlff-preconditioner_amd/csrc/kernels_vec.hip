@@ -328,7 +328,8 @@ void launch_colgemv_part(const double *W, int64_t ldw, int64_t k, const double *
 
 // z = sigma_p * (lam_inv * (r - sum_ks part[ks])) over n local entries; rho partials r.z
 __global__ __launch_bounds__(256) void k_precon_fin(const double *__restrict__ part, int ksplit,
-                                                    int64_t ldp, const double *__restrict__ r,
+                                                    int64_t ldp,
+                                                    const double *r,  // = xf.r when fused: no restrict
                                                     double *__restrict__ z, int64_t n,
                                                     double sigma_p, double lam_inv,
                                                     double *__restrict__ rho_part,
@@ -519,7 +520,8 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
 // and writes one slot, the slots past the grid are zero
 template <int NW>  // waves per workgroup, each summing 1/NW of the partials
 __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ zpart, int G,
-                                                    int64_t ldp, const double *__restrict__ r,
+                                                    int64_t ldp,
+                                                    const double *r,  // = xf.r when fused: no restrict
                                                     double *__restrict__ z, int64_t n,
                                                     double sigma_p, double lam_inv,
                                                     double *__restrict__ rho_part,

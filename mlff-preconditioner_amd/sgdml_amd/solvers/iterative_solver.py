@@ -84,16 +84,17 @@ class Iterative(object):
             pass
 
     # ------------------------------------------------------------ helpers
-    def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n, dense):
+    def _kernel_solver(self, task, R_desc, R_d_desc, tril_perms_lin, n, dense, one_device=False):
         """dense: assemble K on the device (the atomic-interactions mask is formed from it);
         otherwise only the matrix-free operator (the reference's K_op) is set up and
         the preconditioner builds fetch their columns through it, as the reference's
-        IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory."""
-        if self.devices is not None:
+        IterativeCholesky does (iterative_cholesky.py:152-156): no N^2 memory.
+        one_device: the solve runs on the first device even when several are configured
+        (the dense flag_eigvals spectra are one-GPU computations)."""
+        if self.devices is not None and not one_device:
             s = ShardedKernelSolver(n, self.devices)
         else:
-            dev = self.device if self.devices is None else self.devices[0]
-            s = KernelSolver(n, device=dev)
+            s = KernelSolver(n, device=self.devices[0] if self.devices is not None else self.device)
         perms = np.atleast_2d(np.asarray(task["perms"]))
         D = R_desc.shape[1]
         if len(tril_perms_lin) != perms.shape[0] * D:
@@ -158,7 +159,7 @@ class Iterative(object):
         dense = str_preconditioner == "eigvec_precon_atomic_interactions"
         self.close()  # the previous solve's contexts (operator tables, panel, communicator)
         solver = self._kernel_solver(task, np.asarray(R_desc), np.asarray(R_d_desc),
-                                     tril_perms_lin, n, dense)
+                                     tril_perms_lin, n, dense, one_device=bool(flag_eigvals))
         self.solver = solver
         start_preconditioner = timeit.default_timer()
         info_cholesky = None
@@ -357,20 +358,28 @@ class _CGStatus:
         return min(cand)
 
     def _replay(self, trace, j0, j1, tt):
-        """Bookkeeping of the calls of iterates j0 + 1 ... j1 (everything except the displays)."""
-        for j in range(j0 + 1, j1 + 1):
-            t = 0.0 if self.calls == 0 else tt
-            self.avg_tt += t
-            old, self.resid = self.resid, float(trace[j])
-            step = 0.0 if self.num_iters == 0 else self.resid - old
-            self.hist.append(step)
-            h = np.asarray(self.hist)
-            tot = np.abs(h).sum()
-            ratio = (-h.clip(max=0).sum() / tot) if tot > 0 else 1
-            self.eff = 0 if self.num_iters == 0 else (int(100 * ratio) - 50) * 2
+        """Bookkeeping of the calls of iterates j0 + 1 ... j1 (everything except the displays),
+        per chunk rather than per call: only the last HIST_LEN steps reach the history and eff
+        is that of the chunk's last call, so the host work between device chunks is O(HIST_LEN)
+        (the per-call wall time is summed call by call, as the reference accumulates it)."""
+        if j1 <= j0:
+            return
+        n_calls = j1 - j0
+        for _ in range(n_calls):
+            self.avg_tt += 0.0 if self.calls == 0 else tt
             self.calls += 1
-            if j < j1:
-                self.num_iters += 1
+        # call of iterate j: num_iters = num_iters(j0 + 1) + (j - j0 - 1); its step is
+        # trace[j] - (previous call's resid), 0 when that num_iters is 0
+        nfirst = self.num_iters
+        for j in range(max(j0 + 1, j1 - self.HIST_LEN + 1), j1 + 1):
+            old = self.resid if j == j0 + 1 else float(trace[j - 1])
+            self.hist.append(0.0 if nfirst + (j - j0 - 1) == 0 else float(trace[j]) - old)
+        self.resid = float(trace[j1])
+        self.num_iters = nfirst + n_calls - 1
+        h = np.asarray(self.hist)
+        tot = np.abs(h).sum()
+        ratio = (-h.clip(max=0).sum() / tot) if tot > 0 else 1
+        self.eff = 0 if self.num_iters == 0 else (int(100 * ratio) - 50) * 2
         # num_iters is now that of the call of iterate j1 (incremented after it by the caller)
 
     def _at_stop(self, solver, j, tt):

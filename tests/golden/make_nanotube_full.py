@@ -1,0 +1,144 @@
+"""configs[1] at its full size, pinned by the CPU oracle (BASELINE.json configs[1]: nanotube
+N = 15540, rank-2701 pivoted-Cholesky PCG to relres 1e-6).
+
+Geometry: sgdml_amd.synthetic.nanotube_like(14, seed=0) (the bench's --workload nanotube; the
+reference's larger_aims_nanotube.npz is an HTTP download absent here), identity permutation,
+sig = 10, lam = 1e-10 (train.py:866), y = F.ravel() / std (train.py:837-845).  Descriptors by
+oracle.sgdml.descriptors on the host (the GPU test passes these same arrays to the device, so
+both sides start from identical bits).
+
+1. pivoted Cholesky (incomplete_cholesky.py:24-93) of the PSD operator -K_op to the rule-of-
+   thumb rank k = 2701 (plot_data.py:1254-1258), get_col = -K_op e_i + lam e_i
+   (iterative_cholesky.py:152-156) on the oracle's matrix-free operator, diagonal = -diag(K)
+   without lam (iterative_cholesky.py:373).  Recorded per step: the pivot, its residual diagonal
+   and the relative gap to the runner-up candidate (pivot sequences are compared up
+   to the first near-tie).
+2. Woodbury panel (iterative_cholesky.py:141-148) and the scipy-1.7.3 CG solve
+   (iterative_solver.py:995-1009) to 1e-6 in three summation orders of the matrix-free operator
+   and the panel apply (make_noise_band.kop_variant: mf, mf_rev, mf_split): the 'mf' solve is the
+   reference trajectory (trace, alpha = -x), the spread of the others its noise band.
+
+Writes tests/golden/nanotube_n15540.npz and nanotube_n15540_band.json.  CPU only, ~20 min on
+8 cores (2701 operator
+applications for the columns); the reference is not imported (its algorithm is the oracle's restatement).
+"""
+from __future__ import annotations
+
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(REPO), str(REPO / "mlff-preconditioner_amd")]
+GOLDEN = REPO / "tests" / "golden"
+sys.path.insert(0, str(GOLDEN))
+
+from make_noise_band import half_decade_crossings, kop_variant, make_gemv  # noqa: E402
+from oracle.pcg import cg_legacy  # noqa: E402
+from oracle.precon import woodbury_panel  # noqa: E402
+from oracle.sgdml import descriptors, kernel_diag  # noqa: E402
+from sgdml_amd import synthetic  # noqa: E402  (input generation only)
+
+M, N_ATOMS, SIG, LAM, TOL, K_RANK = 14, 370, 10.0, 1e-10, 1e-6, 2701
+
+
+def problem():
+    ds = synthetic.nanotube_like(M, seed=0)
+    Rd, Rdd = descriptors(ds["R"])
+    y, _ = synthetic.labels(ds["F"])
+    return ds["R"], Rd, Rdd, np.arange(N_ATOMS)[None, :], y
+
+
+def pivoted_cholesky_logged(get_col, diagonal, max_rank):
+    """oracle.precon.pivoted_cholesky (incomplete_cholesky.py:24-93) with the per-step pivot
+    value and the relative gap between the largest and the second-largest candidate."""
+    diag = np.array(diagonal, dtype=np.float64, copy=True)
+    n = diag.size
+    index_columns = np.arange(n)
+    L = np.zeros((n, max_rank))
+    piv_val = np.empty(max_rank)
+    gap = np.empty(max_rank)
+    t0 = time.time()
+    for m in range(max_rank):
+        cand = diag[index_columns][m:]
+        i_argmax = int(np.argmax(cand) + m)                                  # :53
+        top2 = np.partition(cand, -2)[-2:] if cand.size > 1 else np.array([0.0, cand[0]])
+        gap[m] = (top2[1] - top2[0]) / top2[1]
+        index_columns[m], index_columns[i_argmax] = index_columns[i_argmax], index_columns[m]
+        m_pi = index_columns[m]
+        i_pi = index_columns[m + 1:]
+        pivot_element = diag[m_pi]
+        piv_val[m] = pivot_element
+        assert pivot_element > 0, "given matrix is not PSD"                  # :62
+        L[m_pi, m] = np.sqrt(pivot_element)
+        k = get_col(m_pi)
+        schur = 0
+        if m > 0:
+            schur = L[i_pi, :m] @ L[m_pi, :m]                                # :72
+        L[i_pi, m] = (k[i_pi] - schur) / L[m_pi, m]                           # :75
+        diag[i_pi] -= L[i_pi, m] ** 2                                         # :78
+        if (m + 1) % 250 == 0:
+            print(f"  pivot {m + 1}/{max_rank}  {time.time() - t0:.0f} s", flush=True)
+    return L, index_columns, piv_val, gap
+
+
+def main():
+    t_all = time.time()
+    R, Rd, Rdd, perms, y = problem()
+    n = y.size
+    assert n == 15540
+    mv0 = kop_variant(Rd, Rdd, perms, SIG, "mf")
+
+    def get_col(i):  # (-K_op) e_i (iterative_cholesky.py:152-156)
+        e = np.zeros(n)
+        e[i] = 1.0
+        return -mv0(e) + LAM * e
+
+    diag = -kernel_diag(Rd, Rdd, perms, SIG)
+    L, piv, piv_val, gap = pivoted_cholesky_logged(get_col, diag, K_RANK)
+    print(f"pivoted Cholesky k={K_RANK}: {time.time() - t_all:.0f} s", flush=True)
+    T, sp = woodbury_panel(L, LAM)
+    del L
+    panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}
+    runs = {}
+    for order in ("mf", "mf_rev", "mf_split"):
+        t0 = time.time()
+        mvK = kop_variant(Rd, Rdd, perms, SIG, order)
+        mvT = make_gemv(T, panel_order[order])
+        mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order[order])
+        x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=TOL, maxiter=5 * n,
+                                    psolve=lambda r: sp * ((r - mvTt(mvT(r))) / LAM))
+        runs[order] = (x, info, tr, it)
+        print(f"solve {order:8s} iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
+    x0, info0, tr0, it0 = runs["mf"]
+    top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+    cr0 = half_decade_crossings(tr0[1:], top)
+    variants = {}
+    for order, (x, info, tr, it) in runs.items():
+        cr = half_decade_crossings(tr[1:], top)
+        dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+        variants[order] = {"iters": int(it), "info": int(info), "d_iters": int(it - it0),
+                           "max_d_crossing": int(max(dc) if dc else 0),
+                           "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+    v = variants.values()
+    band = {"n": n, "k": K_RANK, "ref_order": "mf", "ref_iters": int(it0), "variants": variants,
+            "band_iters": int(max(abs(e["d_iters"]) for e in v)),
+            "band_crossing": int(max(e["max_d_crossing"] for e in v)),
+            "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v)),
+            "first_gap_below_1e-12": int(np.argmax(gap < 1e-12)) if np.any(gap < 1e-12) else None,
+            "min_gap": float(gap.min())}
+    np.savez_compressed(GOLDEN / "nanotube_n15540.npz", R=R, y=y, index_columns=piv[:K_RANK],
+                        pivot_values=piv_val, pivot_gap=gap, trace=tr0, iters=np.int64(it0),
+                        info=np.int64(info0), alphas=-x0)
+    (GOLDEN / "nanotube_n15540_band.json").write_text(json.dumps(band, indent=1, sort_keys=True))
+    print(json.dumps({q: band[q] for q in ("ref_iters", "band_iters", "band_crossing",
+                                           "band_rel_dalpha", "first_gap_below_1e-12", "min_gap")}),
+          flush=True)
+    print(f"total {time.time() - t_all:.0f} s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

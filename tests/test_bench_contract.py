@@ -100,3 +100,16 @@ def test_pmc_head_medians_optional_kernels(tmp_path):
     assert m["k_rec_g"] == (statistics.median(range(110 - steps, 110)), steps)
     with pytest.raises(SystemExit):
         pmc_head.medians(d, ["k_symv_dyn"])                 # a required kernel must be there
+
+
+def test_iteration_bytes_use_the_apply_form_that_ran():
+    """iter_gbs_algorithmic counts the low-rank apply's bytes as the library reports them for
+    the form that ran (one pass: T read once), not the two-pass 16 k N: the round-3 nanotube
+    line (k = 2701, one-pass apply 397.6 MB, operator 32.8 MB) is 431.3 MB per iteration, not
+    the 7.59 TB/s-worth two-pass figure."""
+    n, k = 15540, 2701
+    one_pass = 8.0 * k * n + 16.0 * 256 * n + 24.0 * n
+    b = bench.iteration_bytes(32.8e6, one_pass, n)
+    assert b == pytest.approx(32.8e6 + one_pass + 56.0 * n)
+    assert b < 32.8e6 + 16.0 * k * n                   # below the two-pass count
+    assert bench.iteration_bytes(1e9, 0.0, n) == 1e9 + 56.0 * n   # no preconditioner
