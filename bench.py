@@ -58,6 +58,14 @@ REHEARSE = os.environ.get("MLFF_BENCH_REHEARSE", "0") == "1"
 # A100-PCIe 40 GB, data/data/rule_of_thumb/n = 157500) and N ~ 505k (6.600 s on a Quadro RTX
 # 6000, data/data/rule_of_thumb/n = 500000); here M = 14 / 141 / 455 training geometries
 REF_STEP_S = {15540: 0.105, 156510: 2.073, 505050: 6.600}
+# and for ethanol (few atoms, many points): N = 15741 (M = 583, 0.130 s,
+# data/data/cg_performance_n=15750/2022-03-17_2333_ethanol_points583_meas31), N = 74979 (M = 2777,
+# 0.238 s, Quadro RTX 6000, data/data/rule_of_thumb/n = 75000/...ethanol_min2777_max2777) and
+# N = 157491 (M = 5833, 0.550 s, A100-PCIe, data/data/rule_of_thumb/n = 157500/...ethanol_min5833)
+REF_STEP_S_ETHANOL = {15741: 0.130, 74979: 0.238, 157491: 0.550}
+# fp64 vector peak of the MI355X (AMD spec: 78.6 TFLOP/s, half the 157.3 TFLOP/s fp32 vector rate
+# of MI355X_MICROARCH.md's chip table): the bound of the pair-tile sGDML operator
+FP64_VALU_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # timed region: HIP-event brackets on every TIMING_EVERY-th PCG iteration only
 TIMING_EVERY = int(os.environ.get("MLFF_BENCH_TIMING_EVERY", "8"))
@@ -105,9 +113,15 @@ def parse():
                          "this GPU, collectives skipped (per-rank compute of the sharded "
                          "iteration; not a bench line)")
     ap.add_argument("--solo-rank", type=int, default=0)
-    ap.add_argument("--storage", choices=["auto", "sym", "dense"], default="auto",
+    ap.add_argument("--storage", choices=["auto", "sym", "dense", "matfree"], default="auto",
                     help="operator storage: symmetric 512x512 tiles of the lower block "
-                         "triangle (auto/sym, ~4 N^2 bytes) or dense rows (8 N^2 bytes)")
+                         "triangle (auto/sym, ~4 N^2 bytes), dense rows (8 N^2 bytes) or the "
+                         "matrix-free sGDML operator; for the sGDML workloads sym / dense "
+                         "assemble K on the GPU first (its time in setup_s)")
+    ap.add_argument("--mf-form", choices=["pt", "rec", "pair"], default=None,
+                    help="matrix-free sGDML operator form (MLFF_MF_FORM): pair-tile (few atoms), "
+                         "record-factored (many atoms) or pair sums; default: the library's "
+                         "choice")
     return ap.parse_args()
 
 
@@ -283,6 +297,12 @@ def cpu_baseline_sgdml(solver, Rd, Rdd, perms, b, lam, iters):
 
     psolve = lambda r: apply_panel(T, 1.0, lam, r)  # noqa: E731
     with threadpoolctl.threadpool_limits(limits=cpus["cores"], user_api="blas"):
+        # a bounded sample (~10 s per timed run): the many-point operator is O(M^2) on the host
+        t0 = time.perf_counter()
+        mv(b)
+        psolve(b)
+        one = time.perf_counter() - t0
+        iters = max(1, min(iters, int(10.0 / max(one, 1e-6))))
         per_it, spread = _median_rate(lambda: _time_pcg(mv, psolve, b, iters)[0])
         t_mv = _time_pcg(mv, psolve, b, 1)[1]
     return dict({"value": 1.0 / per_it, "unit": "CG iters/s", "cores": cpus["cores"], "kind": "port",
@@ -401,17 +421,24 @@ def sgdml_workload(args, rank, world, local, pg):
     m, kmin, _ = get_params(name)
     k = args.k if args.k else int(rule_of_thumb(n=n, k_min=kmin, m=m))
     y, _ = synthetic.labels(ds["F"])
+    if args.mf_form:
+        os.environ["MLFF_MF_FORM"] = args.mf_form
     t0 = time.perf_counter()
     Rd, Rdd = sgdml_amd.sgdml_descriptors(ds["R"])
     solver = make_solver(n, rank, world, local, pg)
-    # as the drop-in Iterative.solve: the matrix-free operator only (the reference's
-    # K_op); the pivoted Cholesky fetches its columns through it (no N^2 assembly)
-    solver.sgdml_operator(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
+    if args.storage in ("sym", "dense"):
+        # the stored-K forms of the same operator: K assembled on the GPU (train.py:1121-1308)
+        solver.assemble_sgdml(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
+    else:
+        # as the drop-in Iterative.solve: the matrix-free operator only (the reference's
+        # K_op); the pivoted Cholesky fetches its columns through it (no N^2 assembly)
+        solver.sgdml_operator(Rd, Rdd, np.arange(n_atoms)[None, :], 10.0)
     solver.set_operator(-1.0, 1e-10)
     solver.synchronize()
     t_asm = time.perf_counter() - t0
     _, t_chol = solver.precon_pivchol(k)
     return solver, n, k, y, {"operator_setup_s": t_asm, "pivchol_build_s": t_chol,
+                             "assembled": args.storage in ("sym", "dense"),
                              "workload": f"sgdml_{name}_n{n}_pivchol{k}", "M": M,
                              "n_atoms": n_atoms, "desc": (Rd, Rdd),
                              "perms": np.arange(n_atoms)[None, :]}
@@ -620,7 +647,23 @@ def main():
     roof_op["traffic"], why = pmc_traffic(f"{workload}/{storage}/gpus{world}")
     if why:
         roof_op["traffic_note"] = why
-    if storage == "matfree":
+    mf_form = solver.operator_form() if storage == "matfree" else None
+    if mf_form == "pt":
+        # the pair-tile operator is bound by the fp64 vector pipe: 9 D + 8 flops per (query
+        # point, training point, permutation) -- diff (D), |diff|^2 and diff . Zt (2 x 2D),
+        # F += c diff - w Zt (4D), nrm / m / w / c (8; sqrt and exp counted as one each)
+        M_, D_ = sg_info["M"], sg_info["n_atoms"] * (sg_info["n_atoms"] - 1) // 2
+        ni_ = -(-nloc // (3 * sg_info["n_atoms"]))
+        flops = ni_ * M_ * sg_info["perms"].shape[0] * (9.0 * D_ + 8.0)
+        tf = flops / (gemv_ms * 1e-3) / 1e12
+        roof_op = dict(roof_op, bound="valu_fp64", achieved=tf, peak=FP64_VALU_PEAK_TFLOPS,
+                       unit="TFLOP/s", frac=tf / FP64_VALU_PEAK_TFLOPS,
+                       kernel="k_mf_z + k_pt_pair + k_pt_fin (pair-tile matrix-free sGDML operator)",
+                       flops_per_launch=flops, hbm_gbs_algorithmic=achieved,
+                       note="query points in registers, training points streamed through LDS; "
+                            "bound by the fp64 vector pipe (78.6 TFLOP/s AMD spec), not by its "
+                            "bytes (DESIGN.md 3.8)")
+    elif storage == "matfree":
         roof_op["note"] = ("two dependent launches (Zt, G = sum w Zt and J^T G of a pair block in one "
                            "workgroup; the finisher): ~33 MB per application at M = 14, latency- "
                            "not HBM-bound (PMC traffic in profiles/pmc_traffic.json; DESIGN.md 3.2); "
@@ -704,7 +747,9 @@ def main():
             # BASELINE.md publishes a CG step time only for the nanotube (0.105 s/step at
             # N = 15540, data/data/cg_performance_n=15750/..._nanotube_points14_meas31)
             "vs_baseline": (args.steps / el) / (1.0 / REF_STEP_S[n])
-            if args.workload == "nanotube" and n in REF_STEP_S else None,
+            if args.workload == "nanotube" and n in REF_STEP_S else
+            (args.steps / el) / (1.0 / REF_STEP_S_ETHANOL[n])
+            if args.workload == "ethanol" and n in REF_STEP_S_ETHANOL else None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": workload,
@@ -719,6 +764,7 @@ def main():
                        if sg_info is None else
                        "cholesky (pivoted Cholesky + Woodbury, iterative_cholesky.py:115-150)",
                        "storage": storage,
+                       **({"operator_form": mf_form} if mf_form else {}),
                        "parallelism": f"row-shard x{world} (RCCL allgather/allreduce"
                        + ("/reduce-scatter)" if storage == "sym" else ")")},
             "roofline": roof_dominant,
@@ -736,7 +782,8 @@ def main():
             "solve_to_1e-6": solve,
             "parity_n8192": par,
             "setup_s": dict({"gen_rbf": t_gen, "nystrom_build": t_pre} if sg_info is None else
-                            {"descriptors_and_operator": t_gen, "pivoted_cholesky_build": t_pre},
+                            {("descriptors_and_assembly" if sg_info["assembled"] else
+                              "descriptors_and_operator"): t_gen, "pivoted_cholesky_build": t_pre},
                             storage_pack=t_pack),
         }
     solver.close()

@@ -235,6 +235,17 @@ int mlff_set_storage(mlff_ctx *ctx, int mode);
 /* resolves the storage (building the tiles if needed) and reports the mode in
  * use and the algorithmic HBM bytes of one operator application on this rank */
 int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out);
+/* form of the matrix-free sGDML operator (MLFF_STORAGE_MATFREE; the reference's K_op,
+ * iterative_solver.py:383-445 / predict.py:172-220, evaluated three ways):
+ * MLFF_MF_FORM_PAIR (pair sums, then F, then J^T), MLFF_MF_FORM_REC (record-factored: x-independent
+ * per-pair records, many-atom / few-point systems such as the nanotube), MLFF_MF_FORM_PTILE
+ * (pair-tile: query points in registers, training points streamed through LDS, fp64-vector
+ * bound; few-atom / many-point systems such as ethanol).  -1 when no sGDML operator is set.
+ * Environment MLFF_MF_FORM=pair|rec|pt (read by mlff_sgdml_operator) overrides the default. */
+#define MLFF_MF_FORM_PAIR 0
+#define MLFF_MF_FORM_REC 1
+#define MLFF_MF_FORM_PTILE 2
+int mlff_operator_form(mlff_ctx *ctx, int *form_out);
 /* diag(sigma_K * K) (local) */
 int mlff_get_diag(mlff_ctx *ctx, double *diag_local);
 

@@ -1427,6 +1427,15 @@ int mlff_set_storage(mlff_ctx *ctx, int mode) {
   MLFF_API_END(ctx)
 }
 
+int mlff_operator_form(mlff_ctx *ctx, int *form_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (form_out == nullptr) return set_error(ctx, MLFF_ERR_ARG, "null form_out");
+  *form_out = ctx->mf.ready ? mf_form(ctx) : -1;
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
 int mlff_storage_info(mlff_ctx *ctx, int *mode_out, double *bytes_per_matvec_out) {
   MLFF_API_BEGIN
   MLFF_ENTER(ctx);

@@ -106,6 +106,12 @@ struct MfData {
   int rblk = 0;
   int64_t ldw = 0;
   double *wt = nullptr, *sv = nullptr, *rpart = nullptr;
+  // pair-tile form (kernels_pt.hip k_pt_pair / k_pt_fin; few atoms, D <= 288): in use when
+  // ptile is set (the default where it exists; MLFF_MF_FORM=rec|pair|pt overrides); pt_S chunks
+  // of the (j, p) range, ptpart = pt_S x ni x (padded D) partial F
+  bool ptile = false;
+  int pt_S = 1;
+  double *ptpart = nullptr;
   // energy constraints (use_E_cstr, train.py:212-236; iterative_solver.py:423-440): the
   // operand and result carry M energy entries after the nF = 3 n M force entries (one rank)
   bool E = false;
@@ -639,6 +645,18 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                         const double *x_loc, const int *status, double sigma, double lam,
                         double *pq_part = nullptr, const PFuse *pf = nullptr);
 int mf_diag(mlff_ctx *ctx, double *out);
+// Zt = (J_j x_j)[P_p] of every (j, p) (k_mf_z), status gated
+void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s);
+// pair-tile form (kernels_pt.hip): available for D <= 288; its (j, p) chunks, padded D and the
+// operator y_loc = sigma K x + lam x_loc (+ the x_loc . y_loc partials when pq_part is set)
+bool pt_supported(int64_t D);
+int pt_chunks(int64_t D, int64_t ni, int64_t MP);
+int64_t pt_padded_d(int64_t D);
+void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, int64_t row0,
+                        int64_t nrows, const double *x_loc, double *y_loc, const int *status,
+                        double sigma, double lam, double *pq_part, hipStream_t s);
+// operator form in use: 0 pair sums (k_mf_pair ...), 1 record-factored, 2 pair-tile
+int mf_form(const mlff_ctx *ctx);
 // sigma K_op columns through the single-column path (mf.uvk); false when it is not set up
 bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double sigma,
                 double *out, int64_t ldo);

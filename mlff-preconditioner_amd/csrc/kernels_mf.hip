@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 namespace mlff {
 
@@ -1109,6 +1110,18 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
       mf.rec_wc16 = e4 == nullptr || std::atoi(e4) != 0;
     }
   }
+  // operator form: the pair-tile one where it exists (few atoms), else the record-factored one
+  // where the records fit, else the pair sums; MLFF_MF_FORM=pt|rec|pair asks for one (A/B, tests)
+  {
+    const char *ef = std::getenv("MLFF_MF_FORM");
+    const std::string form = ef != nullptr ? ef : "";
+    if (form == "pair") mf.rec = false;
+    if ((form.empty() || form == "pt") && !E && mf.ni > 0 && pt_supported(D)) {
+      mf.ptile = true;
+      mf.pt_S = pt_chunks(D, mf.ni, MP);
+      MLFF_HIP(ctx, hipMalloc(&mf.ptpart, sizeof(double) * mf.pt_S * mf.ni * pt_padded_d(D)));
+    }
+  }
   if (mf.ni > 0) {
     hipLaunchKernelGGL(k_mf_pair<0>, dim3((unsigned)((MP + kPT - 1) / kPT),
                        (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)nz), dim3(256), 0,
@@ -1128,7 +1141,7 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
 // permutation, <= 16 local points, w in one 16-slot chunk (the nanotube configs[1] system)
 bool mf_can_fuse_p(const mlff_ctx *ctx) {
   const MfData &mf = ctx->mf;
-  return ctx->fuse_p && ctx->world == 1 && mf.rec && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
+  return ctx->fuse_p && ctx->world == 1 && mf.rec && !mf.ptile && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
          mf.rec_rg == 8 && round_up(mf.M * mf.n_perms, kRJ) <= 16 && mf.rec_wc16 &&
          ctx->nrows == ctx->N;
 }
@@ -1151,6 +1164,11 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     if (pq_part != nullptr)  // zero partials of an empty shard
       hipLaunchKernelGGL(k_mf_jt_fin<true>, dim3(kVecGrid), dim3(256), 0, s, mf.ypart, js,
                          (int64_t)0, sigma, lam, x_loc, y_loc, pq_part, status);
+    return;
+  }
+  if (mf.ptile) {
+    launch_pt_operator(mf, mf.ident ? mf.Rd : mf.Rt, xc, ctx->row0, ctx->nrows, x_loc, y_loc, status,
+                       sigma, lam, pq_part, s);
     return;
   }
 #ifdef MLFF_REC_TRACE
@@ -1336,9 +1354,27 @@ bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double 
   return true;
 }
 
+void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s) {
+  const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
+                     mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt, mf.ps, mf.pt,
+                     mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
+}
+
+int mf_form(const mlff_ctx *ctx) { return ctx->mf.ptile ? 2 : ctx->mf.rec ? 1 : 0; }
+
 double mf_bytes(const mlff_ctx *ctx) {
   const MfData &mf = ctx->mf;
   const double MP = (double)(mf.M * mf.n_perms), D = (double)mf.D;
+  if (mf.ptile) {
+    // Zt formed from Rdd and x and written; Rt, Zt read (once: the point blocks re-read them
+    // from L2); the local points' Rd and Rdd rows; the chunk partials written and read; the
+    // operand, the rows and the result.  The kernel is bound by the fp64 vector pipe, not by
+    // these bytes
+    const double ni = (double)mf.ni, DP = (double)pt_padded_d(mf.D);
+    return 8.0 * (3.0 * (double)mf.M * D + 3.0 * MP * D + 4.0 * ni * D +
+                  2.0 * mf.pt_S * ni * DP + (double)ctx->N + 2.0 * ctx->nrows);
+  }
   if (mf.rec) {
     // Rdd of every point once per point group (Zt on the fly; the query points' own rows
     // are the same lines), the u and v halves of the records, the slot partials written
@@ -1362,7 +1398,8 @@ void mf_free(MfData &mf) {
                   (void *)mf.ps, (void *)mf.pt, (void *)mf.m5, (void *)mf.w, (void *)mf.c,
                   (void *)mf.F, (void *)mf.part, (void *)mf.ypart, (void *)mf.xc,
                   (void *)mf.uvk, (void *)mf.pi_d, (void *)mf.piinv_d, (void *)mf.kee,
-                  (void *)mf.eterm, (void *)mf.wt, (void *)mf.sv, (void *)mf.rpart})
+                  (void *)mf.eterm, (void *)mf.wt, (void *)mf.sv, (void *)mf.rpart,
+                  (void *)mf.ptpart})
     if (p) (void)hipFree(p);
   mf = MfData();
 }

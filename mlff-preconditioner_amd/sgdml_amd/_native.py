@@ -72,6 +72,7 @@ SIGNATURES = {
     "mlff_get_diag": (_int, [_c_ctx, _p_dbl]),
     "mlff_set_storage": (_int, [_c_ctx, _int]),
     "mlff_storage_info": (_int, [_c_ctx, _p_int, _p_dbl]),
+    "mlff_operator_form": (_int, [_c_ctx, _p_int]),
     "mlff_precon_none": (_int, [_c_ctx]),
     "mlff_precon_pivchol": (_int, [_c_ctx, _i64, _int, _p_i64, _p_dbl]),
     "mlff_precon_nystrom": (_int, [_c_ctx, _p_i64, _i64, _int, _p_dbl]),

@@ -157,6 +157,9 @@ class ShardedKernelSolver:
         out = self._each("storage_info")
         return out[0][0], float(sum(b for _, b in out))
 
+    def operator_form(self):
+        return self._each("operator_form")[0]
+
     def precon_none(self):
         self._each("precon_none")
 

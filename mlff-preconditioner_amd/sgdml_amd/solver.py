@@ -189,6 +189,13 @@ class KernelSolver:
                                                                                 "dense")
         return name, nbytes.value
 
+    def operator_form(self) -> str | None:
+        """Form of the matrix-free sGDML operator: 'pair', 'rec' (record-factored, many atoms /
+        few points) or 'pt' (pair-tile, few atoms / many points); None without one."""
+        f = ctypes.c_int()
+        self._call("mlff_operator_form", ctypes.byref(f))
+        return {0: "pair", 1: "rec", 2: "pt"}.get(f.value)
+
     def matvec(self, v: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(v, dtype=np.float64)
         if v.shape != (self.n,):

@@ -78,8 +78,21 @@ void rbf_tiles_cols(const double *tiles, int64_t n, const int64_t *idx, int64_t 
   }
 }
 
-/* y = K v (N entries); scratch: nthreads * nb * TB doubles (or NULL: allocated here) */
+static void symv_impl(const double *tiles, int64_t n, const double *v, double *y, int reverse);
+
+/* y = K v (N entries) */
 void rbf_tiles_symv(const double *tiles, int64_t n, const double *v, double *y) {
+  symv_impl(tiles, n, v, y, 0);
+}
+
+/* the same mat-vec in another summation order: tiles visited last to first (every thread's
+ * private vector accumulates its share in reverse), rows of a tile last to first, and the
+ * private vectors added in reverse thread order (a second oracle sample of the N = 65536 solve) */
+void rbf_tiles_symv_rev(const double *tiles, int64_t n, const double *v, double *y) {
+  symv_impl(tiles, n, v, y, 1);
+}
+
+static void symv_impl(const double *tiles, int64_t n, const double *v, double *y, int reverse) {
   const int64_t nb = (n + TB - 1) / TB;
   const int64_t np = nb * TB;
   const int64_t nt = ntiles_of(n);
@@ -92,7 +105,8 @@ void rbf_tiles_symv(const double *tiles, int64_t n, const double *v, double *y) 
     const int th = omp_get_thread_num();
     double *ya = acc + (int64_t)th * np;
 #pragma omp for schedule(static)
-    for (int64_t t = 0; t < nt; ++t) {
+    for (int64_t tt = 0; tt < nt; ++tt) {
+      const int64_t t = reverse ? nt - 1 - tt : tt;
       /* tile index -> (I, J) */
       int64_t I = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) / 2.0);
       while (I * (I + 1) / 2 > t) --I;
@@ -101,7 +115,8 @@ void rbf_tiles_symv(const double *tiles, int64_t n, const double *v, double *y) 
       const double *A = tiles + t * (int64_t)TB * TB;
       const double *vj = vp + J * TB, *vi = vp + I * TB;
       double *yi = ya + I * TB, *yj = ya + J * TB;
-      for (int64_t r = 0; r < TB; ++r) {
+      for (int64_t rr = 0; rr < TB; ++rr) {
+        const int64_t r = reverse ? TB - 1 - rr : rr;
         const double *row = A + r * TB;
         double s = 0.0;
         for (int64_t c = 0; c < TB; ++c) s += row[c] * vj[c];
@@ -115,7 +130,7 @@ void rbf_tiles_symv(const double *tiles, int64_t n, const double *v, double *y) 
   }
   for (int64_t i = 0; i < n; ++i) {
     double s = 0.0;
-    for (int th = 0; th < nth; ++th) s += acc[(int64_t)th * np + i];
+    for (int k = 0; k < nth; ++k) s += acc[(int64_t)(reverse ? nth - 1 - k : k) * np + i];
     y[i] = s;
   }
   free(acc);

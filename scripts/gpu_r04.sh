@@ -1,0 +1,56 @@
+#!/bin/bash
+# Round-4 GPU session: STEPS (space separated) from
+#   suite   driver-exact `pytest -m gpu` (per-test timeout, progress log)
+#   smoke   __graft_entry__.smoke()
+#   bench   default bench line (python bench.py)
+#   nt      nanotube bench line (configs[1])
+#   tests   pytest of $TESTS (-v -s)
+#   ptvar   pair-tile variants on the ethanol shape (M = 583 / 2777): MLFF_PT_VARIANT sweep
+#   eth     ethanol bench lines at the reference's published sizes (M = 583 / 2777 / 5833) with
+#           the pair-tile operator, the record-factored one and (M <= 2777) stored K
+#   ptprof  rocprofv3 --kernel-trace --stats of the ethanol M = 5833 bench
+#   prof    rocprofv3 --kernel-trace --stats of the default bench command
+#   pmc     scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes)
+# every GPU step runs under its own timeout; the first failure ends the script
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r04
+mkdir -p $O
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name $(date +%T)" | tee -a $O/steps.log
+  timeout -k 10 $lim "$@" > $O/$name.txt 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)" | tee -a $O/steps.log
+  if [ $rc -ne 0 ]; then tail -30 $O/$name.txt; exit $rc; fi
+}
+EB="python bench.py --workload ethanol --no-cpu --no-solve --steps 30 --warmup 3"
+for s in ${STEPS:-suite smoke bench}; do
+  case $s in
+    suite) step suite 1100 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread ${PYTEST_EXTRA:-} ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench_default 600 python bench.py ;;
+    nt) step bench_nanotube 300 python bench.py --workload nanotube ;;
+    tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
+    ptvar)
+      for m in 583 2777 5833; do
+        for v in ${PTV:-0 5 6 7 8 9}; do
+          step ptvar_m${m}_v$v 300 env MLFF_PT_VARIANT=$v $EB --m $m --storage matfree --mf-form pt
+        done
+      done
+      step ptvar_prof 600 rocprofv3 --kernel-trace --stats -d $O/ptvar_prof -o eth --output-format csv -- python3 bench.py --workload ethanol --no-cpu --no-solve --steps 30 --warmup 3 --m 2777 --storage matfree ;;
+    eth)
+      for m in 583 2777 5833; do
+        step eth_m${m}_pt 600 $EB --m $m --storage matfree --mf-form pt
+      done
+      for m in 583 2777; do
+        step eth_m${m}_rec 600 $EB --m $m --storage matfree --mf-form rec
+        step eth_m${m}_sym 600 $EB --m $m --storage sym
+        step eth_m${m}_dense 600 $EB --m $m --storage dense
+      done ;;
+    ptprof) step ptprof 600 rocprofv3 --kernel-trace --stats -d $O/ptprof -o eth --output-format csv -- python3 bench.py --workload ethanol --m 5833 --no-cpu --no-solve --steps 30 --warmup 3 --storage matfree ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
+    pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
+  esac
+done
+echo "== all done $(date +%T)" | tee -a $O/steps.log

@@ -18,9 +18,11 @@ RBF with length scale 0.2 (the reference's generator, src/tools/utils.py:173-187
              GPU's storage) with the panel in 512-column tiles
    The spread against the blas solve is the band (iterations, half-decade crossings of the
    running-minimum residual, ||dx|| / ||x||) -> rbf_band_n8192.npz / .json.
-2. N = 65536 (`--full`, ~2-3 h on 8 cores, 17.3 GB of RAM): ONE oracle solve with the tiled
+2. N = 65536 (`--full`, ~2-3 h on 8 cores, 17.3 GB of RAM): the oracle solve with the tiled
    mat-vec (a dense 34.4 GB NumPy K does not fit next to the rest) -> rbf_solve_n65536.npz:
-   iterations, final relres, trace, x.  The GPU solve of the same system is held to the
+   iterations, final relres, trace, x; `--full --order tiles_rev`: the same solve in a second
+   summation order (tiles, tile rows and thread partials reversed, panel columns reversed) ->
+   rbf_solve_n65536_rev.npz.  The GPU solve of the same system is held to the
    N = 8192 band scaled by the iteration count (tests/test_gpu_rbf_band.py).
 
 CPU only; the reference is not imported (its RBF generator is sklearn's formula, restated in
@@ -67,6 +69,7 @@ def tiles_lib():
     lib.rbf_tiles_gen.argtypes = [P, I64, ctypes.c_int, P]
     lib.rbf_tiles_cols.argtypes = [P, I64, ctypes.POINTER(I64), I64, P]
     lib.rbf_tiles_symv.argtypes = [P, I64, P, P]
+    lib.rbf_tiles_symv_rev.argtypes = [P, I64, P, P]
     return lib
 
 
@@ -82,10 +85,11 @@ class Tiles:
         self.t = np.empty(int(self.lib.rbf_tiles_count(self.n)) * 512 * 512)
         self.lib.rbf_tiles_gen(_p(Xs), self.n, Xs.shape[1], _p(self.t))
 
-    def matvec(self, v):
+    def matvec(self, v, reverse=False):
         v = np.ascontiguousarray(v, dtype=np.float64)
         y = np.empty(self.n)
-        self.lib.rbf_tiles_symv(_p(self.t), self.n, _p(v), _p(y))
+        (self.lib.rbf_tiles_symv_rev if reverse else self.lib.rbf_tiles_symv)(
+            _p(self.t), self.n, _p(v), _p(y))
         return y
 
     def cols(self, idx):
@@ -137,13 +141,17 @@ def band(n=8192):
            "band_crossing": int(max(e["max_d_crossing"] for e in v)),
            "band_rel_dx": float(max(e["rel_dx"] for e in v))}
     np.savez_compressed(GOLDEN / f"rbf_band_n{n}.npz", x=x0, trace=tr0, iters=np.int64(it0),
-                        idx=idx, tiles_x=runs["tiles"][0], tiles_trace=runs["tiles"][2])
+                        idx=idx, tiles_x=runs["tiles"][0], tiles_trace=runs["tiles"][2],
+                        **{f"trace_{o}": r[2] for o, r in runs.items()})
     (GOLDEN / f"rbf_band_n{n}.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps({k: out[k] for k in ("ref_iters", "band_iters", "band_crossing",
                                           "band_rel_dx")}), flush=True)
 
 
-def full(n=65536):
+def full(n=65536, order="tiles"):
+    """order: 'tiles' (rbf_tiles_symv, the committed rbf_solve_n65536.npz) or 'tiles_rev'
+    (rbf_tiles_symv_rev with the panel apply in reversed column order: a second sample of the
+    oracle's solve, rbf_solve_n65536_rev.npz)."""
     X, b, idx = problem(n)
     t0 = time.time()
     tiles = Tiles(X, ELL)
@@ -161,12 +169,19 @@ def full(n=65536):
             print(f"  iteration {state['it']}  {el:.0f} s ({el / state['it']:.2f} s/it)",
                   flush=True)
 
-    x, info, tr, it = cg_legacy(lambda v: tiles.matvec(v) + LAM * v, b, tol=TOL,
-                                maxiter=20000, psolve=lambda r: apply_panel(B, sp, LAM, r),
-                                callback=cb)
+    rev = order == "tiles_rev"
+    if rev:
+        mvT = make_gemv(B, "rev")
+        mvTt = make_gemv(np.ascontiguousarray(B.T), "rev")
+        psolve = lambda r: sp * ((r - mvTt(mvT(r))) / LAM)  # noqa: E731
+    else:
+        psolve = lambda r: apply_panel(B, sp, LAM, r)  # noqa: E731
+    x, info, tr, it = cg_legacy(lambda v: tiles.matvec(v, reverse=rev) + LAM * v, b, tol=TOL,
+                                maxiter=20000, psolve=psolve, callback=cb)
     el = time.time() - t0
     relres = float(np.linalg.norm(b - (tiles.matvec(x) + LAM * x)) / np.linalg.norm(b))
-    np.savez_compressed(GOLDEN / f"rbf_solve_n{n}.npz", x=x, trace=tr, iters=np.int64(it),
+    np.savez_compressed(GOLDEN / f"rbf_solve_n{n}{'_rev' if rev else ''}.npz", x=x, trace=tr,
+                        iters=np.int64(it),
                         info=np.int64(info), idx=idx, final_relres=relres,
                         x_norm=np.linalg.norm(x), seconds=el)
     print(json.dumps({"n": n, "iters": int(it), "info": int(info), "final_true_relres": relres,
@@ -178,8 +193,9 @@ if __name__ == "__main__":
     ap.add_argument("--band", action="store_true")
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--order", choices=["tiles", "tiles_rev"], default="tiles")
     a = ap.parse_args()
     if a.band:
         band(a.n or 8192)
     if a.full:
-        full(a.n or 65536)
+        full(a.n or 65536, a.order)

@@ -187,3 +187,48 @@ def test_nanotube_cluster_apply_solve(sg, monkeypatch):
     Ax = -kernel_matvec_matrix_free(Rd, Rdd, perms, SIG, r1.x) + LAM * r1.x
     relres = np.linalg.norm(y - Ax) / np.linalg.norm(y)
     assert relres <= 1.05e-6, relres
+
+
+@pytest.mark.timeout(900)
+def test_config1_full_size_against_oracle_fixture(sg, golden_dir):
+    """configs[1] at its full size against the CPU oracle's own run of it
+    (tests/golden/make_nanotube_full.py -> nanotube_n15540.npz / _band.json): the rank-2701
+    pivoted Cholesky on the matrix-free operator (incomplete_cholesky.py:24-93 with get_col =
+    -K_op e_i, iterative_cholesky.py:152-156) and the PCG solve to 1e-6 (iterative_solver.py:
+    995-1009).  Both sides start from the same descriptors (oracle.sgdml.descriptors of the
+    fixture's geometry).
+    * pivots: identical up to the first near-tie of the oracle's residual diagonal (SURVEY 8(c):
+      relative gap between the best two candidates < 1e-12); every pivot when there is none;
+    * solve: iterations, residual trace and alpha under the tests/parity.py band rule with the
+      band the oracle measured on this system (three summation orders of its operator)."""
+    import json
+
+    from oracle.sgdml import descriptors
+    from tests.parity import assert_pcg_parity
+
+    path = golden_dir / "nanotube_n15540.npz"
+    if not path.exists():
+        pytest.fail("tests/golden/nanotube_n15540.npz missing (make_nanotube_full.py)")
+    f = np.load(path, allow_pickle=False)
+    band = json.loads((golden_dir / "nanotube_n15540_band.json").read_text())
+    Rd, Rdd = descriptors(f["R"])
+    y = f["y"]
+    n, k = y.size, int(band["k"])
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, np.arange(N_ATOMS)[None, :], SIG)
+        s.set_operator(-1.0, LAM)
+        piv, _ = s.precon_pivchol(k)
+        res = s.pcg(y, tol=1e-6, maxiter=5 * n)
+    ref_piv, gap = f["index_columns"], f["pivot_gap"]
+    diff = np.nonzero(piv[:k] != ref_piv[:k])[0]
+    first_tie = np.nonzero(gap < 1e-12)[0]
+    limit = int(first_tie[0]) if first_tie.size else k
+    print(f"configs[1] pivots: first difference at {diff[0] if diff.size else None}, "
+          f"first oracle near-tie at {limit if first_tie.size else None} of {k}")
+    assert diff.size == 0 or diff[0] >= limit, (diff[:5], limit)
+    assert res.info == 0 and int(f["info"]) == 0
+    print(f"configs[1] solve: GPU {res.iters} vs oracle {int(f['iters'])} iterations "
+          f"(band {band['band_iters']}, oracle orders "
+          f"{ {o: v['iters'] for o, v in band['variants'].items()} })")
+    assert_pcg_parity(res.iters, res.trace[1:], -res.x, int(f["iters"]), f["trace"][1:],
+                      f["alphas"], band=band)

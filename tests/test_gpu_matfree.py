@@ -262,8 +262,9 @@ def test_matfree_ragged_shards(sg, golden_dir, m, world):
                                   "ethanol_m40"])
 def test_record_factored_operator_matches_pair_path(sg, golden_dir, name, monkeypatch):
     """The record-factored operator (k_rec_g + k_rec_fin: y = sum c u - J^T G from the
-    pair records, the default when they fit) against the five-kernel pair / F / J^T path
-    (MLFF_MF_REC=0) on the same operand, one rank and three ranks.  Same products,
+    pair records, the default when they fit and the pair-tile form does not apply) against the
+    five-kernel pair / F / J^T path (MLFF_MF_FORM=rec / pair) on the same operand, one rank and
+    three ranks.  Same products,
     regrouped: 1e-13 of the largest entry.  Covers every Zt source of k_rec_g: the LDS x
     stage (one identity permutation, <= 16 points per rank), the per-permutation gathers
     (the golden permutation sets) and the Zt table (M = 40: three 16-point groups, with
@@ -289,16 +290,17 @@ def test_record_factored_operator_matches_pair_path(sg, golden_dir, name, monkey
     v = np.random.default_rng(5).standard_normal(n)
     out = {}
     for rec in ("1", "0"):
-        monkeypatch.setenv("MLFF_MF_REC", rec)
+        monkeypatch.setenv("MLFF_MF_FORM", "rec" if rec == "1" else "pair")
         with sg.KernelSolver(n) as s:
             s.sgdml_operator(Rd, Rdd, perms, sig)
             s.set_operator(-1.0, 1e-10)
+            assert s.operator_form() == ("rec" if rec == "1" else "pair")
             out[rec] = (s.matvec(v), s.storage_info()[1])
     assert out["1"][1] != out["0"][1]  # the two paths report their own algorithmic bytes
     ref = out["0"][0]
     np.testing.assert_allclose(out["1"][0], ref, rtol=0, atol=1e-13 * np.abs(ref).max())
 
-    monkeypatch.setenv("MLFF_MF_REC", "1")
+    monkeypatch.setenv("MLFF_MF_FORM", "rec")
 
     def body(rank, w, key):
         with sg.KernelSolver(n, device=0, rank=rank, world=w,
@@ -344,3 +346,83 @@ def test_record_kernel_point_groups_bitwise(sg, monkeypatch, M):
     for key in ("rg8", "rg4", "rg8wc32"):
         for a, b in zip(out[key], out["rg16"]):
             np.testing.assert_array_equal(a, b)
+
+
+def _molecule(n_atoms, M, seed):
+    """A random small molecule (n_atoms atoms on a perturbed compact frame) and M geometries:
+    descriptor length D = n (n - 1) / 2 picks the pair-tile variant (L lanes per point)."""
+    rng = np.random.default_rng(seed)
+    frame = rng.uniform(-2.0, 2.0, (n_atoms, 3))
+    frame *= (n_atoms / 9.0) ** (1.0 / 3.0)
+    R = frame[None] + 0.08 * rng.standard_normal((M, n_atoms, 3))
+    from oracle.sgdml import descriptors
+
+    return descriptors(R)
+
+
+@pytest.mark.parametrize("n_atoms,M,perm", [(9, 111, False), (9, 40, True), (9, 583, False),
+                                            (9, 300, True), (12, 70, False), (15, 50, False),
+                                            (21, 30, False), (24, 20, False), (5, 9, False)])
+def test_pair_tile_operator_matches_pair_path(sg, golden_dir, monkeypatch, n_atoms, M, perm):
+    """The pair-tile operator (kernels_pt.hip: query points in registers, (j, p) rows streamed
+    through LDS, the default for n <= 24 atoms) against the five-kernel pair / F / J^T path on
+    the same operand: one rank, 3 ranks (row blocks splitting points), every pair-tile variant
+    that covers D (MLFF_PT_VARIANT) and one chunk / many chunks of the (j, p) range
+    (MLFF_PT_CHUNKS).  Same products, another order: 1e-13 of the largest entry.
+    Reference: predict.py:172-220 (K_op of iterative_solver.py:383-445)."""
+    Rd, Rdd = _molecule(n_atoms, M, seed=n_atoms * 1000 + M)
+    if perm:
+        perms = np.atleast_2d(load_golden(golden_dir, "sgdml_ethanol_n270_perms")["perms"])
+    else:
+        perms = np.arange(n_atoms)[None, :]
+    n = 3 * n_atoms * M
+    v = np.random.default_rng(M).standard_normal(n)
+
+    def run(form, extra=None, world=1):
+        monkeypatch.setenv("MLFF_MF_FORM", form)
+        for k, val in (extra or {}).items():
+            monkeypatch.setenv(k, val)
+
+        def body(rank, w, key):
+            with sg.KernelSolver(n, device=0, rank=rank, world=w,
+                                 comm_id=key if w > 1 else None) as s:
+                s.sgdml_operator(Rd, Rdd, perms, 10.0)
+                s.set_operator(-1.0, 1e-10)
+                if s.nrows > 0:
+                    assert s.operator_form() == form, (s.operator_form(), form)
+                return s.matvec(v)
+
+        from tests.test_gpu_multirank import run_ranks
+
+        y = np.concatenate(run_ranks(world, body, timeout=120))
+        for k in (extra or {}):
+            monkeypatch.delenv(k)
+        return y
+
+    ref = run("pair")
+    tol = 1e-13 * np.abs(ref).max()
+    np.testing.assert_allclose(run("pt"), ref, rtol=0, atol=tol)
+    np.testing.assert_allclose(run("pt", world=3), ref, rtol=0, atol=tol)
+    np.testing.assert_allclose(run("pt", {"MLFF_PT_CHUNKS": "1"}), ref, rtol=0, atol=tol)
+    # every entry of kernels_pt.hip's variant table (one that does not cover D runs the default)
+    for i in range(10):
+        np.testing.assert_allclose(run("pt", {"MLFF_PT_VARIANT": str(i)}), ref, rtol=0, atol=tol)
+
+
+def test_pair_tile_pcg_in_noise_band(sg, golden_dir):
+    """A golden solve of the reference (sgdml_ethanol_n621, rank-132 pivoted Cholesky) with the
+    pair-tile operator (the default form for ethanol) against the reference's recorded solve,
+    under its measured noise band (tests/parity.py)."""
+    from tests.parity import assert_pcg_parity
+
+    f = load_golden(golden_dir, "sgdml_ethanol_n621")
+    n, lam = f["y"].size, float(f["lam"])
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(f["R_desc"], f["R_d_desc"], f["perms"], float(f["sig"]))
+        s.set_operator(-1.0, lam)
+        assert s.operator_form() == "pt"
+        s.precon_pivchol(int(f["k_rot"]))
+        r = s.pcg(f["y"], tol=float(f["solver_tol"]), maxiter=5 * n)
+    assert_pcg_parity(r.iters, r.trace[1:], -r.x, int(f["cholesky__num_iters"]),
+                      f["cholesky__trace"], f["cholesky__alphas"],
+                      case="sgdml_ethanol_n621/cholesky")
