@@ -579,10 +579,11 @@ int resolve_storage(mlff_ctx *ctx) {
     return MLFF_OK;
   }
   if (ctx->storage == MLFF_STORAGE_AUTO && ctx->mf.ready) {
-    // the matrix-free operator moves O(M n_perms D) instead of O(N^2) bytes;
-    // take it when it is the cheaper one
-    const double tiles = 4.0 * (double)round_up(ctx->ld, kSymTile) * (double)round_up(ctx->ld, kSymTile) / ctx->world;
-    if (mf_bytes(ctx) < 0.5 * tiles) {
+    // the matrix-free operator or the stored K (tiles, rows): whichever the time model of
+    // the measured rates (mf_seconds) puts first for this rank's share
+    const double Np = (double)round_up(ctx->ld, kSymTile);
+    const double t_tiles = 10e-6 + 4.0 * Np * Np / ctx->world / 6.9e12;  // 2 launches + stream
+    if (mf_seconds(ctx) < t_tiles) {
       ctx->use_sym = false;
       ctx->use_mf = true;
       return MLFF_OK;

@@ -668,6 +668,9 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
                const int32_t *dP, const int32_t *perms_host, const int32_t *piinv_host,
                int n_perms, double sig, double *diag_out);
 double mf_bytes(const mlff_ctx *ctx);
+// modelled seconds of one application of the matrix-free operator in its form on this rank,
+// from the rates measured on MI355X: the storage choice of MLFF_STORAGE_AUTO
+double mf_seconds(const mlff_ctx *ctx);
 void mf_free(MfData &mf);
 int desc_perm_tables(mlff_ctx *ctx, const int32_t *perms, int n, int n_perms,
                      std::vector<int32_t> &Pt, std::vector<int32_t> &piinv);

@@ -1361,6 +1361,17 @@ void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStre
                      mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
 }
 
+double mf_seconds(const mlff_ctx *ctx) {
+  const MfData &mf = ctx->mf;
+  if (mf.ptile) {  // fp64-vector bound: ~40 TFLOP/s of 9 D + 8 flops per pair + 3 launches
+    const double pairs = (double)mf.ni * (double)(mf.M * mf.n_perms);
+    return 10e-6 + pairs * (9.0 * (double)mf.D + 8.0) / 40e12;
+  }
+  // latency-bound streams: the record-factored form (2 launches) at ~1.4 TB/s of its
+  // algorithmic bytes (nanotube 32.8 MB in 23 us), the pair sums (5 launches) at ~0.5 TB/s
+  return mf.rec ? 10e-6 + mf_bytes(ctx) / 1.4e12 : 20e-6 + mf_bytes(ctx) / 0.5e12;
+}
+
 int mf_form(const mlff_ctx *ctx) { return ctx->mf.ptile ? 2 : ctx->mf.rec ? 1 : 0; }
 
 double mf_bytes(const mlff_ctx *ctx) {

@@ -74,8 +74,9 @@ constexpr int pt_tile_rows(int DP) { return DP <= 72 ? 32 : DP <= 144 ? 16 : 8; 
 // NJ independent (j, p) rows per step (their dependent chains -- partial sums, butterfly,
 // sqrt, exp -- interleave); KEEP_DF / KEEP_Z: diff / the Zt row kept in registers between
 // the two passes over the lane's entries (else formed / read from LDS again)
-template <int L, int DL, int NJ, bool KEEP_DF, bool KEEP_Z>
-__global__ __launch_bounds__(kPtThreads) void k_pt_pair(PtArgs a, const int *__restrict__ status) {
+template <int L, int DL, int NJ, bool KEEP_DF, bool KEEP_Z, int WPE = 1>
+__global__ __launch_bounds__(kPtThreads) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+void k_pt_pair(PtArgs a, const int *__restrict__ status) {
   static_assert(DL % 2 == 0 && 64 % L == 0, "lane layout");
   constexpr int DP = L * DL;              // padded descriptor length
   constexpr int G = kPtThreads / L;       // query points per workgroup
@@ -226,56 +227,59 @@ struct PtFin {
   double *pq_part;      // kVecGrid partials of x . y (nullptr: none)
 };
 
-// one wave per query point (4 per workgroup, grid-stride in groups of 4 so that every wave
-// reaches the same barriers): F in the wave's LDS slice, then its 3 n rows
-constexpr int kPtFinMaxD = 288;
+// a workgroup per block of P = 256 / D points (grid-stride over the blocks): F of the block
+// summed over the chunks by one thread per (point, entry) into LDS, then one thread per row of
+// the block forms J_i^T F_i
+constexpr int kPtFinMaxF = 512;  // LDS doubles of F per block (P D <= 512)
 __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ double sF[4][kPtFinMaxD];
+  __shared__ double sF[kPtFinMaxF];
   __shared__ double sh[8];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n3 = 3 * a.n;
+  const int64_t P = a.D <= 256 ? 256 / a.D : 1;  // points per block (D <= 288: P >= 1)
+  const int64_t nblk = (a.ni + P - 1) / P;
+  const int64_t zs = a.ni * a.DP;                 // stride between chunks
   double pq = 0.0;
-  for (int64_t base = (int64_t)blockIdx.x * 4; base < a.ni; base += (int64_t)gridDim.x * 4) {
-    const int64_t il = base + wv;
-    const bool live = il < a.ni;
-    if (live) {
-      for (int64_t d = lane; d < a.D; d += 64) {
-        const double *p = a.part + il * a.DP + d;
-        double s = 0.0;
-        int z = 0;
-        for (; z + 3 < a.S; z += 4) {  // 4 loads in flight, summed in chunk order
-          const double t0 = p[(int64_t)z * a.ni * a.DP], t1 = p[(int64_t)(z + 1) * a.ni * a.DP];
-          const double t2 = p[(int64_t)(z + 2) * a.ni * a.DP], t3 = p[(int64_t)(z + 3) * a.ni * a.DP];
-          s += t0;
-          s += t1;
-          s += t2;
-          s += t3;
-        }
-        for (; z < a.S; ++z) s += p[(int64_t)z * a.ni * a.DP];
-        sF[wv][d] = s;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t p0 = blk * P;
+    const int64_t np = (a.ni - p0) < P ? (a.ni - p0) : P;
+    // F: the chunk partials of (point p0 + e / D, entry e % D) in chunk order, 8 in flight
+    for (int64_t e = threadIdx.x; e < np * a.D; e += 256) {
+      const int64_t q = e / a.D, d = e % a.D;
+      const double *src = a.part + (p0 + q) * a.DP + d;
+      double sum = 0.0;
+      int z = 0;
+      for (; z + 7 < a.S; z += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[(int64_t)(z + u) * zs];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) sum += t[u];
       }
+      for (; z < a.S; ++z) sum += src[(int64_t)z * zs];
+      sF[e] = sum;
     }
     __syncthreads();
-    if (live) {
-      const int64_t i = a.i0 + il;
+    for (int64_t e = threadIdx.x; e < np * n3; e += 256) {
+      const int64_t q = e / n3;
+      const int r = (int)(e % n3);
+      const int64_t i = a.i0 + p0 + q;
+      const int64_t rl = i * n3 + r - a.row0;
+      if (rl < 0 || rl >= a.nrows) continue;
       const double *Ri = a.Rdd + i * a.D * 3;
-      for (int r = lane; r < n3; r += 64) {
-        const int64_t rl = i * n3 + r - a.row0;
-        if (rl < 0 || rl >= a.nrows) continue;
-        const int at = r / 3, c = r % 3;
-        double acc = 0.0;
-        for (int b = 0; b < a.n; ++b) {
-          if (b == at) continue;
-          const int64_t d = pt_pair(at, b);
-          const double rv = Ri[d * 3 + c];
-          acc = fma(at > b ? -rv : rv, sF[wv][d], acc);
-        }
-        double yv = a.sigma * acc;
-        if (a.xloc != nullptr) yv = fma(a.lam, a.xloc[rl], yv);
-        a.y[rl] = yv;
-        if (a.pq_part != nullptr) pq = fma(a.xloc[rl], yv, pq);
+      const double *Fq = sF + q * a.D;
+      const int at = r / 3, c = r % 3;
+      double acc = 0.0;
+      for (int b = 0; b < a.n; ++b) {
+        if (b == at) continue;
+        const int64_t d = pt_pair(at, b);
+        const double rv = Ri[d * 3 + c];
+        acc = fma(at > b ? -rv : rv, Fq[d], acc);
       }
+      double yv = a.sigma * acc;
+      if (a.xloc != nullptr) yv = fma(a.lam, a.xloc[rl], yv);
+      a.y[rl] = yv;
+      if (a.pq_part != nullptr) pq = fma(a.xloc[rl], yv, pq);
     }
     __syncthreads();
   }
@@ -307,6 +311,10 @@ const PtVariant kPtVariants[] = {
     {4, 10, k_pt_pair<4, 10, 2, true, true>},
     {4, 10, k_pt_pair<4, 10, 1, true, true>},
     {1, 36, k_pt_pair<1, 36, 2, false, false>},
+    {2, 18, k_pt_pair<2, 18, 1, true, false, 3>},   // 10: 3 waves per SIMD
+    {2, 18, k_pt_pair<2, 18, 1, true, true, 3>},
+    {2, 18, k_pt_pair<2, 18, 1, false, false, 3>},
+    {2, 18, k_pt_pair<2, 18, 1, false, false, 4>},
 };
 
 const PtVariant *pt_variant(int64_t D) {
@@ -331,7 +339,20 @@ int pt_chunks(int64_t D, int64_t ni, int64_t MP) {
   const PtVariant *v = pt_variant(D);
   if (v == nullptr || ni <= 0) return 1;
   const int64_t G = kPtThreads / v->L, blocks = (ni + G - 1) / G;
-  int64_t S = (512 + blocks - 1) / blocks;
+  // one round of resident workgroups: the chip holds CUs x (workgroups per CU at this
+  // kernel's registers) at once, and a grid one workgroup past that runs a second round of
+  // the same length (M = 2777: 528 workgroups on 512 slots took 120 us, 506 take ~60)
+  int dev = 0, cus = 256, per_cu = 2;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(v->fn),
+                                                     kPtThreads, 0) == hipSuccess && nb > 0)
+      per_cu = nb;
+  }
+  const int64_t slots = (int64_t)cus * per_cu;
+  int64_t S = std::max<int64_t>(1, slots / blocks);
   S = std::min<int64_t>(S, (MP + 15) / 16);
   if (const char *e = std::getenv("MLFF_PT_CHUNKS")) S = std::atoi(e);  // sweeps
   return (int)std::max<int64_t>(1, std::min<int64_t>(S, MP));
@@ -382,8 +403,9 @@ void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, in
   fa.xloc = x_loc;
   fa.y = y_loc;
   fa.pq_part = pq_part;
+  const int64_t P = mf.D <= 256 ? 256 / mf.D : 1;
   const unsigned grid = pq_part != nullptr ? (unsigned)kVecGrid
-                                           : (unsigned)std::min<int64_t>((mf.ni + 3) / 4, 2048);
+                                           : (unsigned)std::min<int64_t>((mf.ni + P - 1) / P, 2048);
   hipLaunchKernelGGL(k_pt_fin, dim3(std::max(grid, 1u)), dim3(256), 0, s, fa, status);
 }
 

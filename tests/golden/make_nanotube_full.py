@@ -18,9 +18,11 @@ both sides start from identical bits).
    and the panel apply (make_noise_band.kop_variant: mf, mf_rev, mf_split): the 'mf' solve is the
    reference trajectory (trace, alpha = -x), the spread of the others its noise band.
 
-Writes tests/golden/nanotube_n15540.npz and nanotube_n15540_band.json.  CPU only, ~20 min on
-8 cores (2701 operator
-applications for the columns); the reference is not imported (its algorithm is the oracle's restatement).
+Writes tests/golden/nanotube_n15540.npz and nanotube_n15540_band.json.  CPU only: 40 min on 4
+cores (2701 operator applications for the columns, 30 min; three solves of 367 iterations); the
+reference is not imported (its algorithm is the oracle's restatement).  Recorded run: 367 / 367 /
+368 iterations, band b_it 1, b_cr 3, ||d alpha|| / ||alpha|| 2.0e-11, no near-tie among the 2701
+pivots (smallest relative gap of the best two candidates 3.1e-7).
 """
 from __future__ import annotations
 

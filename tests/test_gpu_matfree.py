@@ -405,7 +405,7 @@ def test_pair_tile_operator_matches_pair_path(sg, golden_dir, monkeypatch, n_ato
     np.testing.assert_allclose(run("pt", world=3), ref, rtol=0, atol=tol)
     np.testing.assert_allclose(run("pt", {"MLFF_PT_CHUNKS": "1"}), ref, rtol=0, atol=tol)
     # every entry of kernels_pt.hip's variant table (one that does not cover D runs the default)
-    for i in range(10):
+    for i in range(14):
         np.testing.assert_allclose(run("pt", {"MLFF_PT_VARIANT": str(i)}), ref, rtol=0, atol=tol)
 
 
