@@ -21,6 +21,9 @@
 // rounding level.
 #include "common.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace mlff {
 
 namespace {
@@ -126,6 +129,148 @@ __global__ __launch_bounds__(256) void k_trd_update_symv(
   if (lane == 0) p[r] = tau[j] * s;
 }
 
+// ---------------------------------------------------------------------------
+// Blocked reduction (dsytrd / dlatrd, UPLO = 'L'): panels of NB columns.  Inside a panel the
+// trailing block is only READ (y = A v with the block as the last SYR2K left it, the panel's
+// pending updates applied as corrections V t + W s); after the panel one GEMM applies them all,
+// A -= [V W] [W V]^T.  Per column: the symv reads the trailing block once (8 bytes per entry
+// instead of the unblocked update's read + write, 16), the rank-2 NB updates run on the matrix
+// cores.  VW / WV: m x 2 NB row-major, row i = [V(i, 0:NB) | W(i, 0:NB)] and [W | V].
+constexpr int kNB = 16;
+
+__device__ inline void block_sum_many_1024(double (&v)[2 * kNB], int cnt, double *red, double *out) {
+  // the 16 wave sums of each of the cnt values, then the waves added in order by thread q
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2 * kNB; ++q) {
+    if (q >= cnt) break;
+    double x = v[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) red[wave * 2 * kNB + q] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < cnt) {
+    double sum = 0.0;
+    for (int w = 0; w < kRefThreads / 64; ++w) sum += red[w * 2 * kNB + threadIdx.x];
+    out[threadIdx.x] = sum;
+  }
+  __syncthreads();
+}
+
+// Column j of its panel (c = j - j0): (1) c > 0: W(:, c - 1) from the symv y of reflector
+// v_{j-1} (t = W^T v, s = V^T v over the panel's earlier columns; w = tau (y - V t - W s);
+// w += -tau/2 (w . v) v), (2) column j of A with the panel's updates applied, d[j], (3) the
+// reflector of column j (dlarfg) -> V(:, c), tau[j], e[j].  last: only step (1) (the panel's
+// final w; c = the panel width).  One workgroup.
+__global__ __launch_bounds__(kRefThreads) void k_trd_panel_col(
+    const double *__restrict__ A, int64_t m, int64_t j0, int64_t j, int c, bool last,
+    const double *__restrict__ y, double *__restrict__ VW, double *__restrict__ WV,
+    double *__restrict__ col, double *__restrict__ tau, double *__restrict__ d,
+    double *__restrict__ e) {
+  __shared__ double red[(kRefThreads / 64) * 2 * kNB];
+  __shared__ double ts[2 * kNB];
+  const int tid = threadIdx.x;
+  const int64_t ld = 2 * kNB;
+  if (c > 0) {
+    // reflector c - 1 lives in rows >= j (v[j] = 1); its symv y over rows >= j
+    const int q = c - 1;
+    double acc[2 * kNB];
+#pragma unroll
+    for (int u = 0; u < 2 * kNB; ++u) acc[u] = 0.0;
+    for (int64_t i = j + tid; i < m; i += kRefThreads) {
+      const double vi = VW[i * ld + q];
+      const double *row = VW + i * ld;
+#pragma unroll
+      for (int u = 0; u < kNB; ++u) {
+        if (u >= q) break;
+        acc[u] = fma(row[kNB + u], vi, acc[u]);   // t_u = W(:, u) . v
+        acc[kNB + u] = fma(row[u], vi, acc[kNB + u]);  // s_u = V(:, u) . v
+      }
+    }
+    // compact: [t_0 .. t_{q-1}, s_0 .. s_{q-1}]
+    double pk[2 * kNB];
+#pragma unroll
+    for (int u = 0; u < 2 * kNB; ++u) pk[u] = 0.0;
+#pragma unroll
+    for (int u = 0; u < kNB; ++u)
+      if (u < q) {
+        pk[u] = acc[u];
+        pk[q + u] = acc[kNB + u];
+      }
+    block_sum_many_1024(pk, 2 * q, red, ts);
+    const double tq = tau[j - 1];
+    double dot = 0.0;
+    for (int64_t i = j + tid; i < m; i += kRefThreads) {
+      const double *row = VW + i * ld;
+      double w = y[i];
+      for (int u = 0; u < q; ++u) w -= row[u] * ts[u] + row[kNB + u] * ts[q + u];
+      w *= tq;
+      col[i] = w;  // staged
+      dot += w * row[q];
+    }
+    const double alpha = -0.5 * tq * block_sum_1024(dot, red);
+    for (int64_t i = j + tid; i < m; i += kRefThreads) {
+      const double w = fma(alpha, VW[i * ld + q], col[i]);
+      VW[i * ld + kNB + q] = w;
+      WV[i * ld + q] = w;
+    }
+    __syncthreads();
+  }
+  if (last || j >= m) return;
+  // column j (= row j: A symmetric) with the panel's c updates, rows >= j
+  const double *arow = A + j * m;
+  const double *vj = VW + j * ld;
+  for (int64_t i = j + tid; i < m; i += kRefThreads) {
+    const double *row = VW + i * ld;
+    double a = arow[i];
+    for (int u = 0; u < c; ++u) a -= row[u] * vj[kNB + u] + row[kNB + u] * vj[u];
+    col[i] = a;
+  }
+  __syncthreads();
+  if (tid == 0) d[j] = col[j];
+  if (j == m - 1) return;
+  double sq = 0.0;
+  for (int64_t i = j + 2 + tid; i < m; i += kRefThreads) sq += col[i] * col[i];
+  const double xnorm = sqrt(block_sum_1024(sq, red));
+  const double alpha = col[j + 1];
+  double t = 0.0, beta = alpha, scal = 0.0;
+  if (xnorm != 0.0) {
+    beta = -copysign(hypot(alpha, xnorm), alpha);
+    t = (beta - alpha) / beta;
+    scal = 1.0 / (alpha - beta);
+  }
+  if (tid == 0) {
+    tau[j] = t;
+    e[j] = beta;
+    VW[(j + 1) * ld + c] = 1.0;
+    WV[(j + 1) * ld + kNB + c] = 1.0;
+  }
+  for (int64_t i = j + 2 + tid; i < m; i += kRefThreads) {
+    const double v = col[i] * scal;
+    VW[i * ld + c] = v;
+    WV[i * ld + kNB + c] = v;
+  }
+}
+
+// y[r] = sum_{k > j} A[r, k] v[k] for rows r > j (v = VW(:, c), zero at rows <= j): the trailing
+// block read once, one wave per row, 16-byte loads
+__global__ __launch_bounds__(256) void k_trd_symv_ro(const double *__restrict__ A, int64_t m,
+                                                     int64_t j, const double *__restrict__ VW,
+                                                     int c, double *__restrict__ y) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = j + 1 + (int64_t)blockIdx.x * 4 + wave;
+  if (r >= m) return;
+  const double *row = A + r * m;
+  const int64_t ld = 2 * kNB;
+  double s = 0.0;
+  for (int64_t k = j + 1 + lane; k < m; k += 64) s = fma(row[k], VW[k * ld + c], s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) y[r] = s;
+}
+
 // dstebz's Sturm count: number of eigenvalues of the tridiagonal (d, e) below x
 __device__ inline int sturm_count(const double *__restrict__ d, const double *__restrict__ e,
                                   int64_t m, double x, double pivmin) {
@@ -186,6 +331,13 @@ __global__ __launch_bounds__(64) void k_trd_min_eig(const double *__restrict__ d
 
 }  // namespace
 
+// the blocked reduction from this size on (MLFF_SYEV_BLOCKED=0 / 1 forces the unblocked /
+// blocked one; A/B and tests)
+bool syev_blocked(int64_t m) {
+  if (const char *e = std::getenv("MLFF_SYEV_BLOCKED")) return std::atoi(e) != 0;
+  return m >= 512;
+}
+
 // lo_eig of the lower triangle of the device matrix M (m x m, row-major), on ctx->stream;
 // the value is returned to the host (and the tridiagonal (d, e) when d_host / e_host are
 // given: m and m - 1 entries).  M itself is not modified.
@@ -204,6 +356,43 @@ int sym_min_eig(mlff_ctx *ctx, const double *M, int64_t m, double *lo_eig, doubl
   MLFF_HIP(ctx, hipMemsetAsync(buf, 0, sizeof(double) * (8 * m + 8), s));
   const unsigned gc = (unsigned)std::min<int64_t>((m * m + 255) / 256, 8192);
   hipLaunchKernelGGL(k_trd_copy_lower, dim3(gc), dim3(256), 0, s, M, A, m);
+  if (syev_blocked(m)) {
+    // blocked reduction: panels of kNB columns, trailing block read-only inside a panel
+    double *VW = nullptr, *WV = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &VW, (size_t)(m * 2 * kNB)));
+    MLFF_TRY(scratch_alloc(ctx, &WV, (size_t)(m * 2 * kNB)));
+    for (int64_t j0 = 0; j0 < m; j0 += kNB) {
+      const int nbp = (int)std::min<int64_t>(kNB, m - j0);
+      MLFF_HIP(ctx, hipMemsetAsync(VW, 0, sizeof(double) * m * 2 * kNB, s));
+      MLFF_HIP(ctx, hipMemsetAsync(WV, 0, sizeof(double) * m * 2 * kNB, s));
+      for (int c = 0; c < nbp; ++c) {
+        const int64_t j = j0 + c;
+        hipLaunchKernelGGL(k_trd_panel_col, dim3(1), dim3(kRefThreads), 0, s, (const double *)A, m,
+                           j0, j, c, false, (const double *)p, VW, WV, W[0], tau, d, e);
+        if (j + 1 < m)
+          hipLaunchKernelGGL(k_trd_symv_ro, dim3((unsigned)((m - j - 1 + 3) / 4)), dim3(256), 0, s,
+                             (const double *)A, m, j, (const double *)VW, c, p);
+      }
+      const int64_t T0 = j0 + nbp;  // the trailing block after the panel
+      if (T0 < m) {
+        // the panel's last w, then A[T0:, T0:] -= [V W] [W V]^T (K = 2 kNB)
+        hipLaunchKernelGGL(k_trd_panel_col, dim3(1), dim3(kRefThreads), 0, s, (const double *)A, m,
+                           j0, T0, nbp, true, (const double *)p, VW, WV, W[0], tau, d, e);
+        launch_gemm(false, true, m - T0, m - T0, 2 * kNB, -1.0, VW + T0 * 2 * kNB, 2 * kNB,
+                    WV + T0 * 2 * kNB, 2 * kNB, 1.0, A + T0 * m + T0, m, s);
+      }
+      MLFF_HIP(ctx, hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_trd_min_eig, dim3(1), dim3(64), 0, s, (const double *)d,
+                       (const double *)e, m, out);
+    MLFF_HIP(ctx, hipGetLastError());
+    MLFF_HIP(ctx, hipMemcpyAsync(lo_eig, out, sizeof(double), hipMemcpyDeviceToHost, s));
+    if (d_host) MLFF_HIP(ctx, hipMemcpyAsync(d_host, d, sizeof(double) * m, hipMemcpyDeviceToHost, s));
+    if (e_host && m > 1)
+      MLFF_HIP(ctx, hipMemcpyAsync(e_host, e, sizeof(double) * (m - 1), hipMemcpyDeviceToHost, s));
+    MLFF_HIP(ctx, hipStreamSynchronize(s));
+    return MLFF_OK;
+  }
   // R(0); then per column j: S(j), R(j + 1)
   hipLaunchKernelGGL(k_trd_reflect, dim3(1), dim3(kRefThreads), 0, s, (const double *)A, m,
                      (int64_t)0, (const double *)p, (const double *)V[1], W[1], V[0], tau, d, e);

@@ -49,6 +49,10 @@ for s in ${STEPS:-suite smoke bench}; do
         step eth_m${m}_dense 600 $EB --m $m --storage dense
       done ;;
     ptprof) step ptprof 600 rocprofv3 --kernel-trace --stats -d $O/ptprof -o eth --output-format csv -- python3 bench.py --workload ethanol --m 5833 --no-cpu --no-solve --steps 30 --warmup 3 --storage matfree ;;
+    syev)
+      step syev_blocked 600 env MLFF_SYEV_BLOCKED=1 python scripts/bench_syev.py
+      step syev_unblocked 900 env MLFF_SYEV_BLOCKED=0 python scripts/bench_syev.py
+      step syev_prof 900 rocprofv3 --kernel-trace --stats -d $O/syev -o syev --output-format csv -- python3 scripts/bench_syev.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
   esac

@@ -39,11 +39,16 @@ WORKLOADS = {
     "nanotube": ["--workload", "nanotube"],
     # the reference's N = 156510 point (M = 141: Zt stored by k_mf_z, cluster apply)
     "nanotube_m141": ["--workload", "nanotube", "--m", "141"],
+    # the many-point ethanol shape (pair-tile operator): configs[0]'s M = 111 and the
+    # reference's N = 74979 point
+    "ethanol_m111": ["--workload", "ethanol", "--m", "111", "--storage", "matfree"],
+    "ethanol_m2777": ["--workload", "ethanol", "--m", "2777", "--storage", "matfree"],
 }
 GROUPS = {
     "sym": ["k_symv_dyn", "k_sym_reduce"],
     "dense": ["k_gemv<4, 4, 1>"],
     "matfree": ["k_mf_z?", "k_rec_g", "k_rec_fin"],  # ?: launched only where it runs
+    "matfree_pt": ["k_mf_z", "k_pt_pair", "k_pt_fin"],
     "precon0": ["k_gemv<4, 2, 0>", "k_colgemv_part", "k_precon_fin"],
     "precon1": ["k_lr_rows", "k_lr_fin"],
     "precon2": ["k_lr_cluster", "k_lr_fin"],
@@ -110,7 +115,8 @@ def fold(out: Path, wl: str, line: dict, table: dict, sha: str):
     cfg = line["config"]
     storage, world = cfg["storage"], line["n_gpus"]
     workload = cfg["workload"]
-    groups = [(f"{workload}/{storage}/gpus{world}", GROUPS[storage], line["operator_roofline"])]
+    og = "matfree_pt" if cfg.get("operator_form") == "pt" else storage
+    groups = [(f"{workload}/{storage}/gpus{world}", GROUPS[og], line["operator_roofline"])]
     pre = line.get("precon_roofline")
     if pre is not None:
         form = 2 if "k_lr_cluster" in pre["kernel"] else 1 if "k_lr_rows" in pre["kernel"] else 0
@@ -122,7 +128,7 @@ def fold(out: Path, wl: str, line: dict, table: dict, sha: str):
                      "launches": fm[k][1], "hbm_bytes": (2 * fm[k][0] + wm[k][0]) * 1024}
                  for k in fm}
         hbm = sum(p["hbm_bytes"] for p in parts.values())
-        alg = float(roof["bytes_per_launch"])
+        alg = float(roof["bytes_per_launch"])  # (the pair-tile line: its algorithmic bytes)
         table[key] = {
             "kernel": " + ".join(parts), "per_kernel": parts,
             "correction": "hbm = sum_k (2 * FETCH_SIZE_k + WRITE_SIZE_k) * 1024 (MI355X_MICROARCH.md "

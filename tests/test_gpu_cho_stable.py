@@ -54,8 +54,13 @@ CASES = [(1, 0.5, 0.5, None), (2, 1e-3, 1.0, None), (5, 1e-8, 2.0, None),
          (300, 1e-6, 1.0, 3e-13), (700, 1e-9, 10.0, None), (129, -1.0, 1.0, None)]
 
 
-@pytest.mark.parametrize("m,lo,hi,lo_eig", CASES)
-def test_sym_min_eig_vs_lapack(sg, m, lo, hi, lo_eig):
+@pytest.mark.parametrize("blocked", ["0", "1"])
+@pytest.mark.parametrize("m,lo,hi,lo_eig", CASES + [(17, 1e-6, 1.0, None), (520, 1e-9, 1.0, 2e-13)])
+def test_sym_min_eig_vs_lapack(sg, monkeypatch, m, lo, hi, lo_eig, blocked):
+    """Both reductions of kernels_syev.hip: per column (dsytd2) and blocked in 16-column panels
+    with the trailing update as one GEMM per panel (dsytrd / dlatrd; the default from m = 512),
+    partial last panels included (m = 5, 17, 100, 129, 300, 520, 700)."""
+    monkeypatch.setenv("MLFF_SYEV_BLOCKED", blocked)
     M = spd_with_spectrum(m, lo, hi, seed=m, lo_eig=lo_eig)
     Ml = np.tril(M) + np.tril(M, -1).T
     ref = scipy.linalg.eigh(M, eigvals_only=True, subset_by_index=[0, 0])[0]

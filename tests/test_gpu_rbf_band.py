@@ -100,3 +100,60 @@ def test_configs2_n65536_in_scaled_band(golden_dir):
     res_rows = b[rows] - (Krows @ r.x + LAM * r.x[rows])
     # sampled rows of a residual of norm <= 1e-6 ||b||: each is bounded by that norm
     assert np.abs(res_rows).max() <= 1.5e-6 * np.linalg.norm(b)
+
+
+def _first_departure(tr, ref_tr, tol=1e-10):
+    """First iteration j >= 1 where |log10(tr_j / ref_j)| > tol (None if the curves never part)."""
+    m = min(len(tr), len(ref_tr))
+    d = np.abs(np.log10(np.asarray(tr[1:m]) / np.asarray(ref_tr[1:m])))
+    hit = np.nonzero(d > tol)[0]
+    return int(hit[0]) + 1 if hit.size else None
+
+
+def test_configs2_gpu_summation_orders_sample_the_band(golden_dir, monkeypatch):
+    """Where the GPU's N = 8192 solve leaves the oracle's trajectories, and whether its low
+    iteration count is a bias or one sample of the band: the same system solved in five GPU
+    summation orders -- symmetric tiles with the cluster one-pass apply (default) or the two-pass
+    apply (MLFF_LR_ROWS=0), dense rows with either apply, and tiles with 8 row slices per split
+    tile (MLFF_SYM_LSUB=3) -- each compared with the oracle's BLAS-order and tile-order traces
+    (first iteration where they differ by more than 1e-10 in log10) and held to the band rule.
+    Printed table: tests/golden/make_rbf_band.py's band next to these GPU samples."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    bd = band(golden_dir)
+    f = np.load(golden_dir / "rbf_band_n8192.npz", allow_pickle=False)
+    n = bd["n"]
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, K, replace=False))
+    orders = {"sym+cluster": ("sym", {}), "sym+two-pass": ("sym", {"MLFF_LR_ROWS": "0"}),
+              "dense+cluster": ("dense", {}), "dense+two-pass": ("dense", {"MLFF_LR_ROWS": "0"}),
+              "sym(lsub=3)+cluster": ("sym", {"MLFF_SYM_LSUB": "3"})}
+    out = {}
+    for name, (storage, env) in orders.items():
+        for k_, v_ in env.items():
+            monkeypatch.setenv(k_, v_)
+        with sgdml_amd.KernelSolver(n) as s:
+            s.gen_rbf(X, ELL)
+            s.set_operator(1.0, LAM)
+            s.set_storage(storage)
+            s.precon_nystrom(idx)
+            r = s.pcg(b, tol=TOL, maxiter=5 * n)
+        for k_ in env:
+            monkeypatch.delenv(k_)
+        out[name] = r
+    ref_it = int(f["iters"])
+    print(f"\noracle orders: {({o: v['iters'] for o, v in bd['variants'].items()})} "
+          f"(band b_it {bd['band_iters']})")
+    for name, r in out.items():
+        dep_b = _first_departure(r.trace, f["trace"])
+        dep_t = _first_departure(r.trace, f["tiles_trace"])
+        rel = np.linalg.norm(r.x - f["x"]) / np.linalg.norm(f["x"])
+        print(f"GPU {name:22s} {r.iters:5d} iterations; leaves the blas trace at {dep_b}, the "
+              f"tile-order trace at {dep_t}; ||dx||/||x|| {rel:.2e}")
+        assert r.info == 0
+        assert abs(r.iters - ref_it) <= 2 * bd["band_iters"] + 2, (name, r.iters, ref_it)
+        assert rel <= 10 * bd["band_rel_dx"], (name, rel)
+    its = [r.iters for r in out.values()]
+    oracle_its = [v["iters"] for v in bd["variants"].values()]
+    print(f"GPU orders {min(its)}..{max(its)}, oracle orders {min(oracle_its)}..{max(oracle_its)}")
