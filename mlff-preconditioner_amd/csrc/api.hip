@@ -783,14 +783,21 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   size_t c0 = mark_begin(ctx, marks);
   MLFF_TRY(comm_allgather(ctx, zg, ctx->gb, (size_t)ctx->gstride));
   mark_end(ctx, marks, c0, it, 2);
-  launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
-                           status, s);
+  // symmetric tiles (dynamic schedule): p = z + beta p formed by the tile workgroups from the
+  // gathered z and written by the slot reduction (k_update_p_gathered's bits, one launch less)
+  const bool fuse_pg = ctx->fuse_p && ctx->use_sym && ctx->sym.dyn > 0 && ctx->sym.ntiles > 0;
+  PGather pg;
+  if (fuse_pg)
+    pg = PGather{ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->st, it};
+  else
+    launch_update_p_gathered(ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->p_full, ctx->st, it,
+                             status, s);
   const size_t e0 = mark_begin(ctx, marks);
   if (ctx->use_sym) {
     SymPack &sp = ctx->sym;
-    launch_symv(sp, ctx->p_full, sp.P, status, s);
+    launch_symv(sp, ctx->p_full, sp.P, status, s, pg);
     launch_sym_reduce_ranks(sp, ctx->rank, ctx->world, ctx->blk, ctx->p_full, pq_part(ctx),
-                            pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s);
+                            pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s, pg);
     mark_end(ctx, marks, e0, it);
     c0 = mark_begin(ctx, marks);
     MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));

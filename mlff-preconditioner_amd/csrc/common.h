@@ -605,9 +605,20 @@ void launch_sgdml_columns(const double *Rdd, int64_t M, int n, int64_t D, int64_
 // every tile with its mirror (one rank only)
 int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out);
 void sym_free(SymPack &sp);
+// The search-direction update of the sharded iteration (k_update_p_gathered: p = z + beta p,
+// z and every rank's rho partials in the gather buffer gb) folded into the tile mat-vec: the
+// tile workgroups form the operand entries they read, the slot reduction writes p (gb null:
+// not fused)
+struct PGather {
+  const double *gb = nullptr;
+  int64_t gstride = 0, blk = 0;
+  int world = 1;
+  DevState *st = nullptr;
+  long long it = 0;
+};
 // P <- slot partials of K v_full over the stored tiles
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
-                 hipStream_t s);
+                 hipStream_t s, PGather pg = PGather{});
 // one rank: y[i] = sum of the slots of row i (i < n_out); epilogue y = sigma y + lam vloc
 void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogue, double sigma,
                        double lam, const double *vloc, const int *status, hipStream_t s);
@@ -620,7 +631,8 @@ void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double si
 // tail slot `rank` of every block (pq_part / pp_part: kVecGrid scratch each)
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
                              const double *p_full, double *pq_part, double *pp_part,
-                             double sigma, double lam, const int *status, hipStream_t s);
+                             double sigma, double lam, const int *status, hipStream_t s,
+                             PGather pg = PGather{});
 // y = sigma * src + lam * vloc over n entries (src may alias y)
 void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, double lam,
                       const double *vloc, const int *status, hipStream_t s);

@@ -177,6 +177,49 @@ __device__ __forceinline__ void decode_unit(long long u, int nwhole, int lsub, i
   }
 }
 
+// rho of the gathered partials (every rank's kVecGrid rho partials in its gb block, after z):
+// k_update_p_gathered's sum -- thread f adds partials f, f + 256, ... in order (8 in flight),
+// then block_sum256 -- so every workgroup that forms it holds the same bits
+__device__ __forceinline__ double gathered_rho(const PGather &pg, double *sh) {
+  double v = 0.0;
+  const int np = pg.world * kVecGrid;
+  int f = threadIdx.x;
+  for (; f + 7 * 256 < np; f += 8 * 256) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int g = f + u * 256;
+      t[u] = pg.gb[(int64_t)(g / kVecGrid) * pg.gstride + pg.blk + (g % kVecGrid)];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += t[u];
+  }
+  for (; f < np; f += 256) v += pg.gb[(int64_t)(f / kVecGrid) * pg.gstride + pg.blk + (f % kVecGrid)];
+  v = block_sum256(v, sh);
+  __syncthreads();
+  if (threadIdx.x == 0) sh[4] = v;
+  __syncthreads();
+  const double rho = sh[4];
+  __syncthreads();
+  return rho;
+}
+
+// operand entries of the fused form: p = fma(beta, p_old, z) (z at iteration 1), z from the
+// gather buffer -- k_update_p_gathered's arithmetic, the same bits
+__device__ __forceinline__ double pg_z(const PGather &pg, int64_t i) {
+  return pg.gb[(i / pg.blk) * pg.gstride + i % pg.blk];
+}
+__device__ __forceinline__ double pg_val(const PGather &pg, const double *v, int64_t i, double beta) {
+  return pg.it > 1 ? fma(beta, v[i], pg_z(pg, i)) : pg_z(pg, i);
+}
+__device__ __forceinline__ d2 pg_val2(const PGather &pg, const double *v, int64_t i, double beta) {
+  if (pg.gb == nullptr) return *reinterpret_cast<const d2 *>(v + i);
+  const d2 z = *reinterpret_cast<const d2 *>(pg.gb + (i / pg.blk) * pg.gstride + i % pg.blk);
+  if (pg.it <= 1) return z;
+  const d2 po = *reinterpret_cast<const d2 *>(v + i);
+  return d2{fma(beta, po.x, z.x), fma(beta, po.y, z.y)};
+}
+
 __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ tiles,
                                                   const int2 *__restrict__ list,
                                                   const double *__restrict__ v,
@@ -185,7 +228,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
                                                   int nwhole, long long nunits, int nb,
                                                   int lsub,
                                                   unsigned long long *__restrict__ ticket,
-                                                  const int *__restrict__ status) {
+                                                  const int *__restrict__ status, PGather pg) {
   if (status != nullptr && *status != ST_RUNNING) return;
   __shared__ double sh[6 * B + 4 * kRB * 64];
   __shared__ long long s_next;
@@ -197,15 +240,22 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
   const long long G = gridDim.x;
   long long u = blockIdx.x;
   if (u >= nunits) return;
+  // fused p update: beta from the gathered rho partials (block 0 publishes rho for the slot
+  // reduction, which writes p after every tile has read p_old)
+  double beta = 0.0;
+  if (pg.gb != nullptr) {
+    const double rho = gathered_rho(pg, sh);
+    if (pg.it > 1) beta = rho / pg.st->rho1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) pg.st->rho_new = rho;
+  }
   int tile, h, gb0, gb1;
   decode_unit(u, nwhole, lsub, tile, h, gb0, gb1);
   int2 t = list[tile];
   const double *A = tiles + (int64_t)tile * B * B;
   d2 pc[4], a[kRB][4];
   {
-    const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)t.y * B);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+    for (int q = 0; q < 4; ++q) pc[q] = pg_val2(pg, v, (int64_t)t.y * B + 2 * (lane + 64 * q), beta);
     const d2 *rowp = reinterpret_cast<const d2 *>(A + (int64_t)(gb0 + w) * kRB * B) + lane;
 #pragma unroll
     for (int rr = 0; rr < kRB; ++rr)
@@ -213,8 +263,10 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
       for (int q = 0; q < 4; ++q) a[rr][q] = __builtin_nontemporal_load(rowp + rr * (B / 2) + 64 * q);
   }
   if (threadIdx.x == 0) s_next = G + (long long)atomicAdd(ticket, 1ull);
-  for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256)
-    vrow[gb0 * kRB + i] = v[(int64_t)t.x * B + gb0 * kRB + i];
+  for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256) {
+    const int64_t gi = (int64_t)t.x * B + gb0 * kRB + i;
+    vrow[gb0 * kRB + i] = pg.gb != nullptr ? pg_val(pg, v, gi, beta) : v[gi];
+  }
   __syncthreads();
   while (true) {
     const bool diag = t.x == t.y;
@@ -279,9 +331,9 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
       decode_unit(un, nwhole, lsub, tile2, h2, gb02, gb12);
       t2 = list[tile2];
       A2 = tiles + (int64_t)tile2 * B * B;
-      const d2 *v2 = reinterpret_cast<const d2 *>(v + (int64_t)t2.y * B);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pc[q] = v2[lane + 64 * q];
+      for (int q = 0; q < 4; ++q)
+        pc[q] = pg_val2(pg, v, (int64_t)t2.y * B + 2 * (lane + 64 * q), beta);
       const d2 *rowp = reinterpret_cast<const d2 *>(A2 + (int64_t)(gb02 + w) * kRB * B) + lane;
 #pragma unroll
       for (int rr = 0; rr < kRB; ++rr)
@@ -309,8 +361,10 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
     gb1 = gb12;
     t = t2;
     A = A2;
-    for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256)
-      vrow[gb0 * kRB + i] = v[(int64_t)t.x * B + gb0 * kRB + i];
+    for (int i = threadIdx.x; i < (gb1 - gb0) * kRB; i += 256) {
+      const int64_t gi = (int64_t)t.x * B + gb0 * kRB + i;
+      vrow[gb0 * kRB + i] = pg.gb != nullptr ? pg_val(pg, v, gi, beta) : v[gi];
+    }
     __syncthreads();
   }
 }
@@ -415,15 +469,23 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
                                                       const int *__restrict__ own,
                                                       int64_t ld, int64_t blk, int64_t bstride,
                                                       double *__restrict__ yg,
-                                                      const double *__restrict__ p,
+                                                      double *p,  // read, and written when fused
                                                       double *__restrict__ pq_part,
                                                       double *__restrict__ pp_part,
                                                       unsigned long long *__restrict__ ticket,
-                                                      const int *__restrict__ status) {
+                                                      const int *__restrict__ status,
+                                                      PGather pg) {
   if (status != nullptr && *status != ST_RUNNING) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   __shared__ double sh[8];
   double apq = 0.0, app = 0.0;
+  // fused p update: rho as k_symv_dyn summed it, p written here (every tile has read p_old)
+  double beta = 0.0;
+  if (PQ && pg.gb != nullptr) {
+    const double rho = pg.st->rho_new;
+    if (pg.it > 1) beta = rho / pg.st->rho1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) pg.st->rho = rho;
+  }
   const int64_t lo = (int64_t)rank * blk, hi = lo + blk;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ld;
        i += (int64_t)gridDim.x * 256) {
@@ -457,7 +519,13 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
     }
     yg[(i / blk) * bstride + i % blk] = s;
     if (PQ) {
-      const double pv = p[i];
+      double pv;
+      if (pg.gb != nullptr) {
+        pv = pg_val(pg, p, i, beta);
+        p[i] = pv;
+      } else {
+        pv = p[i];
+      }
       apq = fma(pv, s, apq);
       if (i >= lo && i < hi) app = fma(pv, pv, app);
     }
@@ -612,13 +680,13 @@ __global__ __launch_bounds__(256) void k_sym_gen_rbf(const int2 *__restrict__ li
 }  // namespace
 
 void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *status,
-                 hipStream_t s) {
+                 hipStream_t s, PGather pg) {
   if (sp.ntiles == 0) return;
   const int64_t grid = sp.nwhole + ((sp.ntiles - sp.nwhole) << sp.lsub);
   if (sp.dyn > 0) {
     hipLaunchKernelGGL(k_symv_dyn, dim3((unsigned)std::min<int64_t>(sp.dyn, grid)), dim3(256), 0, s,
                        sp.tiles, sp.list, v_full, P, sp.Pq, sp.Np, (int)sp.nwhole, (long long)grid,
-                       (int)sp.nb, sp.lsub, sp.ticket, status);
+                       (int)sp.nb, sp.lsub, sp.ticket, status, pg);
     return;
   }
   hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)grid), dim3(256), 0, s, sp.tiles, sp.list, v_full,
@@ -649,20 +717,22 @@ void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double si
 
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
                              const double *p_full, double *pq_part, double *pp_part,
-                             double sigma, double lam, const int *status, hipStream_t s) {
+                             double sigma, double lam, const int *status, hipStream_t s,
+                             PGather pg) {
   const int64_t ld = (int64_t)world * blk;
   const dim3 grid(kVecGrid);
+  double *pw = const_cast<double *>(p_full);  // written only when the p update is fused
   if (p_full == nullptr) {
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (1 << sp.lsub) - 1, (int)sp.nb, rank,
-                       sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
-                       sp.ticket, status);
+                       sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
+                       sp.ticket, status, PGather{});
     return;
   }
   hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                      (1 << sp.lsub) - 1, (int)sp.nb, rank,
-                     sp.own, ld, blk, sp.ystride, sp.yg, p_full, pq_part, pp_part,
-                     sp.ticket, status);
+                     sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
+                     sp.ticket, status, pg);
   hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
                      rank, world, blk, sp.ystride, sp.yg, status);
 }

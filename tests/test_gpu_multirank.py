@@ -135,6 +135,24 @@ def test_sharded_sym_row_slices(lsub, monkeypatch):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,precon", [(2, "nystrom"), (3, "none"), (8, "nystrom")])
+def test_sharded_fused_p_update_bitwise(world, precon, monkeypatch):
+    """The sharded tiled iteration with p = z + beta p formed inside k_symv_dyn and written by
+    the slot reduction (default) against the separate k_update_p_gathered launch
+    (MLFF_FUSE_P=0): the same arithmetic on the same operands, so iterates, residual curve and
+    stop decisions are bit-identical."""
+    n = 1003
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MLFF_FUSE_P", fuse)
+        out[fuse] = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    for a, b in zip(out["1"], out["0"]):
+        assert a["iters"] == b["iters"] and a["info"] == b["info"] == 0
+        np.testing.assert_array_equal(a["trace"], b["trace"])
+        np.testing.assert_array_equal(a["x"], b["x"])
+
+
+@pytest.mark.timeout(300)
 def test_sharded_sgdml_assembly_rows():
     import sgdml_amd
     from oracle.sgdml import descriptors
