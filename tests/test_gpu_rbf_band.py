@@ -26,8 +26,8 @@ pytestmark = pytest.mark.gpu
 LAM, ELL, K, TOL = 1e-6, 0.2, 256, 1e-6
 
 
-def band(golden_dir):
-    return json.loads((golden_dir / "rbf_band_n8192.json").read_text())
+def band(golden_dir, n=8192):
+    return json.loads((golden_dir / f"rbf_band_n{n}.json").read_text())
 
 
 def gpu_solve(n, maxiter):
@@ -53,10 +53,15 @@ def crossings_ok(tr, ref_tr, slack):
         assert abs(ia - ib) <= slack, (lvl, ia, ib, slack)
 
 
-def test_configs2_n8192_in_band(golden_dir):
-    bd = band(golden_dir)
-    f = np.load(golden_dir / "rbf_band_n8192.npz", allow_pickle=False)
-    n = bd["n"]
+@pytest.mark.parametrize("n", [8192, 16384])
+def test_configs2_in_band(golden_dir, n):
+    """N = 8192 and 16384: the measured six-order band of that size (the band grows faster than
+    the count: b_it 95 of 2963 at 8192, see rbf_band_n16384.json for 16384)."""
+    if not (golden_dir / f"rbf_band_n{n}.json").exists():
+        pytest.fail(f"tests/golden/rbf_band_n{n}.json missing (make_rbf_band.py --band --n {n})")
+    bd = band(golden_dir, n)
+    f = np.load(golden_dir / f"rbf_band_n{n}.npz", allow_pickle=False)
+    assert bd["n"] == n
     _, b, idx, r = gpu_solve(n, 5 * n)
     np.testing.assert_array_equal(idx, f["idx"])
     ref_it, ref_tr, ref_x = int(f["iters"]), f["trace"], f["x"]
