@@ -148,6 +148,26 @@ def band(n=8192):
                                           "band_rel_dx")}), flush=True)
 
 
+def extended(n=8192):
+    """The N = n system in extended precision (np.longdouble products and sums of the mat-vec
+    and of the panel apply, rounded to fp64 once per operator application): where the count lands
+    when the operator's rounding error shrinks -- rbf_ld_n{n}.json."""
+    X, b, idx = problem(n)
+    K = rbf_kernel(X, ELL)
+    B, sp = nystrom_panel(K[:, idx], idx, LAM, 0)
+    t0 = time.time()
+    mvK, mvT = make_gemv(K, "ld"), make_gemv(B, "ld")
+    mvTt = make_gemv(np.ascontiguousarray(B.T), "ld")
+    x, info, tr, it = cg_legacy(lambda v: mvK(v) + LAM * v, b, tol=TOL, maxiter=5 * n,
+                                psolve=lambda r: sp * ((r - mvTt(mvT(r))) / LAM))
+    f = np.load(GOLDEN / f"rbf_band_n{n}.npz", allow_pickle=False)
+    out = {"n": n, "order": "ld", "iters": int(it), "info": int(info),
+           "rel_dx_vs_blas": float(np.linalg.norm(x - f["x"]) / np.linalg.norm(f["x"])),
+           "seconds": time.time() - t0}
+    (GOLDEN / f"rbf_ld_n{n}.json").write_text(json.dumps(out, indent=1, sort_keys=True))
+    print(json.dumps(out), flush=True)
+
+
 def full(n=65536, order="tiles"):
     """order: 'tiles' (rbf_tiles_symv, the committed rbf_solve_n65536.npz) or 'tiles_rev'
     (rbf_tiles_symv_rev with the panel apply in reversed column order: a second sample of the
@@ -194,7 +214,10 @@ if __name__ == "__main__":
     ap.add_argument("--full", action="store_true")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--order", choices=["tiles", "tiles_rev"], default="tiles")
+    ap.add_argument("--ld", action="store_true", help="extended-precision solve of --n")
     a = ap.parse_args()
+    if a.ld:
+        extended(a.n or 8192)
     if a.band:
         band(a.n or 8192)
     if a.full:
