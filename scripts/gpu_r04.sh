@@ -48,6 +48,20 @@ for s in ${STEPS:-suite smoke bench}; do
         step eth_m${m}_sym 600 $EB --m $m --storage sym
         step eth_m${m}_dense 600 $EB --m $m --storage dense
       done ;;
+    eth111)  # configs[0] geometry (N = 2997): pair-tile vs record-factored, kernel split of both
+      step eth111_pt 300 $EB --m 111 --storage matfree --mf-form pt
+      step eth111_rec 300 $EB --m 111 --storage matfree --mf-form rec
+      step eth111_prof_rec 300 rocprofv3 --kernel-trace --stats -d $O/eth111_rec -o eth --output-format csv -- python3 bench.py --workload ethanol --m 111 --no-cpu --no-solve --steps 30 --warmup 3 --storage matfree --mf-form rec
+      step eth111_prof_pt 300 rocprofv3 --kernel-trace --stats -d $O/eth111_pt -o eth --output-format csv -- python3 bench.py --workload ethanol --m 111 --no-cpu --no-solve --steps 30 --warmup 3 --storage matfree --mf-form pt ;;
+    solo)  # per-rank compute floors of configs[2] on W = 8 / 4 (SOLO transport), fused p vs not
+      for W in 8 4; do
+        step solo_w${W} 300 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
+        step solo_w${W}_nofuse 300 env MLFF_FUSE_P=0 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
+      done ;;
+    rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
+      step rehearse_w8 400 env MLFF_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29508 \
+        bench.py --gpus 8 --steps 10 --warmup 2 --no-solve ;;
     ptprof) step ptprof 600 rocprofv3 --kernel-trace --stats -d $O/ptprof -o eth --output-format csv -- python3 bench.py --workload ethanol --m 5833 --no-cpu --no-solve --steps 30 --warmup 3 --storage matfree ;;
     syev)
       step syev_blocked 600 env MLFF_SYEV_BLOCKED=1 python scripts/bench_syev.py

@@ -113,3 +113,14 @@ def test_iteration_bytes_use_the_apply_form_that_ran():
     assert b == pytest.approx(32.8e6 + one_pass + 56.0 * n)
     assert b < 32.8e6 + 16.0 * k * n                   # below the two-pass count
     assert bench.iteration_bytes(1e9, 0.0, n) == 1e9 + 56.0 * n   # no preconditioner
+
+
+def test_many_point_workload_arguments(monkeypatch):
+    """The ethanol legs at the reference's published sizes: matrix-free
+    storage with a chosen operator form, and the reference step times they are quoted against."""
+    a = _args(monkeypatch, "--workload", "ethanol", "--m", "5833", "--storage", "matfree",
+              "--mf-form", "pt")
+    assert (a.workload, a.m, a.storage, a.mf_form) == ("ethanol", 5833, "matfree", "pt")
+    assert 27 * 583 in bench.REF_STEP_S_ETHANOL and 27 * 2777 in bench.REF_STEP_S_ETHANOL
+    assert bench.REF_STEP_S_ETHANOL[27 * 5833] == 0.550
+    assert _args(monkeypatch).mf_form is None          # the library's default form
