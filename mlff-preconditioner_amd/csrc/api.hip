@@ -786,6 +786,9 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   // symmetric tiles (dynamic schedule): p = z + beta p formed by the tile workgroups from the
   // gathered z and written by the slot reduction (k_update_p_gathered's bits, one launch less)
   const bool fuse_pg = ctx->fuse_p && ctx->use_sym && ctx->sym.dyn > 0 && ctx->sym.ntiles > 0;
+  // symmetric tiles + low-rank apply: k_update_xr_shares folded into the next T r pass
+  const bool fold_xr = ctx->fuse_xr && ctx->use_sym && lowrank &&
+                       xr_fold_fits(ctx->blk, ctx->tsplit, ctx->nrows);
   PGather pg;
   if (fuse_pg)
     pg = PGather{ctx->gb, ctx->gstride, ctx->blk, ctx->world, ctx->st, it};
@@ -802,9 +805,10 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
     c0 = mark_begin(ctx, marks);
     MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
     mark_end(ctx, marks, c0, it, 2);
-    launch_update_xr_shares(ctx->x, ctx->r, p_loc, sp.yr, sp.yr + ctx->blk, ctx->world, ctx->nrows,
-                            ctx->sigma_K, ctx->lam, lowrank ? ctx->tpart_base : rr_part(ctx),
-                            ctx->st, status, s);
+    if (!fold_xr)
+      launch_update_xr_shares(ctx->x, ctx->r, p_loc, sp.yr, sp.yr + ctx->blk, ctx->world,
+                              ctx->nrows, ctx->sigma_K, ctx->lam,
+                              lowrank ? ctx->tpart_base : rr_part(ctx), ctx->st, status, s);
   } else {
     MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx)));
     mark_end(ctx, marks, e0, it);
@@ -819,7 +823,17 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
     // z half, kind 1) so a sampled apply is always timed whole
     ctx->timing.sample = (it + 1) % ctx->timing.every == 0;
     const size_t tm = mark_begin(ctx, marks);
-    launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status, s);
+    if (fold_xr) {
+      // x, r update of this iteration inside the T r pass: r_new goes to the other buffer
+      // (ctx->z, unused by the sharded iteration), which becomes r
+      launch_gemv_xr(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->z, ctx->x, p_loc,
+                     ctx->sym.yr, ctx->sym.yr + ctx->blk, ctx->world, ctx->nrows, ctx->sigma_K,
+                     ctx->lam, ctx->tpart_base, ctx->st, ctx->tpart, status, s);
+      std::swap(ctx->r, ctx->z);
+    } else {
+      launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status,
+                        s);
+    }
     mark_end(ctx, marks, tm, it, 3);
     c0 = mark_begin(ctx, marks);
     MLFF_TRY(allreduce(ctx, ctx->tpart_base, (size_t)(kVecGrid + ctx->k * ctx->tsplit)));

@@ -519,6 +519,16 @@ void launch_update_p_gathered(const double *gb, int64_t gstride, int64_t blk, in
 void launch_update_xr_shares(double *x, double *r, const double *p, const double *y,
                              const double *shares, int world, int64_t n, double sigma, double lam,
                              double *rr_part, DevState *st, const int *status, hipStream_t s);
+// launch_update_xr_shares folded into the T r pass of the next apply (launch_gemv_split's
+// tpart): r_new = r - alpha q into r_out (the caller swaps r and r_out), x, the rr partials
+// and T r_new, the bits of the two launches; xr_fold_fits: the split / row-count shapes it
+// covers
+bool xr_fold_fits(int64_t ncols, int splits, int64_t n);
+void launch_gemv_xr(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
+                    const double *r, double *r_out, double *x, const double *p, const double *y,
+                    const double *shares, int world, int64_t n, double sigma, double lam,
+                    double *rr_part, DevState *st, double *tpart, const int *status,
+                    hipStream_t s);
 // pq = sum(pq_part); alpha = rho/pq; x += alpha p; r -= alpha q; rr partials
 void launch_update_xr(double *x, double *r, const double *p, const double *q, int64_t n,
                       const double *pq_part, double *rr_part, DevState *st, const int *status,

@@ -45,17 +45,19 @@ __device__ __forceinline__ bool stop_prologue_wide(const StopFold &f, double *sh
 }
 
 // ---------------------------------------------------------------------------
-// the column range [c_begin, c_end) of R rows, dot v; NT: non-temporal loads of M
+// the column range [c_begin, c_end) of R rows, dot v; NT: non-temporal loads of M.
+// Operand entry c is v2[c - voff] (voff = c_begin: v staged for the range only, k_gemv_xr)
 template <int R, int U, bool NT>
 __device__ __forceinline__ void gemv_rows_body(const d2 *const (&rowp)[R], const d2 *__restrict__ v2,
-                                               int64_t c_begin, int64_t c_end, double (&acc)[R]) {
+                                               int64_t c_begin, int64_t c_end, double (&acc)[R],
+                                               int64_t voff = 0) {
   int64_t c = c_begin + threadIdx.x;
   // main body: U full strides without bounds checks
   for (; c + (int64_t)(U - 1) * 256 < c_end; c += (int64_t)256 * U) {
     d2 xv[U];
     d2 kv[R][U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) xv[u] = v2[c + u * 256];
+    for (int u = 0; u < U; ++u) xv[u] = v2[c - voff + u * 256];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -70,7 +72,7 @@ __device__ __forceinline__ void gemv_rows_body(const d2 *const (&rowp)[R], const
       }
   }
   for (; c < c_end; c += 256) {
-    const d2 xv = v2[c];
+    const d2 xv = v2[c - voff];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const d2 kv = NT ? __builtin_nontemporal_load(rowp[r] + c) : rowp[r][c];
@@ -1067,6 +1069,14 @@ void launch_update_p_gathered(const double *gb, int64_t gstride, int64_t blk, in
                      p_full, st, it, status);
 }
 
+// the r update of the sharded symmetric-tile iteration for one entry: q = sigma y + lam p,
+// r - alpha q (k_update_xr_shares and k_gemv_xr share it: the same bits)
+__device__ __forceinline__ double xr_shares_r(double ri, double yi, double pi, double alpha,
+                                              double sigma, double lam) {
+  const double qi = sigma * yi + lam * pi;
+  return fma(-alpha, qi, ri);
+}
+
 // Several ranks, symmetric tiles: y = this rank's reduce-scattered rows of K p,
 // shares[0..world) = every rank's share of p.q (k_pq_publish).  pq = the shares
 // summed in rank order; q = sigma y + lam p (as k_axpby_loc); then as k_update_xr.
@@ -1093,9 +1103,8 @@ __global__ __launch_bounds__(256) void k_update_xr_shares(double *__restrict__ x
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * 256) {
     const double pi = p[i];
-    const double qi = sigma * y[i] + lam * pi;
     x[i] = fma(alpha, pi, x[i]);
-    const double ri = fma(-alpha, qi, r[i]);
+    const double ri = xr_shares_r(r[i], y[i], pi, alpha, sigma, lam);
     r[i] = ri;
     acc = fma(ri, ri, acc);
   }
@@ -1108,6 +1117,136 @@ void launch_update_xr_shares(double *x, double *r, const double *p, const double
                              double *rr_part, DevState *st, const int *status, hipStream_t s) {
   hipLaunchKernelGGL(k_update_xr_shares, dim3(kVecGrid), dim3(256), 0, s, x, r, p, y, shares, world,
                      n, sigma, lam, rr_part, st, status);
+}
+
+// Several ranks, symmetric tiles, low-rank preconditioner: k_update_xr_shares folded into
+// the T r pass of the next apply (k_gemv<4, 2, 0>).  Every workgroup forms r_new = r - alpha q
+// for the columns of its split and stages it in LDS as the GEMV operand; the workgroups of row
+// group 0 also write r_new into r_out (another buffer: the other row groups still read r),
+// x += alpha p, and the rr partials of the 256-row blocks of their columns, each summed as
+// k_update_xr_shares sums it (one 256-thread block_sum256 per 256 rows), the blocks past the
+// local rows zeroed.  x, r, the rr partials and the T r partials are the bits of the two
+// separate launches.  Needs 2 cs2 % 256 == 0 and n <= kVecGrid * 256 (xr_fold_fits).  Gated
+// (solver stopped): row group 0 copies r into r_out, so the caller's buffer swap keeps the
+// state.
+template <int R, int U, bool NT>
+__global__ __launch_bounds__(256) void k_gemv_xr(const double *__restrict__ M, int64_t ld,
+                                                 int64_t rows, int64_t n2, int64_t cs2,
+                                                 const double *__restrict__ r,
+                                                 double *__restrict__ r_out,
+                                                 double *__restrict__ x,
+                                                 const double *__restrict__ p,
+                                                 const double *__restrict__ y,
+                                                 const double *__restrict__ shares, int world,
+                                                 int64_t n, double sigma, double lam,
+                                                 double *__restrict__ rr_part, DevState *st,
+                                                 double *__restrict__ out, int64_t out_stride,
+                                                 const int *__restrict__ status,
+                                                 int64_t cached_rows) {
+  extern __shared__ d2 vs[];  // r_new of this split's columns (cs2 entries)
+  __shared__ double sh[4 * R > 8 ? 4 * R : 8];
+  const int64_t c_begin = (int64_t)blockIdx.y * cs2;
+  int64_t c_end = c_begin + cs2;
+  if (c_end > n2) c_end = n2;
+  const bool owner = blockIdx.x == 0;
+  const d2 *__restrict__ r2 = reinterpret_cast<const d2 *>(r);
+  d2 *__restrict__ ro2 = reinterpret_cast<d2 *>(r_out);
+  if (*status != ST_RUNNING) {
+    if (owner)
+      for (int64_t c = c_begin + threadIdx.x; c < c_end; c += 256) ro2[c] = r2[c];
+    return;
+  }
+  double pq = 0.0;
+  for (int g = 0; g < world; ++g) pq += shares[g];
+  const double alpha = st->rho / pq;
+  if (owner && blockIdx.y == 0 && threadIdx.x == 0) {
+    st->pq = pq;
+    st->alpha = alpha;
+  }
+  for (int64_t c = c_begin + threadIdx.x; c < c_end; c += 256) {
+    d2 rv = r2[c];
+    const int64_t i = 2 * c;
+    if (i < n) {
+      const double pi = p[i];
+      rv.x = xr_shares_r(rv.x, y[i], pi, alpha, sigma, lam);
+      if (owner) x[i] = fma(alpha, pi, x[i]);
+    }
+    if (i + 1 < n) {
+      const double pi = p[i + 1];
+      rv.y = xr_shares_r(rv.y, y[i + 1], pi, alpha, sigma, lam);
+      if (owner) x[i + 1] = fma(alpha, pi, x[i + 1]);
+    }
+    vs[c - c_begin] = rv;
+    if (owner) ro2[c] = rv;
+  }
+  __syncthreads();
+  if (owner) {
+    const double *vd = reinterpret_cast<const double *>(vs);
+    for (int64_t b0 = 2 * c_begin; b0 < 2 * c_end; b0 += 256) {
+      const int64_t i = b0 + threadIdx.x;
+      double acc = 0.0;
+      if (i < n) {
+        const double ri = vd[i - 2 * c_begin];
+        acc = fma(ri, ri, acc);
+      }
+      const double t = block_sum256(acc, sh);
+      if (threadIdx.x == 0) rr_part[b0 / 256] = t;
+    }
+    if (blockIdx.y == 0)
+      for (int64_t b = (2 * n2 + 255) / 256 + threadIdx.x; b < kVecGrid; b += 256) rr_part[b] = 0.0;
+    __syncthreads();  // sh is reused below
+  }
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const d2 *rowp[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) rowp[q] = reinterpret_cast<const d2 *>(M + (r0 + q) * ld);
+  double acc[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) acc[q] = 0.0;
+  if (NT && r0 + R > cached_rows)
+    gemv_rows_body<R, U, true>(rowp, vs, c_begin, c_end, acc, c_begin);
+  else
+    gemv_rows_body<R, U, false>(rowp, vs, c_begin, c_end, acc, c_begin);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const double s = wave_sum(acc[q]);
+    if (lane == 0) sh[w * R + q] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    const int q = threadIdx.x;
+    const int64_t row = r0 + q;
+    if (row < rows)
+      out[(int64_t)blockIdx.y * out_stride + row] =
+          (sh[q] + sh[R + q]) + (sh[2 * R + q] + sh[3 * R + q]);
+  }
+}
+
+bool xr_fold_fits(int64_t ncols, int splits, int64_t n) {
+  const int64_t n2 = ncols / 2, cs2 = (n2 + splits - 1) / splits;
+  return ncols % 2 == 0 && (2 * cs2) % 256 == 0 && cs2 * 16 <= 64 * 1024 &&
+         n <= (int64_t)kVecGrid * 256;
+}
+
+void launch_gemv_xr(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
+                    const double *r, double *r_out, double *x, const double *p, const double *y,
+                    const double *shares, int world, int64_t n, double sigma, double lam,
+                    double *rr_part, DevState *st, double *tpart, const int *status,
+                    hipStream_t s) {
+  constexpr int R = 4, U = 2;
+  const int64_t n2 = ncols / 2;
+  const int64_t cs2 = (n2 + splits - 1) / splits;
+  const dim3 grid((unsigned)((k + R - 1) / R), (unsigned)splits);
+  const size_t shm = sizeof(d2) * (size_t)cs2;
+  if (panel_streams(k, ldt))
+    hipLaunchKernelGGL((k_gemv_xr<R, U, true>), grid, dim3(256), shm, s, T, ldt, k, n2, cs2, r, r_out,
+                       x, p, y, shares, world, n, sigma, lam, rr_part, st, tpart, k, status,
+                       panel_cached_rows(k, ldt));
+  else
+    hipLaunchKernelGGL((k_gemv_xr<R, U, false>), grid, dim3(256), shm, s, T, ldt, k, n2, cs2, r, r_out,
+                       x, p, y, shares, world, n, sigma, lam, rr_part, st, tpart, k, status,
+                       (int64_t)0);
 }
 
 // alpha = rho / (p.q); x += alpha p; r -= alpha q; rr partials

@@ -58,6 +58,8 @@ for s in ${STEPS:-suite smoke bench}; do
         step solo_w${W} 300 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
         step solo_w${W}_nofuse 300 env MLFF_FUSE_P=0 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
       done ;;
+    soloprof)  # kernel trace of the W = 8 SOLO iteration (per-kernel times and the gaps between them)
+      step soloprof 300 rocprofv3 --kernel-trace --stats -d $O/soloprof -o solo --output-format csv -- python3 bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5 ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL
       step rehearse_w8 400 env MLFF_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29508 \
@@ -69,6 +71,10 @@ for s in ${STEPS:-suite smoke bench}; do
       step syev_prof 900 rocprofv3 --kernel-trace --stats -d $O/syev -o syev --output-format csv -- python3 scripts/bench_syev.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
+    pmcrg)  # nanotube operator traffic with one 16-point group per pair block (each Rdd block read
+            # by one workgroup) against the default two 8-point groups
+      step pmc_rg16 600 env MLFF_REC_RG=16 python scripts/pmc_head.py --out $O/pmc_rg16 --workloads nanotube
+      step pmc_rg8 600 python scripts/pmc_head.py --out $O/pmc_rg8 --workloads nanotube ;;
   esac
 done
 echo "== all done $(date +%T)" | tee -a $O/steps.log

@@ -107,7 +107,14 @@ def problem(n):
     return X, b, idx
 
 
-def band(n=8192):
+ORDERS = ["blas", "rev", "blk7", "blk512", "pair", "tiles"]
+
+
+def band(n=8192, orders=None):
+    """orders: a subset of ORDERS (always with "blas", the reference's order the band is
+    measured from); N = 32768 runs the four orders that take minutes, not hours, at that size
+    (rev / pair: ~3 h each)."""
+    orders = ORDERS if not orders else ["blas"] + [o for o in orders if o != "blas"]
     X, b, idx = problem(n)
     K = rbf_kernel(X, ELL)
     B, sp = nystrom_panel(K[:, idx], idx, LAM, 0)
@@ -115,7 +122,7 @@ def band(n=8192):
     panel_order = {"blas": "blas", "rev": "rev", "blk7": "blk7", "blk512": "blk512",
                    "pair": "pair", "tiles": "blk512"}
     runs = {}
-    for order in ["blas", "rev", "blk7", "blk512", "pair", "tiles"]:
+    for order in orders:
         t0 = time.time()
         mvK = tiles.matvec if order == "tiles" else make_gemv(K, order)
         mvT = make_gemv(B, panel_order[order])
@@ -140,9 +147,10 @@ def band(n=8192):
            "band_iters": int(max(abs(e["d_iters"]) for e in v)),
            "band_crossing": int(max(e["max_d_crossing"] for e in v)),
            "band_rel_dx": float(max(e["rel_dx"] for e in v))}
+    out["orders"] = list(runs)
+    tiles = {"tiles_x": runs["tiles"][0], "tiles_trace": runs["tiles"][2]} if "tiles" in runs else {}
     np.savez_compressed(GOLDEN / f"rbf_band_n{n}.npz", x=x0, trace=tr0, iters=np.int64(it0),
-                        idx=idx, tiles_x=runs["tiles"][0], tiles_trace=runs["tiles"][2],
-                        **{f"trace_{o}": r[2] for o, r in runs.items()})
+                        idx=idx, **tiles, **{f"trace_{o}": r[2] for o, r in runs.items()})
     (GOLDEN / f"rbf_band_n{n}.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps({k: out[k] for k in ("ref_iters", "band_iters", "band_crossing",
                                           "band_rel_dx")}), flush=True)
@@ -215,10 +223,11 @@ if __name__ == "__main__":
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--order", choices=["tiles", "tiles_rev"], default="tiles")
     ap.add_argument("--ld", action="store_true", help="extended-precision solve of --n")
+    ap.add_argument("--orders", nargs="+", choices=ORDERS, default=None)
     a = ap.parse_args()
     if a.ld:
         extended(a.n or 8192)
     if a.band:
-        band(a.n or 8192)
+        band(a.n or 8192, a.orders)
     if a.full:
         full(a.n or 65536, a.order)

@@ -152,6 +152,28 @@ def test_sharded_fused_p_update_bitwise(world, precon, monkeypatch):
         np.testing.assert_array_equal(a["x"], b["x"])
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world,precon,n", [(2, "nystrom", 1003), (3, "pivchol", 1003),
+                                            (8, "nystrom", 1003), (2, "nystrom", 9000),
+                                            (3, "pivchol", 9000)])
+def test_sharded_fused_xr_update_bitwise(world, precon, n, monkeypatch):
+    """The sharded tiled iteration with k_update_xr_shares folded into the next apply's T r
+    pass (k_gemv_xr: r_new staged in LDS, x / r / rr partials written by row group 0, r and
+    the spare vector swapped; default) against the separate launch (MLFF_FUSE_XR=0): the
+    same arithmetic, so iterates, residual curve and stop decisions are bit-identical.
+    n = 9000 runs the T r pass in 6-9 column splits (n = 1003: one); chunk = 5 puts
+    iterations gated after the stop test inside chunks."""
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MLFF_FUSE_XR", fuse)
+        out[fuse] = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    for a, b in zip(out["1"], out["0"]):
+        assert a["iters"] == b["iters"] and a["info"] == b["info"] == 0
+        np.testing.assert_array_equal(a["trace"], b["trace"])
+        np.testing.assert_array_equal(a["x"], b["x"])
+        np.testing.assert_array_equal(a["lev"], b["lev"])
+
+
 @pytest.mark.timeout(300)
 def test_sharded_sgdml_assembly_rows():
     import sgdml_amd
