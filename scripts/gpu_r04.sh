@@ -58,6 +58,8 @@ for s in ${STEPS:-suite smoke bench}; do
         step solo_w${W} 300 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
         step solo_w${W}_nofuse 300 env MLFF_FUSE_P=0 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
       done ;;
+    diag1) step diag1 600 python -u scripts/dev/diag_config1.py ;;
+    diag1b) step diag1b 900 python -u scripts/dev/diag_config1b.py ;;
     soloprof)  # kernel trace of the W = 8 SOLO iteration (per-kernel times and the gaps between them)
       step soloprof 300 rocprofv3 --kernel-trace --stats -d $O/soloprof -o solo --output-format csv -- python3 bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5 ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL

@@ -87,7 +87,26 @@ def pivoted_cholesky_logged(get_col, diagonal, max_rank):
     return L, index_columns, piv_val, gap
 
 
-def main():
+def woodbury_gram_order(L, lam, order):
+    """oracle.precon.woodbury_panel (iterative_cholesky.py:141-143) with the Gram matrix L^T L
+    summed in another order: 'rev' (rows of L reversed) or 'blk8' (8 row blocks added in block
+    order).  The PCG at lam = 1e-10 is sensitive to the panel's rounding: r - T^T T r cancels
+    to O(lam / sigma^2) in the leading directions."""
+    import scipy.linalg
+
+    if order == "rev":
+        Lr = np.ascontiguousarray(L[::-1])
+        G = Lr.T @ Lr
+    else:
+        G = sum(L[b].T @ L[b] for b in np.array_split(np.arange(L.shape[0]), 8))
+    L2 = scipy.linalg.cholesky(lam * np.eye(L.shape[1]) + G, lower=True)
+    return scipy.linalg.solve_triangular(L2, L.T, lower=True)
+
+
+def main(cache=None, panel_orders=()):
+    """cache: .npz path (outside the repository: 336 MB) holding L and the pivot log, written
+    on the first run and read by later ones; panel_orders: Gram-matrix orders of the Woodbury
+    panel whose solves join the band (variants 'panel_<order>')."""
     t_all = time.time()
     R, Rd, Rdd, perms, y = problem()
     n = y.size
@@ -99,22 +118,34 @@ def main():
         e[i] = 1.0
         return -mv0(e) + LAM * e
 
-    diag = -kernel_diag(Rd, Rdd, perms, SIG)
-    L, piv, piv_val, gap = pivoted_cholesky_logged(get_col, diag, K_RANK)
+    if cache is not None and Path(cache).exists():
+        c = np.load(cache, allow_pickle=False)
+        L, piv, piv_val, gap = c["L"], c["piv"], c["piv_val"], c["gap"]
+    else:
+        diag = -kernel_diag(Rd, Rdd, perms, SIG)
+        L, piv, piv_val, gap = pivoted_cholesky_logged(get_col, diag, K_RANK)
+        if cache is not None:
+            np.savez(cache, L=L, piv=piv, piv_val=piv_val, gap=gap)
     print(f"pivoted Cholesky k={K_RANK}: {time.time() - t_all:.0f} s", flush=True)
     T, sp = woodbury_panel(L, LAM)
+    panels = {"": T}
+    for po in panel_orders:
+        panels[po] = woodbury_gram_order(L, LAM, po)
     del L
     panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}
     runs = {}
-    for order in ("mf", "mf_rev", "mf_split"):
+    plan = [(o, "") for o in ("mf", "mf_rev", "mf_split")] + [("mf", po) for po in panel_orders]
+    for order, po in plan:
         t0 = time.time()
+        T = panels[po]
         mvK = kop_variant(Rd, Rdd, perms, SIG, order)
         mvT = make_gemv(T, panel_order[order])
         mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order[order])
         x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=TOL, maxiter=5 * n,
                                     psolve=lambda r: sp * ((r - mvTt(mvT(r))) / LAM))
-        runs[order] = (x, info, tr, it)
-        print(f"solve {order:8s} iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
+        name = order if not po else f"panel_{po}"
+        runs[name] = (x, info, tr, it)
+        print(f"solve {name:8s} iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
     x0, info0, tr0, it0 = runs["mf"]
     top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
     cr0 = half_decade_crossings(tr0[1:], top)
@@ -143,4 +174,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cache", default=None)
+    ap.add_argument("--panel-orders", nargs="*", default=[], choices=["rev", "blk8"])
+    a = ap.parse_args()
+    main(a.cache, a.panel_orders)
