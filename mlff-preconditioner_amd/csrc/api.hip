@@ -22,6 +22,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <mutex>
 
@@ -430,7 +431,29 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
 // device tridiagonalisation + Sturm bisection of kernels_syev.hip), M += (+1e-15 if lo_eig
 // <= 0 else -1e-15) I (:578-579), then the Cholesky factor (:580-582; LinAlgError when it
 // fails).  A (k x k, device) is overwritten with the lower factor; lo_eig_out: the value used.
+//
+// Inside the builds (lo_eig_out == nullptr) the downward shift is tried first: when M - 1e-15 I
+// factors, M's smallest eigenvalue is above 1e-15 (to the factorisation's backward error), so
+// the reference takes the lo_eig > 0 branch and factors this same matrix -- the same factor,
+// without the eigenvalue (whose tridiagonalisation is most of a Nystrom build: 2 x 5.3 s of 13 s
+// at k = 14670, profiles/r04/syev/).  Otherwise (lo_eig at or below 1e-15, where the sign
+// decides) the eigenvalue path runs as before.  MLFF_CHO_FAST=0 (read at context creation):
+// always the eigenvalue path.
 int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out) {
+  if (lo_eig_out == nullptr && ctx->cho_fast) {
+    ScratchScope scope(ctx);
+    double *B = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &B, (size_t)(k * k)));
+    MLFF_HIP(ctx, hipMemcpyAsync(B, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+    launch_add_diag(B, k, -1e-15, ctx->stream);
+    bool ok = false;
+    MLFF_TRY(potrf_lower(ctx, B, k, &ok));
+    if (ok) {
+      MLFF_HIP(ctx, hipMemcpyAsync(A, B, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+      ctx->last_lo_eig = std::numeric_limits<double>::quiet_NaN();  // above 1e-15, not computed
+      return MLFF_OK;
+    }
+  }
   double lo = 0.0;
   MLFF_TRY(sym_min_eig(ctx, A, k, &lo, nullptr, nullptr));
   ctx->last_lo_eig = lo;
@@ -1067,7 +1090,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   mlff_ctx *ctx = new mlff_ctx();
   ctx->device = device;
   for (auto [name, flag] : {std::pair<const char *, bool *>{"MLFF_FUSE_P", &ctx->fuse_p},
-                            std::pair<const char *, bool *>{"MLFF_FUSE_XR", &ctx->fuse_xr}}) {
+                            std::pair<const char *, bool *>{"MLFF_FUSE_XR", &ctx->fuse_xr},
+                            std::pair<const char *, bool *>{"MLFF_CHO_FAST", &ctx->cho_fast}}) {
     const char *e = std::getenv(name);
     *flag = e == nullptr || std::atoi(e) != 0;
   }

@@ -339,6 +339,7 @@ struct mlff_ctx {
   // CG vector updates folded into the matrix-free nanotube iteration; read from
   // MLFF_FUSE_P / MLFF_FUSE_XR (=0: separate launches) when the context is created
   bool fuse_p = true, fuse_xr = true;
+  bool cho_fast = true;  // cho_factor_stable: shifted Cholesky first inside builds (MLFF_CHO_FAST)
   bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
   int lr_q = 0;                // its clusters
   double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials
@@ -557,7 +558,9 @@ int syrk_wide(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t 
 int gram_wide(mlff_ctx *ctx, const double *A, const double *B, int64_t k, int64_t ncols,
               int64_t ldw, double *G);
 // in-place lower Cholesky of the k x k matrix A (row-major, ld = k)
-int potrf_lower(mlff_ctx *ctx, double *A, int64_t k);
+// ok_out: report a matrix that is not positive definite there (MLFF_OK returned) instead of
+// as MLFF_ERR_LINALG
+int potrf_lower(mlff_ctx *ctx, double *A, int64_t k, bool *ok_out = nullptr);
 // smallest eigenvalue of the lower triangle of a device m x m matrix (kernels_syev.hip:
 // Householder tridiagonalisation + Sturm bisection, the eigh of _cho_factor_stable);
 // d_host / e_host (optional): the tridiagonal

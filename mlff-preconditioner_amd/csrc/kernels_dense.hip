@@ -459,7 +459,7 @@ void launch_add_diag(double *A, int64_t k, double v, hipStream_t s) {
   hipLaunchKernelGGL(k_add_diag, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, A, k, v);
 }
 
-int potrf_lower(mlff_ctx *ctx, double *A, int64_t k) {
+int potrf_lower(mlff_ctx *ctx, double *A, int64_t k, bool *ok_out) {
   int *err = &ctx->st->linalg_err;
   MLFF_HIP(ctx, hipMemsetAsync(err, 0, sizeof(int), ctx->stream));
   for (int64_t j0 = 0; j0 < k; j0 += 64) {
@@ -479,6 +479,10 @@ int potrf_lower(mlff_ctx *ctx, double *A, int64_t k) {
   int h_err = 0;
   MLFF_HIP(ctx, hipMemcpyAsync(&h_err, err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ok_out != nullptr) {
+    *ok_out = h_err == 0;
+    return MLFF_OK;
+  }
   if (h_err) return set_error(ctx, MLFF_ERR_LINALG, "Cholesky factorization failed: matrix is not positive definite");
   return MLFF_OK;
 }

@@ -331,11 +331,15 @@ __global__ __launch_bounds__(64) void k_trd_min_eig(const double *__restrict__ d
 
 }  // namespace
 
-// the blocked reduction from this size on (MLFF_SYEV_BLOCKED=0 / 1 forces the unblocked /
-// blocked one; A/B and tests)
+// the blocked reduction only on request (MLFF_SYEV_BLOCKED=1; =0 / unset: the unblocked one).
+// Measured (scripts/bench_syev.py, profiles/r04/syev/): m = 2701 0.250 s blocked vs 0.053 s
+// unblocked, m = 14670 10.3 s vs 5.3 s -- its one-workgroup panel column (269 us per column at
+// m = 14670) and the symv's 256-byte-strided reads of v (298 us per column) cost more than the
+// halved trailing-block traffic saves
 bool syev_blocked(int64_t m) {
+  (void)m;
   if (const char *e = std::getenv("MLFF_SYEV_BLOCKED")) return std::atoi(e) != 0;
-  return m >= 512;
+  return false;
 }
 
 // lo_eig of the lower triangle of the device matrix M (m x m, row-major), on ctx->stream;

@@ -60,6 +60,15 @@ for s in ${STEPS:-suite smoke bench}; do
       done ;;
     diag1) step diag1 600 python -u scripts/dev/diag_config1.py ;;
     diag1b) step diag1b 900 python -u scripts/dev/diag_config1b.py ;;
+    diag1c) step diag1c 900 python -u scripts/dev/diag_config1c.py ;;
+    soloxr)  # SOLO floors: every fusion / the x, r fold off / the p fold off, interleaved twice
+      for rep in 1 2; do
+        for W in 8 4; do
+          step solo_w${W}_r$rep 300 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
+          step solo_w${W}_noxr_r$rep 300 env MLFF_FUSE_XR=0 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
+          step solo_w${W}_nop_r$rep 300 env MLFF_FUSE_P=0 python bench.py --solo-world $W --n 65536 --steps 40 --warmup 5
+        done
+      done ;;
     soloprof)  # kernel trace of the W = 8 SOLO iteration (per-kernel times and the gaps between them)
       step soloprof 300 rocprofv3 --kernel-trace --stats -d $O/soloprof -o solo --output-format csv -- python3 bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5 ;;
     rehearse)  # the multi-rank bench flow on one GPU (torchrun, SOLO ranks over gloo): not RCCL

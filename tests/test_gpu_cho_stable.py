@@ -142,8 +142,14 @@ NYS_TOL = {2: 2e-8, 3: 2e-9}
 LEV_TOL = {2: 5e-8, 3: 5e-9}
 
 
+@pytest.mark.parametrize("fast", ["1", "0"])
 @pytest.mark.parametrize("t", [1, 2, 3])
-def test_golden_nystrom_and_lev_scores(sg, golden_dir, t):
+def test_golden_nystrom_and_lev_scores(sg, golden_dir, t, fast, monkeypatch):
+    """fast = "1" (default): inside the builds the downward-shifted Cholesky is tried before
+    the eigenvalue (api.hip cho_factor_stable); "0": always the eigenvalue path.  Both must
+    raise where the reference raises (t = 1, lo_eig 1.26e-16 in (0, 1e-15)) and match it
+    elsewhere."""
+    monkeypatch.setenv("MLFF_CHO_FAST", fast)
     f = np.load(golden_dir / "cho_stable_ethanol.npz", allow_pickle=False)
     idx = f["idx"]
     s = _solver_for(sg, f, t)
@@ -169,3 +175,25 @@ def test_golden_nystrom_and_lev_scores(sg, golden_dir, t):
             assert rel <= LEV_TOL[t], (t, rel)
     finally:
         s.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_cho_fast_path_same_factors(sg, monkeypatch, variant):
+    """The fast path factors the very matrix the eigenvalue path factors when lo_eig > 1e-15
+    (K_mm of a well-conditioned RBF system): Nystrom panels, applies and leverage scores are
+    bit-identical with MLFF_CHO_FAST=1 and =0 (variant 1 never calls _cho_factor_stable)."""
+    from sgdml_amd import synthetic
+
+    n, k = 1003, 150
+    X, b = synthetic.rbf_points(n, 3, 3)
+    idx = np.sort(np.random.default_rng(5).choice(n, k, replace=False))
+    out = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("MLFF_CHO_FAST", fast)
+        with sg.KernelSolver(n) as s:
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, 1e-3)
+            s.precon_nystrom(idx, variant=variant)
+            out[fast] = (s.precon_panel(), s.precon_apply(b), s.lev_scores(idx, 1e-3))
+    for a, c in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, c)
