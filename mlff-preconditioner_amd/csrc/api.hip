@@ -810,7 +810,7 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
   // gathered z and written by the slot reduction (k_update_p_gathered's bits, one launch less)
   const bool fuse_pg = ctx->fuse_p && ctx->use_sym && ctx->sym.dyn > 0 && ctx->sym.ntiles > 0;
   // symmetric tiles + low-rank apply: k_update_xr_shares folded into the next T r pass
-  const bool fold_xr = ctx->fuse_xr && ctx->use_sym && lowrank &&
+  const bool fold_xr = ctx->fuse_xr_ranks && ctx->use_sym && lowrank &&
                        xr_fold_fits(ctx->blk, ctx->tsplit, ctx->nrows);
   PGather pg;
   if (fuse_pg)
@@ -1095,6 +1095,7 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
     const char *e = std::getenv(name);
     *flag = e == nullptr || std::atoi(e) != 0;
   }
+  if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
   ctx->rank = rank;
   ctx->world = world;
   ctx->N = n_global;

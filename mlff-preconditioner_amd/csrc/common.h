@@ -340,6 +340,9 @@ struct mlff_ctx {
   // MLFF_FUSE_P / MLFF_FUSE_XR (=0: separate launches) when the context is created
   bool fuse_p = true, fuse_xr = true;
   bool cho_fast = true;  // cho_factor_stable: shifted Cholesky first inside builds (MLFF_CHO_FAST)
+  // sharded tiled iteration: k_update_xr_shares folded into the next T r pass (MLFF_FUSE_XR_RANKS=1;
+  // off by default: SOLO floors 4.5 us slower at W = 4, equal at W = 8)
+  bool fuse_xr_ranks = false;
   bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
   int lr_q = 0;                // its clusters
   double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials

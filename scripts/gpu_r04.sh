@@ -61,6 +61,10 @@ for s in ${STEPS:-suite smoke bench}; do
     diag1) step diag1 600 python -u scripts/dev/diag_config1.py ;;
     diag1b) step diag1b 900 python -u scripts/dev/diag_config1b.py ;;
     diag1c) step diag1c 900 python -u scripts/dev/diag_config1c.py ;;
+    diag1qr) step diag1qr 600 python -u scripts/dev/diag_config1c.py --qr ;;
+    syevfast)  # the Nystrom build with the shifted-Cholesky-first cho_factor_stable (default) and without
+      step syev_fast 600 python scripts/bench_syev.py
+      step syev_nofast 900 env MLFF_CHO_FAST=0 python scripts/bench_syev.py ;;
     soloxr)  # SOLO floors: every fusion / the x, r fold off / the p fold off, interleaved twice
       for rep in 1 2; do
         for W in 8 4; do

@@ -159,13 +159,13 @@ def test_sharded_fused_p_update_bitwise(world, precon, monkeypatch):
 def test_sharded_fused_xr_update_bitwise(world, precon, n, monkeypatch):
     """The sharded tiled iteration with k_update_xr_shares folded into the next apply's T r
     pass (k_gemv_xr: r_new staged in LDS, x / r / rr partials written by row group 0, r and
-    the spare vector swapped; default) against the separate launch (MLFF_FUSE_XR=0): the
-    same arithmetic, so iterates, residual curve and stop decisions are bit-identical.
+    the spare vector swapped; MLFF_FUSE_XR_RANKS=1) against the separate launch (default):
+    the same arithmetic, so iterates, residual curve and stop decisions are bit-identical.
     n = 9000 runs the T r pass in 6-9 column splits (n = 1003: one); chunk = 5 puts
     iterations gated after the stop test inside chunks."""
     out = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("MLFF_FUSE_XR", fuse)
+        monkeypatch.setenv("MLFF_FUSE_XR_RANKS", fuse)
         out[fuse] = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
     for a, b in zip(out["1"], out["0"]):
         assert a["iters"] == b["iters"] and a["info"] == b["info"] == 0
