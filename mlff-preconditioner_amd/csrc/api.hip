@@ -439,7 +439,9 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
 // at k = 14670, profiles/r04/syev/).  Otherwise (lo_eig at or below 1e-15, where the sign
 // decides) the eigenvalue path runs as before.  MLFF_CHO_FAST=0 (read at context creation):
 // always the eigenvalue path.
-int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out) {
+int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out,
+                      double *shift_out = nullptr) {
+  if (shift_out) *shift_out = -1e-15;
   if (lo_eig_out == nullptr && ctx->cho_fast) {
     ScratchScope scope(ctx);
     double *B = nullptr;
@@ -459,21 +461,51 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out) {
   ctx->last_lo_eig = lo;
   if (lo_eig_out) *lo_eig_out = lo;
   launch_add_diag(A, k, lo <= 0.0 ? 1e-15 : -1e-15, ctx->stream);
+  if (shift_out) *shift_out = lo <= 0.0 ? 1e-15 : -1e-15;
   return potrf_lower(ctx, A, k);
 }
 
 // Woodbury panel from a wide factor W = L^T (k x blk) in place:
 //   G = lam I + W W^T; L2 = chol(G); W <- L2^-1 W   (iterative_cholesky.py:141-143)
+//
+// ctx->wb_refine (MLFF_WB_REFINE): W is the top block of Q1 = A R1^-1, A = [L; sqrt(lam) I],
+// R1 = L2^T -- one CholeskyQR step.  A second step re-orthogonalises it: G2 = Q1^T Q1 =
+// W W^T + lam L2^-1 L2^-T (= I in exact arithmetic, so the preconditioner is unchanged),
+// C C^T = G2, W <- C^-1 W.  At lam = 1e-10 the PCG count depends on how accurately the
+// Woodbury apply's r - W^T W r cancels (DESIGN.md 2, configs[1] at full size).
+// The second CholeskyQR step of a panel W = L2^-1 X^T (k x blk, this rank's columns) built
+// from L2 L2^T = X^T X + mu I: W is the top block of Q1 = [X; sqrt(mu) I] L2^-T, so
+// G2 = Q1^T Q1 = W W^T + mu L2^-1 L2^-T (= I in exact arithmetic), C C^T = G2, W <- C^-1 W.
+// L2: the lower factor (k x k, the same on every rank).
+int reorthogonalise_panel(mlff_ctx *ctx, double *W, const double *L2, int64_t k, double mu) {
+  ScratchScope scope(ctx);
+  hipStream_t s = ctx->stream;
+  double *Li = nullptr, *G2 = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &Li, k * k));
+  MLFF_TRY(scratch_alloc(ctx, &G2, k * k));
+  MLFF_HIP(ctx, hipMemsetAsync(Li, 0, sizeof(double) * k * k, s));
+  launch_add_diag(Li, k, 1.0, s);
+  MLFF_TRY(trsm_lower_wide(ctx, L2, k, Li, k, k));  // Li = L2^-1
+  MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G2));
+  MLFF_TRY(allreduce(ctx, G2, (size_t)(k * k)));
+  launch_gemm(false, true, k, k, k, mu, Li, k, Li, k, 1.0, G2, k, s);  // + mu Li Li^T
+  MLFF_TRY(potrf_lower(ctx, G2, k));
+  MLFF_TRY(trsm_lower_wide(ctx, G2, k, W, ctx->blk, ctx->blk));
+  return MLFF_OK;
+}
+
 int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
   ScratchScope scope(ctx);
+  hipStream_t s = ctx->stream;
   double *G = nullptr;
   MLFF_TRY(scratch_alloc(ctx, &G, k * k));
   MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
-  launch_add_diag(G, k, ctx->lam, ctx->stream);
+  launch_add_diag(G, k, ctx->lam, s);
   MLFF_TRY(potrf_lower(ctx, G, k));
   MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));
-  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->wb_refine) MLFF_TRY(reorthogonalise_panel(ctx, W, G, k, ctx->lam));
+  MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
 }
 
@@ -547,12 +579,16 @@ int nystrom_panel(mlff_ctx *ctx, const int64_t *idx_host, int64_t k, int variant
   MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));           // C^T C
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
   launch_add_diag(G, k, lam, s);
+  double shift = 0.0;
   if (variant == 0)
-    rc = cho_factor_stable(ctx, G, k, nullptr);
+    rc = cho_factor_stable(ctx, G, k, nullptr, &shift);
   else
     rc = potrf_lower(ctx, G, k);
   if (rc != MLFF_OK) return rc;
   MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));     // B = V^-T C^T
+  // B is the top block of [C; sqrt(lam + shift) I] V^-T: the same second CholeskyQR step as
+  // the Woodbury panel (MLFF_NYS_REFINE)
+  if (ctx->nys_refine) MLFF_TRY(reorthogonalise_panel(ctx, W, G, k, lam + shift));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
 }
@@ -1096,6 +1132,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
     *flag = e == nullptr || std::atoi(e) != 0;
   }
   if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_NYS_REFINE")) ctx->nys_refine = std::atoi(e) != 0;
   ctx->rank = rank;
   ctx->world = world;
   ctx->N = n_global;

@@ -343,6 +343,11 @@ struct mlff_ctx {
   // sharded tiled iteration: k_update_xr_shares folded into the next T r pass (MLFF_FUSE_XR_RANKS=1;
   // off by default: SOLO floors 4.5 us slower at W = 4, equal at W = 8)
   bool fuse_xr_ranks = false;
+  // Woodbury panel re-orthogonalised by a second CholeskyQR step (MLFF_WB_REFINE, woodbury_inplace;
+  // configs[1] at full size: 571 -> 366 iterations, the oracle's 367) and the same for the
+  // Nystrom panel (MLFF_NYS_REFINE)
+  bool wb_refine = true;
+  bool nys_refine = false;
   bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
   int lr_q = 0;                // its clusters
   double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials

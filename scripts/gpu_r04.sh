@@ -62,6 +62,10 @@ for s in ${STEPS:-suite smoke bench}; do
     diag1b) step diag1b 900 python -u scripts/dev/diag_config1b.py ;;
     diag1c) step diag1c 900 python -u scripts/dev/diag_config1c.py ;;
     diag1qr) step diag1qr 600 python -u scripts/dev/diag_config1c.py --qr ;;
+    diag1d) step diag1d 600 python -u scripts/dev/diag_config1d.py ;;
+    nysref)  # configs[2] band tests with the Nystrom panel re-orthogonalised and without
+      step nysref_on 900 env MLFF_NYS_REFINE=1 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_rbf_band.py -k "in_band or scaled"
+      step nysref_off 900 env MLFF_NYS_REFINE=0 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_rbf_band.py -k "in_band or scaled" ;;
     syevfast)  # the Nystrom build with the shifted-Cholesky-first cho_factor_stable (default) and without
       step syev_fast 600 python scripts/bench_syev.py
       step syev_nofast 900 env MLFF_CHO_FAST=0 python scripts/bench_syev.py ;;

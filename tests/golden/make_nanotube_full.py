@@ -87,20 +87,37 @@ def pivoted_cholesky_logged(get_col, diagonal, max_rank):
     return L, index_columns, piv_val, gap
 
 
+PANEL_ORDERS = ["rev", "blk8", "inverse", "noise", "rownoise"]
+
+
 def woodbury_gram_order(L, lam, order):
-    """oracle.precon.woodbury_panel (iterative_cholesky.py:141-143) with the Gram matrix L^T L
-    summed in another order: 'rev' (rows of L reversed) or 'blk8' (8 row blocks added in block
-    order).  The PCG at lam = 1e-10 is sensitive to the panel's rounding: r - T^T T r cancels
-    to O(lam / sigma^2) in the leading directions."""
+    """oracle.precon.woodbury_panel (iterative_cholesky.py:141-143) rounded another way:
+    'rev' / 'blk8': the Gram matrix L^T L summed with the rows of L reversed / in 8 row blocks;
+    'inverse': T = inv(L2) L^T (the triangular inverse, then one GEMM) instead of the
+    triangular solve; 'noise' / 'rownoise': the LAPACK panel with independent relative
+    perturbations of 2e-15 per entry / with 2e-15 (E T), E a k x k Gaussian (a perturbed L2).
+    The PCG at lam = 1e-10 is sensitive to how the panel is rounded (scripts/dev/
+    diag_config1[b,c].py): LAPACK-built panels take 364-366 iterations, the others 552-577."""
     import scipy.linalg
 
+    k = L.shape[1]
     if order == "rev":
         Lr = np.ascontiguousarray(L[::-1])
         G = Lr.T @ Lr
-    else:
+    elif order == "blk8":
         G = sum(L[b].T @ L[b] for b in np.array_split(np.arange(L.shape[0]), 8))
-    L2 = scipy.linalg.cholesky(lam * np.eye(L.shape[1]) + G, lower=True)
-    return scipy.linalg.solve_triangular(L2, L.T, lower=True)
+    else:
+        G = L.T @ L
+    L2 = scipy.linalg.cholesky(lam * np.eye(k) + G, lower=True)
+    if order == "inverse":
+        return np.tril(scipy.linalg.solve_triangular(L2, np.eye(k), lower=True)) @ L.T
+    T = scipy.linalg.solve_triangular(L2, L.T, lower=True)
+    rng = np.random.default_rng(11)
+    if order == "noise":
+        return T * (1.0 + 2e-15 * rng.standard_normal(T.shape))
+    if order == "rownoise":
+        return T + 2e-15 * ((rng.standard_normal((k, k)) / np.sqrt(k)) @ T)
+    return T
 
 
 def main(cache=None, panel_orders=()):
@@ -178,6 +195,6 @@ if __name__ == "__main__":
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--cache", default=None)
-    ap.add_argument("--panel-orders", nargs="*", default=[], choices=["rev", "blk8"])
+    ap.add_argument("--panel-orders", nargs="*", default=[], choices=PANEL_ORDERS)
     a = ap.parse_args()
     main(a.cache, a.panel_orders)
