@@ -18,11 +18,20 @@ both sides start from identical bits).
    and the panel apply (make_noise_band.kop_variant: mf, mf_rev, mf_split): the 'mf' solve is the
    reference trajectory (trace, alpha = -x), the spread of the others its noise band.
 
+3. --panel-orders: more solves of the 'mf' operator with the Woodbury panel rounded another way
+   (woodbury_gram_order): 'rev' / 'blk8' (Gram matrix in other orders) join the band; 'inverse',
+   'noise', 'rownoise' (explicit triangular inverse; 2e-15 perturbations) are recorded beside it
+   as "panel_perturbations": at lam = 1e-10 they take ~550-580 iterations against the LAPACK
+   panels' ~365 (DESIGN.md 2, configs[1] at full size).  --cache keeps L (336 MB) outside the
+   repository for such reruns.
+
 Writes tests/golden/nanotube_n15540.npz and nanotube_n15540_band.json.  CPU only: 40 min on 4
 cores (2701 operator applications for the columns, 30 min; three solves of 367 iterations); the
-reference is not imported (its algorithm is the oracle's restatement).  Recorded run: 367 / 367 /
-368 iterations, band b_it 1, b_cr 3, ||d alpha|| / ||alpha|| 2.0e-11, no near-tie among the 2701
-pivots (smallest relative gap of the best two candidates 3.1e-7).
+reference is not imported (its algorithm is the oracle's restatement).  First recorded run: 367 /
+367 / 368 iterations, band b_it 1, b_cr 3, ||d alpha|| / ||alpha|| 2.0e-11, no near-tie among the
+2701 pivots (smallest relative gap of the best two candidates 3.1e-7).  The committed fixture is
+the round-4 rerun (2 BLAS threads: L differs in its last bits, 'mf' 369 iterations) with the
+panel orders (profiles/r04/make_nanotube_full_r4.log).
 """
 from __future__ import annotations
 
@@ -120,6 +129,24 @@ def woodbury_gram_order(L, lam, order):
     return T
 
 
+# the panels the reference's own formula gives under a change of summation order (LAPACK
+# Cholesky + triangular solve): the band; the perturbed constructions are recorded beside it
+PERTURBED = ("panel_inverse", "panel_noise", "panel_rownoise")
+
+
+def band_json(n, it0, variants, gap):
+    fam = [e for o, e in variants.items() if o not in PERTURBED]
+    band = {"n": n, "k": K_RANK, "ref_order": "mf", "ref_iters": int(it0),
+            "variants": {o: e for o, e in variants.items() if o not in PERTURBED},
+            "panel_perturbations": {o: e for o, e in variants.items() if o in PERTURBED},
+            "band_iters": int(max(abs(e["d_iters"]) for e in fam)),
+            "band_crossing": int(max(e["max_d_crossing"] for e in fam)),
+            "band_rel_dalpha": float(max(e["rel_dalpha"] for e in fam)),
+            "first_gap_below_1e-12": int(np.argmax(gap < 1e-12)) if np.any(gap < 1e-12) else None,
+            "min_gap": float(gap.min())}
+    return band
+
+
 def main(cache=None, panel_orders=()):
     """cache: .npz path (outside the repository: 336 MB) holding L and the pivot log, written
     on the first run and read by later ones; panel_orders: Gram-matrix orders of the Woodbury
@@ -173,13 +200,7 @@ def main(cache=None, panel_orders=()):
         variants[order] = {"iters": int(it), "info": int(info), "d_iters": int(it - it0),
                            "max_d_crossing": int(max(dc) if dc else 0),
                            "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
-    v = variants.values()
-    band = {"n": n, "k": K_RANK, "ref_order": "mf", "ref_iters": int(it0), "variants": variants,
-            "band_iters": int(max(abs(e["d_iters"]) for e in v)),
-            "band_crossing": int(max(e["max_d_crossing"] for e in v)),
-            "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v)),
-            "first_gap_below_1e-12": int(np.argmax(gap < 1e-12)) if np.any(gap < 1e-12) else None,
-            "min_gap": float(gap.min())}
+    band = band_json(n, it0, variants, gap)
     np.savez_compressed(GOLDEN / "nanotube_n15540.npz", R=R, y=y, index_columns=piv[:K_RANK],
                         pivot_values=piv_val, pivot_gap=gap, trace=tr0, iters=np.int64(it0),
                         info=np.int64(info0), alphas=-x0)
@@ -187,6 +208,7 @@ def main(cache=None, panel_orders=()):
     print(json.dumps({q: band[q] for q in ("ref_iters", "band_iters", "band_crossing",
                                            "band_rel_dalpha", "first_gap_below_1e-12", "min_gap")}),
           flush=True)
+    print(json.dumps({o: e["iters"] for o, e in band["panel_perturbations"].items()}), flush=True)
     print(f"total {time.time() - t_all:.0f} s", flush=True)
 
 

@@ -320,8 +320,10 @@ def test_record_kernel_point_groups_bitwise(sg, monkeypatch, M):
     """k_rec_g with 8-point groups (the default for one identity permutation), 4-point groups
     and the round-2 16-point groups (MLFF_REC_RG), with the w / x stage as one 16-slot chunk
     or a 32-slot one (MLFF_REC_WC16), computes the same sums in the same order: operator
-    outputs and a short PCG are bit-identical.  M = 17 exceeds one 16-point group (the Zt-table
-    path, the same kernel for every setting)."""
+    outputs and a short PCG's iterates are bit-identical.  M = 17 exceeds one 16-point group
+    (the Zt-table path, the same kernel for every setting).  The residual curve is bitwise too
+    except where the default 8-point form runs the four-launch iteration (x and r
+    the same bits, the ||r||^2 partials summed in another fixed order): there within 2 ulp."""
     from sgdml_amd import synthetic
 
     ds = synthetic.nanotube_like(M, seed=2)
@@ -344,8 +346,12 @@ def test_record_kernel_point_groups_bitwise(sg, monkeypatch, M):
     monkeypatch.delenv("MLFF_REC_RG")
     monkeypatch.delenv("MLFF_REC_WC16")
     for key in ("rg8", "rg4", "rg8wc32"):
-        for a, b in zip(out[key], out["rg16"]):
-            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(out[key][0], out["rg16"][0])
+        np.testing.assert_array_equal(out[key][2], out["rg16"][2])
+        if key == "rg8":
+            np.testing.assert_allclose(out[key][1], out["rg16"][1], rtol=4.5e-16, atol=0)
+        else:
+            np.testing.assert_array_equal(out[key][1], out["rg16"][1])
 
 
 def _molecule(n_atoms, M, seed):
