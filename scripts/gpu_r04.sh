@@ -90,6 +90,9 @@ for s in ${STEPS:-suite smoke bench}; do
       step syev_prof 900 rocprofv3 --kernel-trace --stats -d $O/syev -o syev --output-format csv -- python3 scripts/bench_syev.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
     pmc) step pmc 900 python scripts/pmc_head.py --out $O/pmc_head ;;
+    parity)  # the drop-in on every golden solve, Woodbury panel in two CholeskyQR steps (default) and in one
+      step parity_refine 600 python scripts/parity_report.py
+      step parity_onestep 600 env MLFF_WB_REFINE=0 python scripts/parity_report.py ;;
     pmcrg)  # nanotube operator traffic with one 16-point group per pair block (each Rdd block read
             # by one workgroup) against the default two 8-point groups
       step pmc_rg16 600 env MLFF_REC_RG=16 python scripts/pmc_head.py --out $O/pmc_rg16 --workloads nanotube

@@ -200,7 +200,11 @@ def test_config1_full_size_against_oracle_fixture(sg, golden_dir):
     * pivots: identical up to the first near-tie of the oracle's residual diagonal (SURVEY 8(c):
       relative gap between the best two candidates < 1e-12); every pivot when there is none;
     * solve: iterations, residual trace and alpha under the tests/parity.py band rule with the
-      band the oracle measured on this system (three summation orders of its operator)."""
+      band the oracle measured on this system (three summation orders of its operator, two of
+      its Woodbury panel's Gram matrix: 366-369 iterations).  The fixture also records panels
+      rounded differently (explicit inverse, 2e-15 perturbations: 564-578 iterations,
+      "panel_perturbations"); the device's one-step panel fell there (571), its re-orthogonalised
+      panel (the default) is held to the band."""
     import json
 
     from oracle.sgdml import descriptors
