@@ -364,7 +364,12 @@ def rbf_band():
         f = np.load(g / "rbf_solve_n65536.npz", allow_pickle=False)
         full = {"iters": int(f["iters"]), "info": int(f["info"]),
                 "final_true_relres": float(f["final_relres"]), "x_norm": float(f["x_norm"]),
-                "cpu_seconds": float(f["seconds"])}
+                "cpu_seconds": float(f["seconds"]), "_x": f["x"]}
+        if (g / "rbf_solve_n65536_rev.npz").exists():  # a second summation order of the oracle
+            fr = np.load(g / "rbf_solve_n65536_rev.npz", allow_pickle=False)
+            full["second_order_iters"] = int(fr["iters"])
+            full["second_order_rel_dx"] = float(np.linalg.norm(fr["x"] - f["x"]) /
+                                                np.linalg.norm(f["x"]))
     return bd, full
 
 
@@ -712,10 +717,18 @@ def main():
         if sg_info is None and n == 65536 and k == 256 and full is not None and bd is not None:
             # the CPU oracle's solve of this very system (committed fixture, ~2 h of CPU time:
             # make_rbf_band.py --full), held to the N = 8192 band scaled by the count
-            b_it = int(np.ceil(bd["band_iters"] * full["iters"] / bd["ref_iters"]))
+            scale = full["iters"] / bd["ref_iters"]
+            b_it = int(np.ceil(bd["band_iters"] * scale))
+            x_cpu = full.pop("_x")
             solve["cpu_ref"] = dict(full, source="tests/golden/rbf_solve_n65536.npz")
             solve["band_iters_scaled"] = b_it
-            solve["in_band"] = bool(abs(res.iters - full["iters"]) <= 2 * b_it + 2)
+            ok = abs(res.iters - full["iters"]) <= 2 * b_it + 2
+            if world == 1:  # ||dx|| / ||x|| against the oracle's x, and its scaled band
+                solve["rel_dx_vs_cpu_ref"] = float(np.linalg.norm(res.x - x_cpu) /
+                                                   np.linalg.norm(x_cpu))
+                solve["band_rel_dx_scaled"] = float(bd["band_rel_dx"] * max(1.0, scale))
+                ok = ok and solve["rel_dx_vs_cpu_ref"] <= 10 * solve["band_rel_dx_scaled"]
+            solve["in_band"] = bool(ok)
 
     out = None
     if rank == 0:

@@ -62,8 +62,12 @@ def kname(full: str) -> str:
 
 
 def matches(full: str, want: str) -> bool:
+    """'k_gemv<4, 2, 0>' matches k_gemv<4, 2, 0> and its instantiations with further template
+    arguments (k_gemv<4, 2, 0, false>: the load-policy flag of a panel that fits the MALL)."""
     k = kname(full)
-    return k == want if "<" in want else re.sub(r"<.*", "", k) == want
+    if "<" in want:
+        return k == want or k.startswith(want[:-1] + ",")
+    return re.sub(r"<.*", "", k) == want
 
 
 # counters are collected for the measured groups' kernels only (the builds launch ~20k other
