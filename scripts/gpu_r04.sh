@@ -63,6 +63,15 @@ for s in ${STEPS:-suite smoke bench}; do
     diag1c) step diag1c 900 python -u scripts/dev/diag_config1c.py ;;
     diag1qr) step diag1qr 600 python -u scripts/dev/diag_config1c.py --qr ;;
     diag1d) step diag1d 600 python -u scripts/dev/diag_config1d.py ;;
+    lcrr)  # cluster apply: held row (D = 2) vs re-read row (D = 4 / 6 / 8), interleaved, at the
+           # reference's large published points (ethanol N = 74979 / 157491, nanotube N = 156510)
+      for rep in 1 2; do
+        for D in 0 4 6 8; do
+          step lcrr_eth5833_D${D}_r$rep 300 env MLFF_LC_REREAD=$D $EB --m 5833 --storage matfree --steps 20
+          step lcrr_eth2777_D${D}_r$rep 300 env MLFF_LC_REREAD=$D $EB --m 2777 --storage matfree --steps 20
+          step lcrr_nt141_D${D}_r$rep 300 env MLFF_LC_REREAD=$D python bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
+        done
+      done ;;
     nysref)  # configs[2] band tests with the Nystrom panel re-orthogonalised and without
       step nysref_on 900 env MLFF_NYS_REFINE=1 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_rbf_band.py -k "in_band or scaled"
       step nysref_off 900 env MLFF_NYS_REFINE=0 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread tests/test_gpu_rbf_band.py -k "in_band or scaled" ;;

@@ -236,3 +236,4 @@ def test_config1_full_size_against_oracle_fixture(sg, golden_dir):
           f"{ {o: v['iters'] for o, v in band['variants'].items()} })")
     assert_pcg_parity(res.iters, res.trace[1:], -res.x, int(f["iters"]), f["trace"][1:],
                       f["alphas"], band=band)
+
