@@ -402,6 +402,9 @@ def parity_small(n, k, lam, ell, tol=1e-6):
         out["band"] = {"b_iters": bd["band_iters"], "b_rel_dx": bd["band_rel_dx"],
                        "oracle_orders": {o: v["iters"] for o, v in bd["variants"].items()},
                        "source": "tests/golden/rbf_band_n8192.json"}
+        ld = REPO / "tests" / "golden" / f"rbf_ld_n{n}.json"
+        if ld.exists():  # the oracle with extended-precision sums: the exact-arithmetic proxy
+            out["band"]["extended_precision_iters"] = json.loads(ld.read_text())["iters"]
         out["in_band"] = bool(abs(r.iters - it) <= 2 * bd["band_iters"] + 2
                               and out["rel_dx"] <= 10 * bd["band_rel_dx"])
     return out

@@ -73,6 +73,11 @@ def test_configs2_in_band(golden_dir, n):
     crossings_ok(r.trace[1:], ref_tr[1:], 2 * bd["band_crossing"] + 2)
     rel = np.linalg.norm(r.x - ref_x) / np.linalg.norm(ref_x)
     assert rel <= 10 * bd["band_rel_dx"], rel
+    ld = golden_dir / f"rbf_ld_n{n}.json"
+    if ld.exists():  # the oracle in extended precision: another sample, the exact-arithmetic proxy
+        it_ld = json.loads(ld.read_text())["iters"]
+        print(f"N={n}: extended-precision oracle {it_ld} iterations")
+        assert abs(r.iters - it_ld) <= 2 * bd["band_iters"] + 2, (r.iters, it_ld)
 
 
 def test_configs2_n65536_in_scaled_band(golden_dir):
