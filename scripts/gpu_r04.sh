@@ -63,6 +63,13 @@ for s in ${STEPS:-suite smoke bench}; do
     diag1c) step diag1c 900 python -u scripts/dev/diag_config1c.py ;;
     diag1qr) step diag1qr 600 python -u scripts/dev/diag_config1c.py --qr ;;
     diag1d) step diag1d 600 python -u scripts/dev/diag_config1d.py ;;
+    headlines)  # every bench line at HEAD: ethanol at the reference's published sizes (pair-tile),
+                # nanotube configs[1] and the N = 156510 point
+      for m in 583 2777 5833; do
+        step head_eth_m$m 600 python bench.py --workload ethanol --m $m --no-cpu --steps 30 --warmup 3
+      done
+      step head_nt 300 python bench.py --workload nanotube
+      step head_nt141 600 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
     lcrr)  # cluster apply: held row (D = 2) vs re-read row (D = 4 / 6 / 8), interleaved, at the
            # reference's large published points (ethanol N = 74979 / 157491, nanotube N = 156510)
       for rep in 1 2; do
