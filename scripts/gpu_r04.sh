@@ -70,6 +70,9 @@ for s in ${STEPS:-suite smoke bench}; do
       done
       step head_nt 300 python bench.py --workload nanotube
       step head_nt141 600 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
+    ethsolve)  # ethanol N = 15741 solve to 1e-6 with the Woodbury panel in two CholeskyQR steps and in one
+      step ethsolve_refine 300 python bench.py --workload ethanol --m 583 --no-cpu --steps 10 --warmup 2 --solve-maxiter 80000
+      step ethsolve_onestep 300 env MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --no-cpu --steps 10 --warmup 2 --solve-maxiter 80000 ;;
     lcrr)  # cluster apply: held row (D = 2) vs re-read row (D = 4 / 6 / 8), interleaved, at the
            # reference's large published points (ethanol N = 74979 / 157491, nanotube N = 156510)
       for rep in 1 2; do
