@@ -722,6 +722,16 @@ def main():
             # make_rbf_band.py --full), held to the N = 8192 band scaled by the count
             scale = full["iters"] / bd["ref_iters"]
             b_it = int(np.ceil(bd["band_iters"] * scale))
+            # the band's growth measured at 8192 / 16384 / 32768 (b_it / iters linear in
+            # log2 N, tests/golden/make_rbf_band.py), extrapolated to this N
+            g = REPO / "tests" / "golden"
+            pts = [(np.log2(m), json.loads((g / f"rbf_band_n{m}.json").read_text()))
+                   for m in (8192, 16384, 32768) if (g / f"rbf_band_n{m}.json").exists()]
+            if len(pts) >= 2:
+                c = np.polyfit([p[0] for p in pts],
+                               [p[1]["band_iters"] / p[1]["ref_iters"] for p in pts], 1)
+                solve["band_fraction_extrapolated"] = float(np.polyval(c, np.log2(n)))
+                b_it = max(b_it, int(np.ceil(solve["band_fraction_extrapolated"] * full["iters"])))
             x_cpu = full.pop("_x")
             solve["cpu_ref"] = dict(full, source="tests/golden/rbf_solve_n65536.npz")
             solve["band_iters_scaled"] = b_it

@@ -70,6 +70,9 @@ for s in ${STEPS:-suite smoke bench}; do
       done
       step head_nt 300 python bench.py --workload nanotube
       step head_nt141 600 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
+    calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
+      step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
+      step calib_fetch 60 rocprofv3 --pmc FETCH_SIZE -d $O/calib -o calib --output-format csv -- $O/pmc_calib ;;
     ethsolve)  # ethanol N = 15741 solve to 1e-6 with the Woodbury panel in two CholeskyQR steps and in one
       step ethsolve_refine 300 python bench.py --workload ethanol --m 583 --no-cpu --steps 10 --warmup 2 --solve-maxiter 80000
       step ethsolve_onestep 300 env MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --no-cpu --steps 10 --warmup 2 --solve-maxiter 80000 ;;

@@ -53,10 +53,11 @@ def crossings_ok(tr, ref_tr, slack):
         assert abs(ia - ib) <= slack, (lvl, ia, ib, slack)
 
 
-@pytest.mark.parametrize("n", [8192, 16384])
+@pytest.mark.parametrize("n", [8192, 16384, 32768])
 def test_configs2_in_band(golden_dir, n):
-    """N = 8192 and 16384: the measured six-order band of that size (the band grows faster than
-    the count: b_it 95 of 2963 at 8192, see rbf_band_n16384.json for 16384)."""
+    """N = 8192, 16384, 32768: the measured band of that size (six oracle orders; four at 32768).
+    The band grows faster than the count: b_it 95 of 2963 (3.2 %), 176 of 4700 (3.7 %), 266 of
+    6174 (4.3 %)."""
     if not (golden_dir / f"rbf_band_n{n}.json").exists():
         pytest.fail(f"tests/golden/rbf_band_n{n}.json missing (make_rbf_band.py --band --n {n})")
     bd = band(golden_dir, n)
@@ -93,6 +94,18 @@ def test_configs2_n65536_in_scaled_band(golden_dir):
     scale = ref_it / bd["ref_iters"]
     b_it = int(np.ceil(bd["band_iters"] * scale))
     b_cr = int(np.ceil(bd["band_crossing"] * scale))
+    # the band's growth with N, measured at 8192 / 16384 / 32768 (b_it / iters linear in log2 N),
+    # extrapolated to 65536
+    pts = []
+    for m in (8192, 16384, 32768):
+        if (golden_dir / f"rbf_band_n{m}.json").exists():
+            bm = band(golden_dir, m)
+            pts.append((np.log2(m), bm["band_iters"] / bm["ref_iters"]))
+    if len(pts) >= 2:
+        c = np.polyfit([p[0] for p in pts], [p[1] for p in pts], 1)
+        frac = float(np.polyval(c, np.log2(n)))
+        print(f"N={n}: band fraction extrapolated from {len(pts)} sizes: {frac:.4f}")
+        b_it = max(b_it, int(np.ceil(frac * ref_it)))
     rev = golden_dir / "rbf_solve_n65536_rev.npz"
     if rev.exists():  # the oracle's second summation order at this size: its spread, measured
         fr = np.load(rev, allow_pickle=False)
