@@ -70,6 +70,9 @@ for s in ${STEPS:-suite smoke bench}; do
       done
       step head_nt 300 python bench.py --workload nanotube
       step head_nt141 600 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
+    nt141ab)  # nanotube N = 156510 solve to 1e-6 with the Woodbury panel in one CholeskyQR step (the
+              # default two-step line is headlines/head_nt141)
+      step nt141_onestep 600 env MLFF_WB_REFINE=0 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
