@@ -457,11 +457,43 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out,
     }
   }
   double lo = 0.0;
-  MLFF_TRY(sym_min_eig(ctx, A, k, &lo, nullptr, nullptr));
+  std::vector<double> d((size_t)k), e((size_t)(k > 1 ? k - 1 : 0));
+  MLFF_TRY(sym_min_eig(ctx, A, k, &lo, d.data(), e.data()));
+  // |lo| <= 2 eps ||M|| (||M|| bounded by Gershgorin on the tridiagonal, which is similar to M):
+  // eigh's own rounding (~eps ||M||, tests/golden/cho_stable_ethanol.npz delta = 0) decides the
+  // sign there, so the device's sign may differ from LAPACK's.  When such a lo > 0 makes the
+  // downward shift fail, the upward one the reference takes for lo <= 0 is tried before
+  // LinAlgError.  (The fixture's lo = 1.26e-16 at ||M|| ~ 0.03 is 20x above the bound and still
+  // raises like the reference.)  MLFF_CHO_TEST_NOISY_POSITIVE=1: a noisy lo is taken as > 0
+  // (the test of this retry; never set in production).
+  double gersh = 0.0;
+  for (int64_t i = 0; i < k; ++i)
+    gersh = std::max(gersh, std::fabs(d[i]) + (i > 0 ? std::fabs(e[i - 1]) : 0.0) +
+                                (i + 1 < k ? std::fabs(e[i]) : 0.0));
+  const bool noisy = std::fabs(lo) <= 2.0 * std::numeric_limits<double>::epsilon() * gersh;
+  if (noisy && lo <= 0.0) {
+    const char *t = std::getenv("MLFF_CHO_TEST_NOISY_POSITIVE");
+    if (t != nullptr && std::atoi(t) == 1) lo = std::fabs(lo) > 0.0 ? std::fabs(lo) : 1e-300;
+  }
   ctx->last_lo_eig = lo;
   if (lo_eig_out) *lo_eig_out = lo;
-  launch_add_diag(A, k, lo <= 0.0 ? 1e-15 : -1e-15, ctx->stream);
-  if (shift_out) *shift_out = lo <= 0.0 ? 1e-15 : -1e-15;
+  if (!(noisy && lo > 0.0)) {
+    launch_add_diag(A, k, lo <= 0.0 ? 1e-15 : -1e-15, ctx->stream);
+    if (shift_out) *shift_out = lo <= 0.0 ? 1e-15 : -1e-15;
+    return potrf_lower(ctx, A, k);
+  }
+  ScratchScope scope(ctx);
+  double *keep = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &keep, (size_t)(k * k)));
+  MLFF_HIP(ctx, hipMemcpyAsync(keep, A, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+  launch_add_diag(A, k, -1e-15, ctx->stream);
+  bool ok = false;
+  MLFF_TRY(potrf_lower(ctx, A, k, &ok));
+  if (ok) return MLFF_OK;
+  MLFF_HIP(ctx, hipMemcpyAsync(A, keep, sizeof(double) * k * k, hipMemcpyDeviceToDevice, ctx->stream));
+  launch_add_diag(A, k, 1e-15, ctx->stream);
+  if (shift_out) *shift_out = 1e-15;
+  ctx->cho_flipped = true;
   return potrf_lower(ctx, A, k);
 }
 

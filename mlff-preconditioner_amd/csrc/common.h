@@ -356,6 +356,7 @@ struct mlff_ctx {
   int *lr_fault = nullptr;     // ST_FAULT when a cluster hand-off timed out (precon_apply)
   int lr_fallbacks = 0;        // cluster applies that timed out and fell back to two passes
   double last_lo_eig = 0.0;
+  bool cho_flipped = false;  // a cho_factor_stable retried upward after a noisy lo > 0
   bool eig_converged = true;   // last truncated eigensolve met kEigTol (kernels_eig.hip)
   double eig_rel_resid = 0.0;  // its worst Ritz residual / |theta_0|    // lo_eig of the last _cho_factor_stable (cho_factor_stable)
   double *tpart = nullptr;       // = tpart_base + kVecGrid

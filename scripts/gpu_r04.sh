@@ -73,6 +73,16 @@ for s in ${STEPS:-suite smoke bench}; do
     nt141ab)  # nanotube N = 156510 solve to 1e-6 with the Woodbury panel in one CholeskyQR step (the
               # default two-step line is headlines/head_nt141)
       step nt141_onestep 600 env MLFF_WB_REFINE=0 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3 ;;
+    lr1024)  # one-pass panel apply with 1024-thread workgroups (8 double2 per thread, 4 waves per
+             # SIMD) vs 512 (16 double2, 2 waves per SIMD), interleaved; then the parity tests under it
+      for rep in 1 2; do
+        for T in 512 1024; do
+          step lr${T}_nt_r$rep 300 env MLFF_LR_THREADS=$T python bench.py --workload nanotube --no-cpu --steps 200 --warmup 20
+          step lr${T}_eth_r$rep 300 env MLFF_LR_THREADS=$T python bench.py --workload ethanol --m 583 --no-cpu --steps 200 --warmup 20 --no-solve
+        done
+      done
+      step lr1024_prof 300 env MLFF_LR_THREADS=1024 rocprofv3 --kernel-trace --stats -d $O/lr1024prof -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --steps 200 --warmup 20 --no-solve
+      step lr1024_tests 600 env MLFF_LR_THREADS=1024 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py tests/test_gpu_fused_iteration.py && step cho_tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_cho_stable.py ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib

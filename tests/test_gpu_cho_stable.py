@@ -107,6 +107,34 @@ def test_cho_factor_stable_raises_like_the_reference(sg):
             s.cho_factor_stable(M)
 
 
+@pytest.mark.parametrize("force_positive", ["0", "1"])
+def test_cho_factor_stable_noisy_sign_retries_upward(sg, monkeypatch, force_positive):
+    """An exactly singular PSD M (a duplicated inducing column, ||M|| = 1e-2): lo_eig is at
+    eigh's rounding level (|lo| <= 2 eps ||M||), where the sign is noise in the reference itself
+    (its duplicate fixture: -2.2e-18).  With lo read as > 0 the downward shift leaves an
+    eigenvalue of -1e-15, far above the Cholesky's backward error (~m eps ||M|| = 1e-16) -- it
+    fails, and the factor must come from the upward shift (the reference's lo <= 0 branch)
+    instead of LinAlgError.  force_positive = "1": the device's noisy lo is taken as
+    positive (MLFF_CHO_TEST_NOISY_POSITIVE), so the retry runs whatever sign it computed."""
+    m, i, j = 40, 5, 23
+    M = spd_with_spectrum(m, 1e-4, 1e-2, seed=11)
+    M = np.tril(M) + np.tril(M, -1).T
+    M[:, j] = M[:, i]
+    M[j, :] = M[i, :]
+    assert np.array_equal(M, M.T)
+    monkeypatch.setenv("MLFF_CHO_TEST_NOISY_POSITIVE", force_positive)
+    with sg.KernelSolver(8) as s:
+        L, lo = s.cho_factor_stable(M)
+    assert abs(lo) <= 2 * EPS * 1e-2 * 3, lo
+    if force_positive == "1":
+        assert lo > 0
+    with pytest.raises(np.linalg.LinAlgError):
+        scipy.linalg.cho_factor(M - 1e-15 * np.eye(m))
+    Ms = M + 1e-15 * np.eye(m)
+    np.testing.assert_array_equal(np.triu(L, 1), 0.0)
+    assert np.abs(L @ L.T - Ms).max() <= 8 * m * EPS * 1e-2
+
+
 def _solver_for(sg, f, t):
     R = f[f"R_{t}"]
     M_pts, n_atoms = R.shape[:2]
