@@ -398,24 +398,14 @@ int lr_rows_groups(int64_t k) {
 // (no bounds test, no 64-bit address per load).  aux 2 = non-temporal.
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
-template <int M, int AUX, int NTH = kLrThreads>
+template <int M, int AUX>
 __device__ __forceinline__ void lr_load_row(d2 (&buf)[M], const double *row, int bytes) {
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(row), 0, bytes, 0x00020000);
   const int voff = (int)threadIdx.x * 16;
 #pragma unroll
   for (int m = 0; m < M; ++m)
-    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * NTH * 16, AUX));
-}
-
-// the NTH / 64 wave sums of a row in a fixed order: pairs, then pairs of pairs, ...
-template <int NW>
-__device__ __forceinline__ double lr_wave_tree(const double *q) {
-  if constexpr (NW == 1) {
-    return q[0];
-  } else {
-    return lr_wave_tree<NW / 2>(q) + lr_wave_tree<NW / 2>(q + NW / 2);
-  }
+    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * kLrThreads * 16, AUX));
 }
 
 // Registers per lane: the row being reduced (cur), the next row in flight (nxt) and r, M
@@ -423,12 +413,11 @@ __device__ __forceinline__ double lr_wave_tree(const double *q) {
 // thread (z_sh[m * kLrThreads + tid]), so no barrier guards them.
 // Row i (in cur): t_i, z_sh += cur t_i; row i + 1 loaded into nxt first (a descriptor of
 // zero bytes past the last row: the loads return zeros and move nothing).
-template <int M, int AUX, int NTH = kLrThreads>
+template <int M, int AUX>
 __device__ __forceinline__ void lr_row_step(d2 (&cur)[M], d2 (&nxt)[M], const d2 (&rv)[M],
                                             d2 *z_sh, const double *__restrict__ T, int64_t ldt,
                                             int64_t i, int64_t i0, int64_t i1, double *red) {
-  constexpr int NW = NTH / 64;
-  lr_load_row<M, AUX, NTH>(nxt, T + (i + 1 < i1 ? i + 1 : i) * ldt, i + 1 < i1 ? (int)(ldt * 8) : 0);
+  lr_load_row<M, AUX>(nxt, T + (i + 1 < i1 ? i + 1 : i) * ldt, i + 1 < i1 ? (int)(ldt * 8) : 0);
   double a0 = 0.0, a1 = 0.0;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -437,51 +426,50 @@ __device__ __forceinline__ void lr_row_step(d2 (&cur)[M], d2 (&nxt)[M], const d2
   }
   const double s = wave_sum(a0 + a1);
   const int p = (int)((i - i0) & 1);  // two slot sets: one barrier per row suffices
-  if ((threadIdx.x & 63) == 0) red[p * NW + (threadIdx.x >> 6)] = s;
+  if ((threadIdx.x & 63) == 0) red[p * 8 + (threadIdx.x >> 6)] = s;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  // (NTH = 512: ((q0 + q1) + (q2 + q3)) + ((q4 + q5) + (q6 + q7)), the original order)
-  const double t = lr_wave_tree<NW>(red + p * NW);
+  static_assert(kLrThreads == 512, "eight wave sums per row");
+  const double *q = red + p * 8;
+  const double t = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
 #pragma unroll
   for (int m = 0; m < M; m += 4) {
 #pragma unroll
     for (int u = 0; u < 4 && m + u < M; ++u) {
-      d2 zv = z_sh[threadIdx.x + NTH * (m + u)];
+      d2 zv = z_sh[threadIdx.x + kLrThreads * (m + u)];
       zv.x = fma(cur[m + u].x, t, zv.x);
       zv.y = fma(cur[m + u].y, t, zv.y);
-      z_sh[threadIdx.x + NTH * (m + u)] = zv;
+      z_sh[threadIdx.x + kLrThreads * (m + u)] = zv;
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // the workgroup's rows [i0, i1), all read with one load policy (AUX)
-template <int M, int AUX, int NTH = kLrThreads>
+template <int M, int AUX>
 __device__ __forceinline__ bool lr_rows_loop(const d2 (&rv)[M], d2 *z_sh,
                                              const double *__restrict__ T, int64_t ldt,
                                              int64_t i0, int64_t i1, double *red,
                                              const StopFold &fold) {
   d2 A[M], B[M];
-  lr_load_row<M, AUX, NTH>(A, T + i0 * ldt, i0 < i1 ? (int)(ldt * 8) : 0);
+  lr_load_row<M, AUX>(A, T + i0 * ldt, i0 < i1 ? (int)(ldt * 8) : 0);
   // the stop test of the previous iteration while the first row is in flight (every
   // thread reaches the same decision; false: the solver stopped)
   if (!stop_prologue_wide(fold, red)) return false;
 #pragma unroll
-  for (int m = 0; m < M; ++m) z_sh[threadIdx.x + NTH * m] = d2{0.0, 0.0};
+  for (int m = 0; m < M; ++m) z_sh[threadIdx.x + kLrThreads * m] = d2{0.0, 0.0};
   int64_t i = i0;
   for (; i + 1 < i1; i += 2) {
-    lr_row_step<M, AUX, NTH>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
-    lr_row_step<M, AUX, NTH>(B, A, rv, z_sh, T, ldt, i + 1, i0, i1, red);
+    lr_row_step<M, AUX>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
+    lr_row_step<M, AUX>(B, A, rv, z_sh, T, ldt, i + 1, i0, i1, red);
   }
-  if (i < i1) lr_row_step<M, AUX, NTH>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
+  if (i < i1) lr_row_step<M, AUX>(A, B, rv, z_sh, T, ldt, i, i0, i1, red);
   return true;
 }
 
-// NTH = 1024 (MLFF_LR_THREADS=1024, A/B): 16 waves with M / 2 double2 each, so 4 waves per SIMD
-// hold the two row buffers and r in ~110 registers instead of 2 waves in 224
-template <int M, int NTH = kLrThreads>
-__global__ __launch_bounds__(NTH) void k_lr_rows(const double *__restrict__ T, int64_t ldt,
+template <int M>
+__global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict__ T, int64_t ldt,
                                                         int64_t k, int rpw,
                                                         const double *__restrict__ r,
                                                         double *__restrict__ zpart,
@@ -489,20 +477,20 @@ __global__ __launch_bounds__(NTH) void k_lr_rows(const double *__restrict__ T, i
                                                         const int *__restrict__ status,
                                                         StopFold fold, XrFold xf) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ d2 z_sh[M * NTH];
-  __shared__ double red[2 * (NTH / 64) > 16 ? 2 * (NTH / 64) : 16];
+  __shared__ d2 z_sh[M * kLrThreads];
+  __shared__ double red[16];
   const int bytes = (int)(ldt * 8);
   const int64_t i0 = (int64_t)blockIdx.x * rpw;
   const int64_t i1 = i0 + rpw < k ? i0 + rpw : k;
   // r and the first row are requested before the stop test of the previous iteration
   // (its partials' round trip then overlaps them; a stopped solver drops them unused)
   d2 rv[M];
-  lr_load_row<M, 0, NTH>(rv, r, bytes);  // zeros beyond ldt
+  lr_load_row<M, 0>(rv, r, bytes);  // zeros beyond ldt
   if (xf.x != nullptr) {
     // the residual of the previous iteration, r - alpha q (k_update_xr's arithmetic), before
     // the first row is requested (q, r and a row in registers at once would spill)
     d2 qv[M];
-    lr_load_row<M, 0, NTH>(qv, xf.q, bytes);
+    lr_load_row<M, 0>(qv, xf.q, bytes);
     const double rho = xf.st->rho;
     const double pq = reduce_parts_bcast_wide(xf.pq_part, kVecGrid, red);
     const double alpha = rho / pq;
@@ -516,16 +504,16 @@ __global__ __launch_bounds__(NTH) void k_lr_rows(const double *__restrict__ T, i
       rv[m].y = fma(-alpha, qv[m].y, rv[m].y);
     }
   }
-  const bool go = blockIdx.x < cached_wgs ? lr_rows_loop<M, 0, NTH>(rv, z_sh, T, ldt, i0, i1, red, fold)
-                                           : lr_rows_loop<M, 2, NTH>(rv, z_sh, T, ldt, i0, i1, red, fold);
+  const bool go = blockIdx.x < cached_wgs ? lr_rows_loop<M, 0>(rv, z_sh, T, ldt, i0, i1, red, fold)
+                                           : lr_rows_loop<M, 2>(rv, z_sh, T, ldt, i0, i1, red, fold);
   if (!go) return;
   const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
       zpart + (int64_t)blockIdx.x * ldt, 0, bytes, 0x00020000);
   const int voff = (int)threadIdx.x * 16;
 #pragma unroll
   for (int m = 0; m < M; ++m)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + NTH * m]),
-                                           out, voff, m * NTH * 16, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + kLrThreads * m]),
+                                           out, voff, m * kLrThreads * 16, 0);
 }
 
 // z[j] = sigma_p lam_inv (r[j] - sum_{g < G} zpart[g, j]) for j < n, the G partials in
@@ -937,15 +925,7 @@ void launch_lr_apply_rows(const double *T, int64_t ldt, int64_t k, const double 
   int cached = panel_streams(k, ldt) ? (int)(panel_cached_rows(k, ldt) / rpw) : G;
   if (const char *e = std::getenv("MLFF_LR_CACHE_WGS")) cached = std::atoi(e);
   const dim3 grid((unsigned)G);
-  static const int nth = [] {
-    const char *e = std::getenv("MLFF_LR_THREADS");
-    return e != nullptr && std::atoi(e) == 1024 ? 1024 : 512;
-  }();
-  if (nth == 1024 && n2 > 12 * kLrThreads)  // 16 double2 per thread at 512 -> 8 at 1024
-    hipLaunchKernelGGL((k_lr_rows<8, 1024>), grid, dim3(1024), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
-  else if (nth == 1024 && n2 > 8 * kLrThreads)
-    hipLaunchKernelGGL((k_lr_rows<6, 1024>), grid, dim3(1024), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
-  else if (n2 <= 4 * kLrThreads)
+  if (n2 <= 4 * kLrThreads)
     hipLaunchKernelGGL(k_lr_rows<4>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
   else if (n2 <= 8 * kLrThreads)
     hipLaunchKernelGGL(k_lr_rows<8>, grid, dim3(kLrThreads), 0, s, T, ldt, k, rpw, r, zpart, cached, status, fold, xf);
