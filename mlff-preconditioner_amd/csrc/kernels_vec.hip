@@ -5,6 +5,7 @@
 // Reference semantics: scipy 1.7.3 CGREVCOM + python wrapper as called from
 // src/sGDML/sgdml/solvers/iterative_solver.py:995-1005; preconditioner applies
 // iterative_cholesky.py:145-148, iterative_solver.py:315-318 and :376-379.
+#include <cstdio>
 #include <cstring>
 
 #include "common.h"
@@ -649,14 +650,15 @@ constexpr int kLcMaxC = 44;  // members per cluster.  Apply time against two pas
                              // (the hand-off of the slowest of C members paces each step)
 constexpr int kLcD = 2, kLcL = 1;
 
-__device__ __forceinline__ void lc_load(d2 (&buf)[kLcM], const double *T, int64_t ldt,
+template <int M>
+__device__ __forceinline__ void lc_load(d2 (&buf)[M], const double *T, int64_t ldt,
                                         int64_t row, int64_t i1, int64_t c0, int segbytes) {
   const bool ok = row < i1;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<double *>(T + (ok ? row : 0) * ldt + c0), 0, ok ? segbytes : 0, 0x00020000);
   const int voff = (int)threadIdx.x * 16;
 #pragma unroll
-  for (int m = 0; m < kLcM; ++m)
+  for (int m = 0; m < M; ++m)
     buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * kLcThreads * 16, 2));
 }
 
@@ -711,9 +713,9 @@ __device__ __forceinline__ bool lc_consume(const LcArgs &a, int row, unsigned lo
 // (loading); the rows between wait for their partials or are in flight.  The sync
 // wave (8) polls, sums and publishes: its hand-off loads never queue behind row loads, and
 // the row waves' code holds no hand-off load a counter wait could be charged for.
-template <int D, int L>
-__device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[kLcM],
-                                            d2 (&b2)[kLcM], d2 (&b3)[kLcM], const d2 *r_sh,
+template <int D, int L, int M>
+__device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[M],
+                                            d2 (&b2)[M], d2 (&b3)[M], const d2 *r_sh,
                                             d2 *z_sh, double *red, const double *tsh,
                                             const int *bail) {
   const int w = threadIdx.x >> 6;
@@ -722,7 +724,7 @@ __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[kLc
   if (jp >= a.i0 && jp < a.i1) {
     double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-    for (int m = 0; m < kLcM; ++m) {
+    for (int m = 0; m < M; ++m) {
       const d2 rv = r_sh[threadIdx.x + kLcThreads * m];
       a0 = fma(b2[m].x, rv.x, a0);
       a1 = fma(b2[m].y, rv.y, a1);
@@ -735,7 +737,7 @@ __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[kLc
   if (j >= a.i0 && j < a.i1) {
     const double t = tsh[j & 1];
 #pragma unroll
-    for (int m = 0; m < kLcM; ++m) {
+    for (int m = 0; m < M; ++m) {
       d2 zv = z_sh[threadIdx.x + kLcThreads * m];
       zv.x = fma(b0[m].x, t, zv.x);
       zv.y = fma(b0[m].y, t, zv.y);
@@ -745,14 +747,28 @@ __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[kLc
   return true;
 }
 
+// n0 / n1: row j's granules as loaded one step earlier (MLFF_LC_PREFETCH, default on): they were
+// published D steps before j, so the look usually finds them complete and the step does not wait
+// a memory round trip of its own; row j + 1's look is issued here for the next step.  Off: the
+// look is issued at the start of the step and waited for (one round trip per step under the row
+// stream's load: ~3.2 us at every D, L and segment width, profiles/r04/lc_cfg_ab/)
 template <int D>
 __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const double *red,
-                                             double *tsh, int *bail) {
+                                             double *tsh, int *bail, unsigned long long &n0,
+                                             unsigned long long &n1, bool prefetch) {
   const int lane = threadIdx.x & 63;
   const int jp = j + D;
   if (j >= a.i0 && j < a.i1) {
     unsigned long long x0 = 0, x1 = 0;
-    if (lane < a.C) {
+    if (prefetch) {
+      x0 = n0;
+      x1 = n1;
+      if (lane < a.C && j + 1 < a.i1) {
+        unsigned long long *g = lc_granule(a, j + 1);
+        n0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        n1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (lane < a.C) {
       unsigned long long *g = lc_granule(a, j);
       x0 = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       x1 = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -779,34 +795,35 @@ __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const doubl
   return true;
 }
 
-template <int D, int L, int U>
-__device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D + L + 1][kLcM],
+template <int D, int L, int M, int U>
+__device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D + L + 1][M],
                                              const d2 *r_sh, d2 *z_sh, double *red,
                                              const double *tsh, const int *bail) {
   constexpr int NB = D + L + 1;
   if constexpr (U == NB) {
     return true;
   } else {
-    if (!lc_row_step<D, L>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh, red,
-                           tsh, bail))
+    if (!lc_row_step<D, L, M>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh,
+                              red, tsh, bail))
       return false;
-    return lc_row_steps<D, L, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
+    return lc_row_steps<D, L, M, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
   }
 }
 
-template <int D, int L>
+template <int D, int L, int M>
 __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__restrict__ T, int64_t ldt,
                                                            int64_t k, int C, int rpc,
                                                            const double *__restrict__ r,
                                                            double *__restrict__ zpart,
                                                            unsigned long long *slots,
                                                            unsigned epoch, int *fault,
-                                                           int mute_block,
+                                                           int mute_block, int prefetch,
                                                            const int *__restrict__ status,
                                                            StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  __shared__ d2 r_sh[kLcM * kLcThreads];
-  __shared__ d2 z_sh[kLcM * kLcThreads];
+  constexpr int SEG = M * 2 * kLcThreads;
+  __shared__ d2 r_sh[M * kLcThreads];
+  __shared__ d2 z_sh[M * kLcThreads];
   __shared__ double red[16];
   __shared__ double tsh[2];
   __shared__ int bail;
@@ -816,8 +833,8 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
   a.C = C;
   const int q = blockIdx.x / C;
   a.c = blockIdx.x % C;
-  a.c0 = (int64_t)a.c * kLcSeg;
-  const int64_t segcols = ldt - a.c0 < kLcSeg ? ldt - a.c0 : kLcSeg;
+  a.c0 = (int64_t)a.c * SEG;
+  const int64_t segcols = ldt - a.c0 < SEG ? ldt - a.c0 : SEG;
   a.segbytes = (int)(segcols * 8);
   a.i0 = q * rpc;
   a.i1 = a.i0 + rpc < (int)k ? a.i0 + rpc : (int)k;
@@ -827,12 +844,12 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
   const bool row_wave = threadIdx.x < kLcThreads;
   constexpr int NB = D + L + 1;
   if (row_wave) {
-    d2 B[NB][kLcM];
-    d2 rv[kLcM];
+    d2 B[NB][M];
+    d2 rv[M];
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double *>(r + a.c0), 0, a.segbytes, 0x00020000);
 #pragma unroll
-    for (int m = 0; m < kLcM; ++m)
+    for (int m = 0; m < M; ++m)
       rv[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(
                                          rs, (int)threadIdx.x * 16, m * kLcThreads * 16, 0));
 #pragma unroll
@@ -840,19 +857,19 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
       lc_load(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
     if (!stop_prologue_wide(fold, red)) return;
 #pragma unroll
-    for (int m = 0; m < kLcM; ++m) {
+    for (int m = 0; m < M; ++m) {
       r_sh[threadIdx.x + kLcThreads * m] = rv[m];
       z_sh[threadIdx.x + kLcThreads * m] = d2{0.0, 0.0};
     }
     __syncthreads();  // bail = 0 (sync wave)
     bool ok = true;
     for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
-      ok = lc_row_steps<D, L, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
+      ok = lc_row_steps<D, L, M, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
     if (!ok) return;
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
         zpart + (int64_t)q * ldt + a.c0, 0, a.segbytes, 0x00020000);
 #pragma unroll
-    for (int m = 0; m < kLcM; ++m)
+    for (int m = 0; m < M; ++m)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + kLcThreads * m]),
                                              out, (int)threadIdx.x * 16, m * kLcThreads * 16, 0);
   } else {
@@ -860,14 +877,50 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
     if (threadIdx.x == kLcThreads) bail = 0;
     __syncthreads();
     bool ok = true;
+    unsigned long long n0 = 0, n1 = 0;  // epoch 0 is never a launch's: the first look polls
     for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
-      for (int u = 0; u < NB && ok; ++u) ok = lc_sync_step<D>(a, j + u, red, tsh, &bail);
+      for (int u = 0; u < NB && ok; ++u)
+        ok = lc_sync_step<D>(a, j + u, red, tsh, &bail, n0, n1, prefetch != 0);
     if (!ok && threadIdx.x == kLcThreads)
       __hip_atomic_store(fault, ST_FAULT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-int lr_cluster_members(int64_t ldt) { return (int)((ldt + kLcSeg - 1) / kLcSeg); }
+// MLFF_LC_CFG="D,L,M" (A/B of the hand-off slack D, load distance L and double2 per thread M,
+// segment 1024 M columns): one of the instantiations below, else the default (2, 1, 8)
+struct LcCfg {
+  int D, L, M;
+};
+static LcCfg lc_cfg() {
+  static const LcCfg cfg = [] {
+    LcCfg c{kLcD, kLcL, kLcM};
+    if (const char *e = std::getenv("MLFF_LC_CFG")) {
+      LcCfg w{0, 0, 0};
+      if (std::sscanf(e, "%d,%d,%d", &w.D, &w.L, &w.M) == 3) {
+        const LcCfg ok[] = {{2, 1, 8}, {1, 1, 8}, {3, 1, 6}, {3, 2, 6}, {4, 2, 4}};
+        for (const LcCfg &o : ok)
+          if (o.D == w.D && o.L == w.L && o.M == w.M) c = w;
+      }
+    }
+    return c;
+  }();
+  return cfg;
+}
+static int64_t lc_seg() { return (int64_t)lc_cfg().M * 2 * kLcThreads; }
+// dynamic LDS that keeps a member alone on its CU (M = 4 needs 66 KB of the 160)
+static size_t lc_pad() { return lc_cfg().M <= 4 ? 16384 : 0; }
+
+template <typename F>
+static auto lc_dispatch(F &&f) {
+  const LcCfg c = lc_cfg();
+  if (c.M == 8 && c.D == 1) return f(k_lr_cluster<1, 1, 8>);
+  if (c.M == 6 && c.L == 1) return f(k_lr_cluster<3, 1, 6>);
+  if (c.M == 6) return f(k_lr_cluster<3, 2, 6>);
+  if (c.M == 4) return f(k_lr_cluster<4, 2, 4>);
+  return f(k_lr_cluster<kLcD, kLcL, kLcM>);
+}
+
+int lr_cluster_members(int64_t ldt) { return (int)((ldt + lc_seg() - 1) / lc_seg()); }
 bool lr_cluster_fits(int64_t ldt) {
   static const int maxc = [] {  // MLFF_LC_MAXC: sweeps of the member cap (at most 64: one wave polls)
     const char *e = std::getenv("MLFF_LC_MAXC");
@@ -882,8 +935,9 @@ int lr_cluster_count(int64_t ldt, int device) {
   int cus = 0, per_cu = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lr_cluster<kLcD, kLcL>, kLcThreads + 64, 0) !=
-      hipSuccess)
+  if (lc_dispatch([&](auto kern) {
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kLcThreads + 64, lc_pad());
+      }) != hipSuccess)
     return 0;
   const int resident = cus * std::min(per_cu, 1);  // one member per CU
   return resident / C;
@@ -901,14 +955,21 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
   // MLFF_LC_TEST_MUTE=<b>[@<e>]: workgroup b never publishes (from the launch with epoch e
   // on, default every launch), so its cluster's hand-offs time out (tests of the ~0.1 s fault
   // bail-out, also in the middle of a chunk of PCG iterations; never set in production)
+  static const int prefetch = [] {
+    const char *e = std::getenv("MLFF_LC_PREFETCH");
+    return e != nullptr && std::atoi(e) == 0 ? 0 : 1;
+  }();
   int mute = -1;
   if (const char *mute_env = std::getenv("MLFF_LC_TEST_MUTE")) {
     const char *at = std::strchr(mute_env, '@');
     const unsigned from = at ? (unsigned)std::atoi(at + 1) : 0u;
     if (epoch >= from) mute = std::atoi(mute_env);
   }
-  hipLaunchKernelGGL((k_lr_cluster<kLcD, kLcL>), dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), 0, s,
-                     T, ldt, k, C, rpc, r, zpart, slots, epoch, fault, mute, status, fold);
+  lc_dispatch([&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), lc_pad(), s, T, ldt, k, C, rpc,
+                       r, zpart, slots, epoch, fault, mute, prefetch, status, fold);
+    return 0;
+  });
   if (n > 0)
     launch_lr_fin(zpart, Q, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n));
 }

@@ -83,6 +83,34 @@ for s in ${STEPS:-suite smoke bench}; do
       done
       step lr1024_prof 300 env MLFF_LR_THREADS=1024 rocprofv3 --kernel-trace --stats -d $O/lr1024prof -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --steps 200 --warmup 20 --no-solve
       step lr1024_tests 600 env MLFF_LR_THREADS=1024 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py tests/test_gpu_fused_iteration.py && step cho_tests 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_cho_stable.py ;;
+    lccfg)  # cluster apply: hand-off slack D, load distance L, double2 per thread M (MLFF_LC_CFG),
+            # interleaved twice at the reference's large published points; then the cluster tests
+      for rep in 1 2; do
+        for c in ${LCC:-2,1,8 2,2,6 3,1,6 3,2,6 2,2,4 4,2,4 3,3,4 5,1,4}; do
+          t=${c//,/_}
+          step lc${t}_nt141_r$rep 300 env MLFF_LC_CFG=$c python bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
+          step lc${t}_eth5833_r$rep 300 env MLFF_LC_CFG=$c $EB --m 5833
+        done
+      done
+      for c in ${LCT:-3,2,6 4,2,4}; do
+        t=${c//,/_}
+        step lc${t}_tests 600 env MLFF_LC_CFG=$c python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_core.py -k "one_pass or cluster" tests/test_gpu_configs.py::test_nanotube_cluster_apply_solve
+      done ;;
+    lcpf)  # cluster apply with the next row's hand-off look issued one step early (MLFF_LC_PREFETCH)
+           # vs at the start of its own step, at several D / L / M; then the cluster tests
+      for rep in 1 2; do
+        for c in ${LCC:-2,1,8 1,1,8 3,1,6 3,2,6 4,2,4}; do
+          for pf in 1 0; do
+            t=${c//,/_}_pf$pf
+            step lc${t}_nt141_r$rep 300 env MLFF_LC_PREFETCH=$pf MLFF_LC_CFG=$c python bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
+            step lc${t}_eth5833_r$rep 300 env MLFF_LC_PREFETCH=$pf MLFF_LC_CFG=$c $EB --m 5833
+          done
+        done
+        for pf in 1 0; do
+          step lc_pf${pf}_rbf_r$rep 300 env MLFF_LC_PREFETCH=$pf python bench.py --no-cpu --no-solve --steps 50 --warmup 5
+        done
+      done
+      step lcpf_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_core.py -k "one_pass or cluster" tests/test_gpu_configs.py::test_nanotube_cluster_apply_solve ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
