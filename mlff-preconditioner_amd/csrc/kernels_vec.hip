@@ -625,32 +625,39 @@ static unsigned lr_fin_grid(int64_t n) {
 
 // ---------------------------------------------------------------------------
 // One-pass low-rank apply for rows longer than one workgroup's registers (one rank,
-// N_loc up to kLcMaxC x 8192 columns, e.g. the N = 156510 nanotube system).  A row
-// is split over a CLUSTER of C workgroups (column segments of kLcSeg = 8192 columns, 64 KB:
-// 512 threads x 8 double2 in registers; r's and the partial z's segments in LDS), and the
-// Q = floor(CUs / C) clusters own contiguous row ranges.  Per row each member forms its
-// segment's partial dot (fixed-order block sum) and publishes it as two 8-byte {epoch, 32
-// bits} granules (relaxed agent-scope atomic stores, MI355X "R2" hand-off: the data is the
-// flag); D row-steps later every member's sync wave reads the C granule pairs of that row
-// until every tag equals the launch's epoch, sums the C partials in member order (the same
-// bits in every member) and the members accumulate z_seg += T[i, seg] t_i from the row still
-// held in registers.  D + L + 1 register buffers: row j (consumed), rows j + 1 … j + D - 1
-// (waiting for their partials), j + D (partial formed and published; loaded L steps
+// N_loc up to kLcMaxC x 7168 columns, e.g. the N = 156510 nanotube system).  A row
+// is split over a CLUSTER of C workgroups (column segments of kLcSeg = 7168 columns, 56 KB:
+// 448 row threads x 8 double2 in registers, plus one sync wave; r's and the partial z's
+// segments in LDS), and the Q = floor(CUs / C) clusters own contiguous row ranges.  Per row
+// each member forms its segment's partial dot (fixed-order block sum) and publishes it as two
+// 8-byte {epoch, 32 bits} granules (relaxed agent-scope atomic stores, MI355X "R2" hand-off:
+// the data is the flag); D row-steps later every member's sync wave reads the C granule pairs
+// of that row until every tag equals the launch's epoch, sums the C partials in member order
+// (the same bits in every member) and the members accumulate z_seg += T[i, seg] t_i from the
+// row still held in registers.  D + L + 1 register buffers: row j (consumed), rows j + 1 …
+// j + D - 1 (waiting for their partials), j + D (partial formed and published; loaded L steps
 // earlier), rows in flight up to j + D + L (loading): D row-steps of slack for the hand-off,
 // L steps between a row's load and its use.  A member that waits for more than ~0.1 s writes
 // ST_FAULT to `fault` and leaves (the host reports an error; a cluster can only stall if its
 // members are not all resident, which the host checks with the occupancy query before it
 // chooses this path).
-constexpr int kLcThreads = 512;
-constexpr int kLcSeg = 8192;
-constexpr int kLcM = kLcSeg / (2 * kLcThreads);  // 8 double2 per thread per row
-constexpr int kLcMaxC = 44;  // members per cluster.  Apply time against two passes
-                             // (nanotube, rule-of-thumb k): C = 3..14 -21..-41 %, C = 20
-                             // -31 %, C = 28 -27 %, C = 41 -8 %, C = 62 (N = 505050) +14 %
-                             // (the hand-off of the slowest of C members paces each step)
-constexpr int kLcD = 2, kLcL = 1;
+//
+// Why 7 row waves and D = 4 (round 4, profiles/r04/lc_*_ab/): the step time is the hand-off
+// round trip / D.  With 8 row waves + the sync wave a workgroup is 9 waves, 3 on some SIMD, so
+// every wave gets <= 168 registers: 4 row buffers (D = 2, L = 1).  At D = 2 the apply took
+// ~3.2 us per row-step whatever the bytes per step (segments of 4096 / 6144 / 8192 columns:
+// nanotube N = 156510 8.4 / 5.1 / 4.0 ms).  7 row waves + the sync wave are 8 waves, 2 per
+// SIMD, 256 registers each: 6 buffers, D = 4: 2.73 ms (frac 0.84; D = 3: 2.92, D = 2: 4.25).
+constexpr int kLcThreads = 448;  // row threads (7 waves); the workgroup is kLcThreads + 64
+constexpr int kLcM = 8;          // double2 per thread per row
+constexpr int kLcSeg = kLcM * 2 * kLcThreads;
+constexpr int kLcMaxC = 44;  // members per cluster.  Apply time against two passes (round 3,
+                             // 8192-column segments, D = 2; nanotube, rule-of-thumb k):
+                             // C = 3..14 -21..-41 %, C = 20 -31 %, C = 28 -27 %, C = 41 -8 %,
+                             // C = 62 (N = 505050) +14 %
+constexpr int kLcD = 4, kLcL = 1;
 
-template <int M>
+template <int M, int RT>
 __device__ __forceinline__ void lc_load(d2 (&buf)[M], const double *T, int64_t ldt,
                                         int64_t row, int64_t i1, int64_t c0, int segbytes) {
   const bool ok = row < i1;
@@ -659,7 +666,18 @@ __device__ __forceinline__ void lc_load(d2 (&buf)[M], const double *T, int64_t l
   const int voff = (int)threadIdx.x * 16;
 #pragma unroll
   for (int m = 0; m < M; ++m)
-    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * kLcThreads * 16, 2));
+    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * RT * 16, 2));
+}
+
+// the RT / 64 row waves' partial sums in a fixed tree (8 waves: ((q0 + q1) + (q2 + q3)) +
+// ((q4 + q5) + (q6 + q7)))
+template <int NW>
+__device__ __forceinline__ double lc_wave_tree(const double *q) {
+  if constexpr (NW == 1) {
+    return q[0];
+  } else {
+    return lc_wave_tree<NW / 2>(q) + lc_wave_tree<NW - NW / 2>(q + NW / 2);
+  }
 }
 
 struct LcArgs {
@@ -713,19 +731,19 @@ __device__ __forceinline__ bool lc_consume(const LcArgs &a, int row, unsigned lo
 // (loading); the rows between wait for their partials or are in flight.  The sync
 // wave (8) polls, sums and publishes: its hand-off loads never queue behind row loads, and
 // the row waves' code holds no hand-off load a counter wait could be charged for.
-template <int D, int L, int M>
+template <int D, int L, int M, int RT>
 __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[M],
                                             d2 (&b2)[M], d2 (&b3)[M], const d2 *r_sh,
                                             d2 *z_sh, double *red, const double *tsh,
                                             const int *bail) {
   const int w = threadIdx.x >> 6;
   const int jp = j + D;
-  lc_load(b3, a.T, a.ldt, j + D + L, a.i1, a.c0, a.segbytes);
+  lc_load<M, RT>(b3, a.T, a.ldt, j + D + L, a.i1, a.c0, a.segbytes);
   if (jp >= a.i0 && jp < a.i1) {
     double a0 = 0.0, a1 = 0.0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const d2 rv = r_sh[threadIdx.x + kLcThreads * m];
+      const d2 rv = r_sh[threadIdx.x + RT * m];
       a0 = fma(b2[m].x, rv.x, a0);
       a1 = fma(b2[m].y, rv.y, a1);
     }
@@ -738,10 +756,10 @@ __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[M],
     const double t = tsh[j & 1];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      d2 zv = z_sh[threadIdx.x + kLcThreads * m];
+      d2 zv = z_sh[threadIdx.x + RT * m];
       zv.x = fma(b0[m].x, t, zv.x);
       zv.y = fma(b0[m].y, t, zv.y);
-      z_sh[threadIdx.x + kLcThreads * m] = zv;
+      z_sh[threadIdx.x + RT * m] = zv;
     }
   }
   return true;
@@ -752,7 +770,7 @@ __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[M],
 // a memory round trip of its own; row j + 1's look is issued here for the next step.  Off: the
 // look is issued at the start of the step and waited for (one round trip per step under the row
 // stream's load: ~3.2 us at every D, L and segment width, profiles/r04/lc_cfg_ab/)
-template <int D>
+template <int D, int RT>
 __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const double *red,
                                              double *tsh, int *bail, unsigned long long &n0,
                                              unsigned long long &n1, bool prefetch) {
@@ -784,7 +802,7 @@ __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const doubl
   if (*bail) return false;
   if (jp >= a.i0 && jp < a.i1 && lane == 0 && !a.mute) {
     const double *q = red + (jp & 1) * 8;
-    const double ps = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+    const double ps = lc_wave_tree<RT / 64>(q);
     const unsigned long long bits = __builtin_bit_cast(unsigned long long, ps);
     unsigned long long *g = a.slots + ((size_t)jp * a.C + a.c) * 2;
     __hip_atomic_store(g, ((unsigned long long)a.epoch << 32) | (bits & 0xffffffffull),
@@ -795,7 +813,7 @@ __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const doubl
   return true;
 }
 
-template <int D, int L, int M, int U>
+template <int D, int L, int M, int RT, int U>
 __device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D + L + 1][M],
                                              const d2 *r_sh, d2 *z_sh, double *red,
                                              const double *tsh, const int *bail) {
@@ -803,15 +821,15 @@ __device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D +
   if constexpr (U == NB) {
     return true;
   } else {
-    if (!lc_row_step<D, L, M>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh,
+    if (!lc_row_step<D, L, M, RT>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh,
                               red, tsh, bail))
       return false;
-    return lc_row_steps<D, L, M, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
+    return lc_row_steps<D, L, M, RT, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
   }
 }
 
-template <int D, int L, int M>
-__global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__restrict__ T, int64_t ldt,
+template <int D, int L, int M, int RT = kLcThreads>
+__global__ __launch_bounds__(RT + 64) void k_lr_cluster(const double *__restrict__ T, int64_t ldt,
                                                            int64_t k, int C, int rpc,
                                                            const double *__restrict__ r,
                                                            double *__restrict__ zpart,
@@ -821,9 +839,9 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
                                                            const int *__restrict__ status,
                                                            StopFold fold) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  constexpr int SEG = M * 2 * kLcThreads;
-  __shared__ d2 r_sh[M * kLcThreads];
-  __shared__ d2 z_sh[M * kLcThreads];
+  constexpr int SEG = M * 2 * RT;
+  __shared__ d2 r_sh[M * RT];
+  __shared__ d2 z_sh[M * RT];
   __shared__ double red[16];
   __shared__ double tsh[2];
   __shared__ int bail;
@@ -841,7 +859,7 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
   a.slots = slots;
   a.epoch = epoch;
   a.mute = (int)blockIdx.x == mute_block;
-  const bool row_wave = threadIdx.x < kLcThreads;
+  const bool row_wave = threadIdx.x < RT;
   constexpr int NB = D + L + 1;
   if (row_wave) {
     d2 B[NB][M];
@@ -851,72 +869,74 @@ __global__ __launch_bounds__(kLcThreads + 64) void k_lr_cluster(const double *__
 #pragma unroll
     for (int m = 0; m < M; ++m)
       rv[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(
-                                         rs, (int)threadIdx.x * 16, m * kLcThreads * 16, 0));
+                                         rs, (int)threadIdx.x * 16, m * RT * 16, 0));
 #pragma unroll
     for (int t = 0; t < L; ++t)  // rows i0 .. i0 + L - 1 (the steps start at j = i0 - D)
-      lc_load(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
+      lc_load<M, RT>(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
     if (!stop_prologue_wide(fold, red)) return;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      r_sh[threadIdx.x + kLcThreads * m] = rv[m];
-      z_sh[threadIdx.x + kLcThreads * m] = d2{0.0, 0.0};
+      r_sh[threadIdx.x + RT * m] = rv[m];
+      z_sh[threadIdx.x + RT * m] = d2{0.0, 0.0};
     }
     __syncthreads();  // bail = 0 (sync wave)
     bool ok = true;
     for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
-      ok = lc_row_steps<D, L, M, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
+      ok = lc_row_steps<D, L, M, RT, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
     if (!ok) return;
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
         zpart + (int64_t)q * ldt + a.c0, 0, a.segbytes, 0x00020000);
 #pragma unroll
     for (int m = 0; m < M; ++m)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + kLcThreads * m]),
-                                             out, (int)threadIdx.x * 16, m * kLcThreads * 16, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, z_sh[threadIdx.x + RT * m]),
+                                             out, (int)threadIdx.x * 16, m * RT * 16, 0);
   } else {
     if (!stop_prologue_wide(fold, red)) return;
-    if (threadIdx.x == kLcThreads) bail = 0;
+    if (threadIdx.x == RT) bail = 0;
     __syncthreads();
     bool ok = true;
     unsigned long long n0 = 0, n1 = 0;  // epoch 0 is never a launch's: the first look polls
     for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
       for (int u = 0; u < NB && ok; ++u)
-        ok = lc_sync_step<D>(a, j + u, red, tsh, &bail, n0, n1, prefetch != 0);
-    if (!ok && threadIdx.x == kLcThreads)
+        ok = lc_sync_step<D, RT>(a, j + u, red, tsh, &bail, n0, n1, prefetch != 0);
+    if (!ok && threadIdx.x == RT)
       __hip_atomic_store(fault, ST_FAULT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-// MLFF_LC_CFG="D,L,M" (A/B of the hand-off slack D, load distance L and double2 per thread M,
-// segment 1024 M columns): one of the instantiations below, else the default (2, 1, 8)
+// MLFF_LC_CFG="D,L,M,RT" (A/B of the hand-off slack D, load distance L, double2 per thread M and
+// row threads RT; segment 2 M RT columns): one of the instantiations below, else the default
+// (4, 1, 8, 448)
 struct LcCfg {
-  int D, L, M;
+  int D, L, M, RT;
 };
 static LcCfg lc_cfg() {
   static const LcCfg cfg = [] {
-    LcCfg c{kLcD, kLcL, kLcM};
+    LcCfg c{kLcD, kLcL, kLcM, kLcThreads};
     if (const char *e = std::getenv("MLFF_LC_CFG")) {
-      LcCfg w{0, 0, 0};
-      if (std::sscanf(e, "%d,%d,%d", &w.D, &w.L, &w.M) == 3) {
-        const LcCfg ok[] = {{2, 1, 8}, {1, 1, 8}, {3, 1, 6}, {3, 2, 6}, {4, 2, 4}};
+      LcCfg w{0, 0, 0, kLcThreads};
+      if (std::sscanf(e, "%d,%d,%d,%d", &w.D, &w.L, &w.M, &w.RT) >= 3) {
+        const LcCfg ok[] = {{4, 1, 8, 448}, {3, 2, 8, 448}, {4, 2, 8, 448}, {5, 1, 8, 448},
+                            {2, 1, 8, 512}, {3, 1, 6, 512}};
         for (const LcCfg &o : ok)
-          if (o.D == w.D && o.L == w.L && o.M == w.M) c = w;
+          if (o.D == w.D && o.L == w.L && o.M == w.M && o.RT == w.RT) c = w;
       }
     }
     return c;
   }();
   return cfg;
 }
-static int64_t lc_seg() { return (int64_t)lc_cfg().M * 2 * kLcThreads; }
-// dynamic LDS that keeps a member alone on its CU (M = 4 needs 66 KB of the 160)
-static size_t lc_pad() { return lc_cfg().M <= 4 ? 16384 : 0; }
+static int64_t lc_seg() { return (int64_t)lc_cfg().M * 2 * lc_cfg().RT; }
+static int lc_threads() { return lc_cfg().RT + 64; }
 
 template <typename F>
 static auto lc_dispatch(F &&f) {
   const LcCfg c = lc_cfg();
-  if (c.M == 8 && c.D == 1) return f(k_lr_cluster<1, 1, 8>);
-  if (c.M == 6 && c.L == 1) return f(k_lr_cluster<3, 1, 6>);
-  if (c.M == 6) return f(k_lr_cluster<3, 2, 6>);
-  if (c.M == 4) return f(k_lr_cluster<4, 2, 4>);
+  if (c.RT == 448 && c.D == 3) return f(k_lr_cluster<3, 2, 8, 448>);
+  if (c.RT == 448 && c.D == 4 && c.L == 2) return f(k_lr_cluster<4, 2, 8, 448>);
+  if (c.RT == 448 && c.D == 5) return f(k_lr_cluster<5, 1, 8, 448>);
+  if (c.RT == 512 && c.M == 8) return f(k_lr_cluster<2, 1, 8, 512>);  // round 3's form
+  if (c.RT == 512 && c.M == 6) return f(k_lr_cluster<3, 1, 6, 512>);
   return f(k_lr_cluster<kLcD, kLcL, kLcM>);
 }
 
@@ -936,7 +956,7 @@ int lr_cluster_count(int64_t ldt, int device) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
     return 0;
   if (lc_dispatch([&](auto kern) {
-        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kLcThreads + 64, lc_pad());
+        return hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, lc_threads(), 0);
       }) != hipSuccess)
     return 0;
   const int resident = cus * std::min(per_cu, 1);  // one member per CU
@@ -966,7 +986,7 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
     if (epoch >= from) mute = std::atoi(mute_env);
   }
   lc_dispatch([&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(Q * C)), dim3(kLcThreads + 64), lc_pad(), s, T, ldt, k, C, rpc,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(Q * C)), dim3(lc_threads()), 0, s, T, ldt, k, C, rpc,
                        r, zpart, slots, epoch, fault, mute, prefetch, status, fold);
     return 0;
   });

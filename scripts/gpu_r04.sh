@@ -111,6 +111,30 @@ for s in ${STEPS:-suite smoke bench}; do
         done
       done
       step lcpf_tests 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_core.py -k "one_pass or cluster" tests/test_gpu_configs.py::test_nanotube_cluster_apply_solve ;;
+    lcrt)  # cluster apply with 7 row waves (2 waves per SIMD, 256 registers: 3-6 rows in registers)
+           # vs 8 (3 per SIMD, 4 rows), interleaved; configs[2]; then the cluster tests on one of them
+      for rep in 1 2; do
+        for c in ${LCC:-2,1,8,512 2,2,8,448 2,3,8,448 3,2,8,448 3,3,8,448 2,4,8,448}; do
+          t=${c//,/_}
+          step lc${t}_nt141_r$rep 300 env MLFF_LC_CFG=$c python bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
+          step lc${t}_eth5833_r$rep 300 env MLFF_LC_CFG=$c $EB --m 5833
+          step lc${t}_rbf_r$rep 300 env MLFF_LC_CFG=$c python bench.py --no-cpu --no-solve --steps 50 --warmup 5
+        done
+      done
+      step lcrt_tests 600 env MLFF_LC_CFG=${LCTEST:-2,3,8,448} python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_core.py -k "one_pass or cluster" tests/test_gpu_configs.py::test_nanotube_cluster_apply_solve ;;
+    lcd)  # 7 row waves: hand-off slack D 3 / 4 / 5, interleaved; then the cluster tests (every case)
+      for rep in 1 2; do
+        for c in ${LCC:-3,2,8,448 4,1,8,448 4,2,8,448 5,1,8,448 3,3,8,448}; do
+          t=${c//,/_}
+          step lc${t}_nt141_r$rep 300 env MLFF_LC_CFG=$c python bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
+          step lc${t}_eth5833_r$rep 300 env MLFF_LC_CFG=$c $EB --m 5833
+        done
+      done
+      timeout -k 10 600 env MLFF_LC_CFG=${LCTEST:-3,2,8,448} python -u -m pytest -q -rf --timeout 300 --timeout-method thread -m gpu tests/test_gpu_core.py -k "one_pass or cluster" tests/test_gpu_configs.py::test_nanotube_cluster_apply_solve > $O/lcd_tests.txt 2>&1
+      echo "== lcd_tests rc=$?" | tee -a $O/steps.log ;;
+    lrdiag)  # the 20000 x 400 random-panel solve's traces, one-pass (default / 7 row waves) and two-pass
+      step lrdiag_default 300 python -u scripts/dev/diag_lowrank_20000.py $O/lr20000_default.npz
+      step lrdiag_448 300 env MLFF_LC_CFG=4,1,8,448 python -u scripts/dev/diag_lowrank_20000.py $O/lr20000_448.npz ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib

@@ -13,7 +13,14 @@ outputs and against itself under re-ordered summation (the noise floor):
             iteration count within 10 % (at least +-3), the first iterations
             pointwise within 1e-6 in log10, every half-decade crossing of the
             running-minimum residual within 10 % (+3) iterations of the
-            reference's, ||dx|| / ||x|| <= 1e-6.
+            reference's, ||dx|| / ||x|| <= 1e-6.  A level the running minimum skims
+            (a plateau within KNIFE = 0.01 in log10 of it) is crossed at an ill-defined
+            iteration: each run's crossing is then the range from its first value
+            within 10^(lvl + KNIFE) to its first below 10^(lvl - KNIFE), and the two
+            ranges must lie within that slack of each other.  (The 20000 x 400 random-
+            panel solve of test_one_pass_lowrank_apply sits at -0.4973 / -0.4981 /
+            -0.5029 from iteration 66 to 98 in three GPU summation orders: 66 or 97 by
+            a 1 % difference in the residual; tests/golden/lowrank_knife_traces.npz.)
 
 Golden solves of the reference (case = "fixture/preconditioner") are held to their MEASURED
 noise band instead (tests/golden/noise_band.json, tests/golden/make_noise_band.py): the
@@ -45,6 +52,22 @@ def noise_band(case: str) -> dict:
 
 def envelope(trace):
     return np.minimum.accumulate(np.asarray(trace))
+
+
+KNIFE = 0.01
+
+
+def _first_below(e, lvl):
+    hit = e <= 10 ** lvl
+    return int(np.argmax(hit)) if np.any(hit) else len(e)
+
+
+def crossing_gap(ea, eb, lvl, knife=KNIFE):
+    """Distance in iterations between the crossing ranges of two running minima at lvl
+    (0 when they overlap); without plateaus it is |crossing(a) - crossing(b)|."""
+    a0, a1 = _first_below(ea, lvl + knife), _first_below(ea, lvl - knife)
+    b0, b1 = _first_below(eb, lvl + knife), _first_below(eb, lvl - knife)
+    return max(0, max(a0, b0) - min(a1, b1))
 
 
 def assert_pcg_parity(iters, trace, x, ref_iters, ref_trace, ref_x, mode="chaotic",
@@ -88,9 +111,9 @@ def assert_pcg_parity(iters, trace, x, ref_iters, ref_trace, ref_x, mode="chaoti
         ea, eb = envelope(trace), envelope(ref_trace)
         top, bot = np.log10(eb[0]), np.log10(max(eb[-1], ea[-1]))
         for lvl in np.arange(np.floor(top) - 0.5, bot, -0.5):
-            ia = int(np.argmax(ea <= 10 ** lvl)) if np.any(ea <= 10 ** lvl) else len(ea)
-            ib = int(np.argmax(eb <= 10 ** lvl)) if np.any(eb <= 10 ** lvl) else len(eb)
-            assert abs(ia - ib) <= max(3, int(np.ceil(iter_frac * ib)) + 3), (lvl, ia, ib)
+            ia, ib = _first_below(ea, lvl), _first_below(eb, lvl)
+            gap = crossing_gap(ea, eb, lvl)
+            assert gap <= max(3, int(np.ceil(iter_frac * ib)) + 3), (lvl, ia, ib, gap)
     if x is not None and ref_x is not None:
         rel = np.linalg.norm(np.asarray(x) - np.asarray(ref_x)) / np.linalg.norm(ref_x)
         assert rel <= x_tol, rel
