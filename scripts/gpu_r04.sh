@@ -135,6 +135,16 @@ for s in ${STEPS:-suite smoke bench}; do
     lrdiag)  # the 20000 x 400 random-panel solve's traces, one-pass (default / 7 row waves) and two-pass
       step lrdiag_default 300 python -u scripts/dev/diag_lowrank_20000.py $O/lr20000_default.npz
       step lrdiag_448 300 env MLFF_LC_CFG=4,1,8,448 python -u scripts/dev/diag_lowrank_20000.py $O/lr20000_448.npz ;;
+    lrform)  # rows that fit one workgroup: the per-workgroup one-pass apply vs the cluster form
+             # (MLFF_LR_FORM was a temporary switch of api.hip, removed after this A/B)
+      for rep in 1 2; do
+        for f in rows cluster; do
+          step lrf_${f}_nt_r$rep 300 env MLFF_LR_FORM=$f python bench.py --workload nanotube --no-cpu --steps 200 --warmup 20
+          step lrf_${f}_eth583_r$rep 300 env MLFF_LR_FORM=$f python bench.py --workload ethanol --m 583 --no-cpu --steps 200 --warmup 20 --no-solve
+        done
+      done
+      timeout -k 10 600 env MLFF_LR_FORM=cluster python -u -m pytest -q -rf --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py tests/test_gpu_fused_iteration.py tests/test_gpu_golden.py > $O/lrf_tests.txt 2>&1
+      echo "== lrf_tests rc=$?" | tee -a $O/steps.log ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
