@@ -657,7 +657,7 @@ constexpr int kLcMaxC = 44;  // members per cluster.  Apply time against two pas
                              // C = 62 (N = 505050) +14 %
 constexpr int kLcD = 4, kLcL = 1;
 
-template <int M, int RT>
+template <int M, int RT, int AUX>
 __device__ __forceinline__ void lc_load(d2 (&buf)[M], const double *T, int64_t ldt,
                                         int64_t row, int64_t i1, int64_t c0, int segbytes) {
   const bool ok = row < i1;
@@ -666,7 +666,7 @@ __device__ __forceinline__ void lc_load(d2 (&buf)[M], const double *T, int64_t l
   const int voff = (int)threadIdx.x * 16;
 #pragma unroll
   for (int m = 0; m < M; ++m)
-    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * RT * 16, 2));
+    buf[m] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, m * RT * 16, AUX));
 }
 
 // the RT / 64 row waves' partial sums in a fixed tree (8 waves: ((q0 + q1) + (q2 + q3)) +
@@ -731,14 +731,14 @@ __device__ __forceinline__ bool lc_consume(const LcArgs &a, int row, unsigned lo
 // (loading); the rows between wait for their partials or are in flight.  The sync
 // wave (8) polls, sums and publishes: its hand-off loads never queue behind row loads, and
 // the row waves' code holds no hand-off load a counter wait could be charged for.
-template <int D, int L, int M, int RT>
+template <int D, int L, int M, int RT, int AUX>
 __device__ __forceinline__ bool lc_row_step(const LcArgs &a, int j, d2 (&b0)[M],
                                             d2 (&b2)[M], d2 (&b3)[M], const d2 *r_sh,
                                             d2 *z_sh, double *red, const double *tsh,
                                             const int *bail) {
   const int w = threadIdx.x >> 6;
   const int jp = j + D;
-  lc_load<M, RT>(b3, a.T, a.ldt, j + D + L, a.i1, a.c0, a.segbytes);
+  lc_load<M, RT, AUX>(b3, a.T, a.ldt, j + D + L, a.i1, a.c0, a.segbytes);
   if (jp >= a.i0 && jp < a.i1) {
     double a0 = 0.0, a1 = 0.0;
 #pragma unroll
@@ -813,7 +813,7 @@ __device__ __forceinline__ bool lc_sync_step(const LcArgs &a, int j, const doubl
   return true;
 }
 
-template <int D, int L, int M, int RT, int U>
+template <int D, int L, int M, int RT, int AUX, int U>
 __device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D + L + 1][M],
                                              const d2 *r_sh, d2 *z_sh, double *red,
                                              const double *tsh, const int *bail) {
@@ -821,14 +821,16 @@ __device__ __forceinline__ bool lc_row_steps(const LcArgs &a, int j, d2 (&B)[D +
   if constexpr (U == NB) {
     return true;
   } else {
-    if (!lc_row_step<D, L, M, RT>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh,
+    if (!lc_row_step<D, L, M, RT, AUX>(a, j + U, B[U], B[(U + D) % NB], B[(U + D + L) % NB], r_sh, z_sh,
                               red, tsh, bail))
       return false;
-    return lc_row_steps<D, L, M, RT, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
+    return lc_row_steps<D, L, M, RT, AUX, U + 1>(a, j, B, r_sh, z_sh, red, tsh, bail);
   }
 }
 
-template <int D, int L, int M, int RT = kLcThreads>
+// AUX: the row loads' cache policy (2: non-temporal, the panel streams; 0: default, a panel that
+// fits the MALL beside the operator stays there from one iteration to the next, panel_streams)
+template <int D, int L, int M, int RT = kLcThreads, int AUX = 2>
 __global__ __launch_bounds__(RT + 64) void k_lr_cluster(const double *__restrict__ T, int64_t ldt,
                                                            int64_t k, int C, int rpc,
                                                            const double *__restrict__ r,
@@ -872,7 +874,7 @@ __global__ __launch_bounds__(RT + 64) void k_lr_cluster(const double *__restrict
                                          rs, (int)threadIdx.x * 16, m * RT * 16, 0));
 #pragma unroll
     for (int t = 0; t < L; ++t)  // rows i0 .. i0 + L - 1 (the steps start at j = i0 - D)
-      lc_load<M, RT>(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
+      lc_load<M, RT, AUX>(B[(D + t) % NB], T, ldt, a.i0 + t, a.i1, a.c0, a.segbytes);
     if (!stop_prologue_wide(fold, red)) return;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -882,7 +884,7 @@ __global__ __launch_bounds__(RT + 64) void k_lr_cluster(const double *__restrict
     __syncthreads();  // bail = 0 (sync wave)
     bool ok = true;
     for (int j = a.i0 - D; j < a.i1 && ok; j += NB)
-      ok = lc_row_steps<D, L, M, RT, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
+      ok = lc_row_steps<D, L, M, RT, AUX, 0>(a, j, B, r_sh, z_sh, red, tsh, &bail);
     if (!ok) return;
     const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
         zpart + (int64_t)q * ldt + a.c0, 0, a.segbytes, 0x00020000);
@@ -929,9 +931,20 @@ static LcCfg lc_cfg() {
 static int64_t lc_seg() { return (int64_t)lc_cfg().M * 2 * lc_cfg().RT; }
 static int lc_threads() { return lc_cfg().RT + 64; }
 
+// MLFF_LC_CACHED=0 / 1 (A/B): the row loads' policy regardless of the panel's size
+static bool lc_cached(int64_t k, int64_t ldt) {
+  static const int force = [] {
+    const char *e = std::getenv("MLFF_LC_CACHED");
+    return e != nullptr ? std::atoi(e) : -1;
+  }();
+  return force >= 0 ? force != 0 : !panel_streams(k, ldt);
+}
+
 template <typename F>
-static auto lc_dispatch(F &&f) {
+static auto lc_dispatch(F &&f, bool cached = false) {
   const LcCfg c = lc_cfg();
+  if (cached && c.D == kLcD && c.L == kLcL && c.M == kLcM && c.RT == kLcThreads)
+    return f(k_lr_cluster<kLcD, kLcL, kLcM, kLcThreads, 0>);
   if (c.RT == 448 && c.D == 3) return f(k_lr_cluster<3, 2, 8, 448>);
   if (c.RT == 448 && c.D == 4 && c.L == 2) return f(k_lr_cluster<4, 2, 8, 448>);
   if (c.RT == 448 && c.D == 5) return f(k_lr_cluster<5, 1, 8, 448>);
@@ -985,11 +998,13 @@ void launch_lr_apply_cluster(const double *T, int64_t ldt, int64_t k, int Q, con
     const unsigned from = at ? (unsigned)std::atoi(at + 1) : 0u;
     if (epoch >= from) mute = std::atoi(mute_env);
   }
-  lc_dispatch([&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3((unsigned)(Q * C)), dim3(lc_threads()), 0, s, T, ldt, k, C, rpc,
-                       r, zpart, slots, epoch, fault, mute, prefetch, status, fold);
-    return 0;
-  });
+  lc_dispatch(
+      [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)(Q * C)), dim3(lc_threads()), 0, s, T, ldt, k, C,
+                           rpc, r, zpart, slots, epoch, fault, mute, prefetch, status, fold);
+        return 0;
+      },
+      lc_cached(k, ldt));
   if (n > 0)
     launch_lr_fin(zpart, Q, ldt, r, z, n, sigma_p, lam_inv, rho_part, status, s, lr_fin_grid(n));
 }

@@ -145,6 +145,19 @@ for s in ${STEPS:-suite smoke bench}; do
       done
       timeout -k 10 600 env MLFF_LR_FORM=cluster python -u -m pytest -q -rf --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py tests/test_gpu_fused_iteration.py tests/test_gpu_golden.py > $O/lrf_tests.txt 2>&1
       echo "== lrf_tests rc=$?" | tee -a $O/steps.log ;;
+    lccache)  # configs[2]'s cluster apply: row loads with default policy (the 134 MB panel stays in
+              # the MALL) vs non-temporal, interleaved three times
+      for rep in 1 2 3; do
+        for c in 1 0; do
+          step lcc${c}_rbf_r$rep 300 env MLFF_LC_CACHED=$c python bench.py --no-cpu --no-solve --steps 100 --warmup 10
+        done
+      done ;;
+    lcfin)  # k_lr_fin's waves per workgroup for configs[2]'s Q = 25 cluster partials
+      for rep in 1 2; do
+        for w in 16 8 4; do
+          step lcfin${w}_rbf_r$rep 300 env MLFF_LR_FIN_WAVES=$w python bench.py --no-cpu --no-solve --steps 100 --warmup 10
+        done
+      done ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
