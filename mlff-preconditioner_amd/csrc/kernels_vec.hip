@@ -593,24 +593,27 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
     for (int64_t i = gridDim.x + threadIdx.x; i < kVecGrid; i += 64 * NW) xf.rr_part[i] = 0.0;
 }
 
-// waves of k_lr_fin (MLFF_LR_FIN_WAVES = 4 / 8 / 16 for A/B; nanotube, 2 interleaved rounds:
-// apply 66.3-66.6 us with 4, 65.8-65.9 with 16; k_lr_fin 8.1 -> 7.1 us)
-static int lr_fin_waves() {
-  static const int nw = [] {
+// waves of k_lr_fin: 16 for the rows form's G = 256 partials (nanotube, 2 interleaved rounds:
+// apply 66.3-66.6 us with 4, 65.8-65.9 with 16; k_lr_fin 8.1 -> 7.1 us), 4 for the cluster
+// form's few (configs[2], Q = 25: apply 38.2-38.3 us with 4, 38.4-38.5 with 8, 42.2-42.3 with 16,
+// profiles/r04/lc_fin_ab/).  MLFF_LR_FIN_WAVES = 4 / 8 / 16 overrides (A/B)
+static int lr_fin_waves(int G) {
+  static const int forced = [] {
     const char *e = std::getenv("MLFF_LR_FIN_WAVES");
-    const int v = e ? std::atoi(e) : 16;
-    return v == 8 || v == 16 ? v : 4;
+    const int v = e ? std::atoi(e) : 0;
+    return v == 4 || v == 8 || v == 16 ? v : 0;
   }();
-  return nw;
+  return forced != 0 ? forced : (G >= 128 ? 16 : 4);
 }
 
 static void launch_lr_fin(const double *zpart, int G, int64_t ldp, const double *r, double *z,
                           int64_t n, double sigma_p, double lam_inv, double *rho_part,
                           const int *status, hipStream_t s, unsigned grid, XrFold xf = XrFold{}) {
-  if (lr_fin_waves() == 16)
+  const int nw = lr_fin_waves(G);
+  if (nw == 16)
     hipLaunchKernelGGL(k_lr_fin<16>, dim3(grid), dim3(1024), 0, s, zpart, G, ldp, r, z, n, sigma_p,
                        lam_inv, rho_part, status, xf);
-  else if (lr_fin_waves() == 8)
+  else if (nw == 8)
     hipLaunchKernelGGL(k_lr_fin<8>, dim3(grid), dim3(512), 0, s, zpart, G, ldp, r, z, n, sigma_p,
                        lam_inv, rho_part, status, xf);
   else
