@@ -158,6 +158,14 @@ for s in ${STEPS:-suite smoke bench}; do
           step lcfin${w}_rbf_r$rep 300 env MLFF_LR_FIN_WAVES=$w python bench.py --no-cpu --no-solve --steps 100 --warmup 10
         done
       done ;;
+    redlanes)  # configs[2]'s slot reduction with two lanes per row vs one, interleaved
+      for rep in 1 2; do
+        for l in 2 1; do
+          step red${l}_rbf_r$rep 300 env MLFF_SYM_REDUCE_LANES=$l python bench.py --no-cpu --no-solve --steps 100 --warmup 10
+        done
+      done ;;
+    pmccopy)  # the table just collected, for the bench lines of this same call
+      cp $O/pmc_head/pmc_traffic.json profiles/pmc_traffic.json ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
