@@ -378,56 +378,7 @@ constexpr int kOwnSplit = 1 << 24;  // flag bit of an owned-slot entry: the tile
 // y[i] = sum_{t=0}^{nb-1} of the slots of row i (one rank); EPI: y = sigma y + lam vloc;
 // PQ (with EPI): also the p.q partial sums (vloc = p) of each workgroup -> pq_part
 // (grid = kVecGrid workgroups, grid-stride over the rows)
-// the slots [ta, tb) of row i in slot order: below t8 (no split tile) 16 / 8 loads in flight
-// per thread, the rest in batches of 8 with the split planes ((P + Pq0) + Pq1) + ...
-__device__ __forceinline__ double slot_sum(const double *__restrict__ P, const double *__restrict__ Pq,
-                                           const unsigned char *__restrict__ split, int64_t Np,
-                                           int nb, int nq, int64_t i, int bi, int ta, int tb,
-                                           int t8) {
-  const int64_t pl = (int64_t)nb * Np;
-  double s = 0.0;
-  int t = ta;
-  const int tf = t8 < tb ? t8 : tb;
-  for (; t + 15 < tf; t += 16) {
-    double v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) s += v[u];
-  }
-  for (; t + 7 < tf; t += 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += v[u];
-  }
-  for (; t < tb; t += 8) {
-    double v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      v[u] = 0.0;
-      const int tu = t + u;
-      if (tu < tb) {
-        v[u] = P[(int64_t)tu * Np + i];
-        if (tu > bi && split[(int64_t)tu * nb + bi])
-          for (int hq = 0; hq < nq; ++hq) v[u] += Pq[hq * pl + (int64_t)tu * Np + i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (t + u < tb) s += v[u];
-  }
-  return s;
-}
-
-// y[i] = sum_{t=0}^{nb-1} P[t, i] over the slots of row i (one rank); EPI: y = sigma y + lam vloc;
-// PQ (with EPI): also the p.q partial sums (vloc = p) of each workgroup -> pq_part
-// (grid = kVecGrid workgroups, grid-stride over the rows).  LANES = 2: two lanes per row, each
-// summing half of the slots (lane 0 the first half), added once (the same bits in both lanes):
-// the kVecGrid grid covers N = 65536 rows with every thread, and each thread waits for half as
-// many round trips (LANES = 1: one lane per row, half the grid idle at that size)
-template <bool EPI, bool PQ, int LANES = 1>
+template <bool EPI, bool PQ>
 __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P,
                                                     const double *__restrict__ Pq,
                                                     const unsigned char *__restrict__ split,
@@ -438,26 +389,54 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
                                                     double *__restrict__ pq_part,
                                                     unsigned long long *__restrict__ ticket,
                                                     const int *__restrict__ status) {
-  static_assert(LANES == 1 || LANES == 2, "one or two lanes per row");
   if (status != nullptr && *status != ST_RUNNING) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   double apq = 0.0;
-  const int ln = LANES == 2 ? (int)(threadIdx.x & 1) : 0;
-  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) / LANES;
-  const int64_t stride = (int64_t)gridDim.x * 256 / LANES;
-  // slot ranges of the lanes: [0, half) and [half, nb), half a multiple of 16
-  const int half = LANES == 2 ? ((nb / 2 + 15) / 16) * 16 : nb;
-  for (int64_t i = i0; i < n_out; i += stride) {
+  const int64_t pl = (int64_t)nb * Np;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_out;
+       i += (int64_t)gridDim.x * 256) {
     const int bi = (int)(i / B);
+    double s = 0.0;
     // slots below t_split hold no split tile for this row block (t_split: the smallest
-    // row-block index of a split tile, nb if none)
+    // row-block index of a split tile, nb if none).  8 slot loads in flight per
+    // thread; the additions stay in slot order
     const int tend = t_split > bi ? t_split : bi + 1;
     const int t8 = tend < nb ? tend : nb;
-    const int ta = ln == 0 ? 0 : (half < nb ? half : nb);
-    const int tb = ln == 0 ? (half < nb ? half : nb) : nb;
-    double s = slot_sum(P, Pq, split, Np, nb, nq, i, bi, ta, tb, t8);
-    if (LANES == 2) s += __shfl_xor(s, 1, 64);
-    if (ln != 0) continue;
+    // (16 in flight: at one row per thread the 512-workgroup PQ grid leaves 1 wave per SIMD,
+    // so the slot loads' round trips are the kernel's time)
+    int t = 0;
+    for (; t + 15 < t8; t += 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; t + 7 < t8; t += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(P + (int64_t)(t + u) * Np + i);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    // the remaining slots (split tiles among them) in batches of 8 as well; every slot
+    // value is ((P + Pq0) + Pq1) + ... + Pq_{nq-1}, added in slot order
+    for (; t < nb; t += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = 0.0;
+        const int tu = t + u;
+        if (tu < nb) {
+          v[u] = P[(int64_t)tu * Np + i];
+          if (tu > bi && split[(int64_t)tu * nb + bi])
+            for (int hq = 0; hq < nq; ++hq) v[u] += Pq[hq * pl + (int64_t)tu * Np + i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (t + u < nb) s += v[u];
+    }
     if (EPI) {
       double yv = sigma * s;
       if (vloc != nullptr) yv += lam * vloc[i];
@@ -730,16 +709,6 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
 
 void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
                           const double *p, double *pq_part, const int *status, hipStream_t s) {
-  // MLFF_SYM_REDUCE_LANES=1 (A/B): one lane per row
-  static const int lanes = [] {
-    const char *e = std::getenv("MLFF_SYM_REDUCE_LANES");
-    return e != nullptr && std::atoi(e) == 1 ? 1 : 2;
-  }();
-  if (lanes == 2)
-    hipLaunchKernelGGL((k_sym_reduce<true, true, 2>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
-                       sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y,
-                       sigma, lam, p, pq_part, sp.ticket, status);
-  else
   hipLaunchKernelGGL((k_sym_reduce<true, true>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
                      sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y, sigma,
                      lam, p, pq_part,
