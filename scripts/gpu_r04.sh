@@ -169,6 +169,15 @@ for s in ${STEPS:-suite smoke bench}; do
     bigprof)  # kernel stats of the large published points at HEAD (the 7-row-wave cluster apply)
       step prof_nt141 600 rocprofv3 --kernel-trace --stats -d $O/prof_nt141 -o nt141 --output-format csv -- python3 bench.py --workload nanotube --m 141 --no-cpu --no-solve --steps 20 --warmup 3
       step prof_eth5833 600 rocprofv3 --kernel-trace --stats -d $O/prof_eth5833 -o eth --output-format csv -- python3 bench.py --workload ethanol --m 5833 --no-cpu --no-solve --steps 30 --warmup 3 ;;
+    rpw)  # rows per workgroup of the one-pass apply (fewer partial vectors vs fewer CUs streaming)
+      for rep in 1 2; do
+        for r in 1 7 10; do
+          step rpw${r}_eth583_r$rep 300 env MLFF_LR_MIN_RPW=$r python bench.py --workload ethanol --m 583 --no-cpu --steps 200 --warmup 20 --no-solve
+        done
+        for r in 1 14; do
+          step rpw${r}_nt_r$rep 300 env MLFF_LR_MIN_RPW=$r python bench.py --workload nanotube --no-cpu --steps 200 --warmup 20 --no-solve
+        done
+      done ;;
     diageth) step diageth 900 python -u scripts/dev/diag_ethanol_refine.py ;;
     calib)  # FETCH_SIZE calibration of k_rec_g's access widths (scripts/dev/pmc_calib.hip)
       step calib_build 120 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 scripts/dev/pmc_calib.hip -o $O/pmc_calib
