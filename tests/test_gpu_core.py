@@ -312,7 +312,7 @@ def test_one_pass_lowrank_apply(sg, monkeypatch, n, k, clusters):
     """The one-pass low-rank apply (k_lr_rows + k_lr_fin: each panel row read once, t_i
     kept in the workgroup) against the two-pass apply (T r, then T^T t) and NumPy, on
     every register-tile width (M = 4, 8, 12, 16 double2 per thread), ragged row groups
-    (k = 1031: 148 groups of 7 rows, the last of 2) and k < one workgroup's rows; rows
+    (k = 1031: 207 groups of 5 rows, the last of 1) and k < one row per workgroup; rows
     longer than 16384 columns take the cluster form (k_lr_cluster: C = 3, 6, 10 workgroups per
     row, all resident clusters or MLFF_LR_CLUSTERS of them, ragged row ranges).  Then a
     PCG solve on both applies, held to the chaotic-regime contract of tests/parity.py (a
