@@ -4,6 +4,13 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (the plain first form), the script
+launches its own N ranks: the parent process -- before it imports the library or touches a
+GPU -- starts N fresh `python bench.py` children with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set (one per GPU, rank r on device r), waits for all of
+them, stops the rest when one fails and exits with the first failing child's status; rank 0
+prints the JSON line to the shared stdout.  Under torchrun (WORLD_SIZE set) it is one rank.
+
 Workload: synthetic SPD RBF kernel, x ~ U[0,1)^3 (numpy default_rng seed 0), length
 scale 0.2, A = K + 1e-6 I, b = sum(x^2), rank-256 Nystrom preconditioner on uniform
 random columns (`random_scores`, seed 0):
@@ -39,6 +46,9 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -118,11 +128,87 @@ def parse():
                          "triangle (auto/sym, ~4 N^2 bytes), dense rows (8 N^2 bytes) or the "
                          "matrix-free sGDML operator; for the sGDML workloads sym / dense "
                          "assemble K on the GPU first (its time in setup_s)")
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="--gpus N > 1 without WORLD_SIZE: seconds the self-launched ranks may "
+                         "take before they are stopped (exit 124)")
     ap.add_argument("--mf-form", choices=["pt", "rec", "pair"], default=None,
                     help="matrix-free sGDML operator form (MLFF_MF_FORM): pair-tile (few atoms), "
                          "record-factored (many atoms) or pair sums; default: the library's "
                          "choice")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 that nothing listens on now (the rendezvous port)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_plan(argv, n: int, port: int, base_env) -> list:
+    """(command, environment) of each of the n rank processes the plain `bench.py --gpus n`
+    launches: the same script and arguments, rank r on local device r, the torchrun variables
+    (RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR, MASTER_PORT)."""
+    plans = []
+    for r in range(n):
+        env = dict(base_env)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plans.append(([sys.executable, "-u", str(Path(__file__).resolve()), *argv], env))
+    return plans
+
+
+def launch_ranks(plans, timeout: float, poll: float = 0.2) -> int:
+    """Start every planned rank as a child process (never exec: this process stays the parent),
+    wait for all of them; when one exits non-zero, or the timeout passes, stop the others
+    (SIGTERM, then SIGKILL after 10 s) and return that status (124 on the timeout), else 0.
+    The children share this process's stdout / stderr, so rank 0's JSON line is the
+    script's output."""
+    procs = []
+    stopping = {"sig": None}
+
+    def on_signal(sig, _frame):
+        stopping["sig"] = sig
+
+    old = {s_: signal.signal(s_, on_signal) for s_ in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for cmd, env in plans:
+            procs.append(subprocess.Popen(cmd, env=env))
+        deadline = time.monotonic() + timeout
+        rc = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                return 0
+            if stopping["sig"] is not None:
+                rc = 128 + int(stopping["sig"])
+                break
+            if time.monotonic() > deadline:
+                print(f"bench.py: ranks still running after {timeout:.0f} s: stopping them",
+                      file=sys.stderr)
+                rc = 124
+                break
+            time.sleep(poll)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.monotonic() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        if rc < 0:  # a child killed by a signal: the shell's convention
+            rc = 128 - rc
+        return rc
+    finally:
+        for s_, h in old.items():
+            signal.signal(s_, h)
 
 
 def dist_setup(args):
@@ -189,17 +275,21 @@ def make_solver(n, rank, world, local, pg):
 
 def csrc_hash() -> str:
     """Content hash of the library sources (csrc/ and include/): PMC traffic figures are
-    only valid for the code they were collected on."""
-    import hashlib
+    only valid for the code they were collected on (build_native.src_hash, which the build
+    also compiles into the library as mlff_build_hash)."""
+    import build_native
 
-    h = hashlib.sha256()
-    files = sorted(list((REPO / "mlff-preconditioner_amd" / "csrc").glob("*"))
-                   + list((REPO / "include").glob("*.h")))
-    for f in files:
-        if f.is_file():
-            h.update(f.relative_to(REPO).as_posix().encode())
-            h.update(f.read_bytes())
-    return h.hexdigest()[:16]
+    return build_native.src_hash()
+
+
+def library_hash() -> str | None:
+    """The source hash compiled into the loaded libmlffpcg.so (None if it cannot be read)."""
+    try:
+        from sgdml_amd import _native
+
+        return _native.build_hash()
+    except Exception:  # noqa: BLE001
+        return None
 
 
 def pmc_traffic(key: str):
@@ -215,6 +305,12 @@ def pmc_traffic(key: str):
     if e is None:
         return None, f"no PMC entry for {key}"
     sha = csrc_hash()
+    lib_sha = library_hash()
+    if lib_sha != sha:
+        print(f"warning: libmlffpcg.so was built from sources {lib_sha}, the tree is {sha}: "
+              f"PMC traffic refused", file=sys.stderr)
+        return None, (f"binary/source mismatch: the loaded library was built from {lib_sha}, "
+                      f"these sources are {sha} (rebuild with build_native.py)")
     if e.get("csrc_sha") != sha:
         return None, (f"stale: PMC entry {key} was collected on sources {e.get('csrc_sha')}, "
                       f"these are {sha} (scripts/pmc_head.py re-collects)")
@@ -581,6 +677,10 @@ def main():
     args = parse()
     if args.solo_world > 1:
         return solo_profile(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # plain `bench.py --gpus N`: launch the N ranks here (nothing has touched a GPU yet)
+        sys.exit(launch_ranks(spawn_plan(sys.argv[1:], args.gpus, free_port(), os.environ),
+                              args.launch_timeout))
     rank, world, local, pg = dist_setup(args)
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)

@@ -95,6 +95,9 @@ typedef struct mlff_ctx mlff_ctx;
 
 /* ---- library / devices ---------------------------------------------------- */
 int mlff_version(void);                       /* 100 * major + minor */
+/* Content hash (16 hex digits) of the csrc/ + include/ sources this binary was built from
+ * (build_native.py src_hash, compiled in at link time): ties a shipped .so to its sources. */
+const char *mlff_build_hash(void);
 int mlff_device_count(int *n_out);
 /* RCCL unique id (128 bytes) for a world > 1 context; rank 0 creates it and the
  * caller broadcasts it (torch.distributed / any channel) to the other ranks. */

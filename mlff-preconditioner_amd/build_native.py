@@ -37,6 +37,36 @@ LDFLAGS = ["-shared", f"--offload-arch={ARCH}", "-L/opt/rocm/lib", "-lrccl",
            "-Wl,-rpath,/opt/rocm/lib"]
 
 
+def src_hash() -> str:
+    """Content hash of the library sources (csrc/ and include/*.h), 16 hex digits: compiled into
+    the library (mlff_build_hash) so that a loaded binary can be tied to the tree it claims to be
+    built from (bench.py checks it before reporting PMC traffic collected on these sources)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(list(CSRC.glob("*")) + list((REPO / "include").glob("*.h")))
+    for f in files:
+        if f.is_file():
+            h.update(f.relative_to(REPO).as_posix().encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def _hash_object(force: bool) -> Path:
+    """build/obj/build_hash.o: mlff_build_hash() returning src_hash(); rewritten and recompiled
+    only when the hash changes."""
+    src = OBJ / "build_hash.cpp"
+    obj = OBJ / "build_hash.o"
+    text = ('extern "C" const char *mlff_build_hash(void) { return "%s"; }\n' % src_hash())
+    if force or not src.exists() or src.read_text() != text or not obj.exists():
+        src.write_text(text)
+        cmd = [HIPCC, "-O2", "-fPIC", "-x", "c++", "-c", str(src), "-o", str(obj)]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"hipcc failed for build_hash.cpp:\n{res.stdout}\n{res.stderr}")
+    return obj
+
+
 def _newest_header() -> float:
     hs = list(CSRC.glob("*.h")) + list((REPO / "include").glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
@@ -63,6 +93,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs.append(_hash_object(force))
     if (force or not LIB.exists()
             or LIB.stat().st_mtime < max(o.stat().st_mtime for o in objs)):
         cmd = [HIPCC, *LDFLAGS, *map(str, objs), "-o", str(LIB)]

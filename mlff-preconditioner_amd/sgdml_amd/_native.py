@@ -45,6 +45,7 @@ _dbl = ctypes.c_double
 
 SIGNATURES = {
     "mlff_version": (_int, []),
+    "mlff_build_hash": (ctypes.c_char_p, []),
     "mlff_device_count": (_int, [_p_int]),
     "mlff_comm_unique_id": (_int, [ctypes.c_char_p]),
     "mlff_comm_selftest": (_int, [_int, _i64, ctypes.POINTER(ctypes.c_double)]),
@@ -164,6 +165,11 @@ def i64ptr(a: np.ndarray | None):
 def i32ptr(a: np.ndarray):
     assert a.dtype == np.int32 and a.flags.c_contiguous
     return a.ctypes.data_as(_p_i32)
+
+
+def build_hash() -> str:
+    """The source hash compiled into the loaded library (build_native.src_hash at build time)."""
+    return load_library().mlff_build_hash().decode()
 
 
 def device_count() -> int:

@@ -30,6 +30,21 @@ def test_library_exports_every_declared_symbol():
     assert lib.mlff_version() == 100
 
 
+def test_library_is_built_from_these_sources():
+    """The shipped .so carries the hash of the sources it was compiled from (mlff_build_hash);
+    it must be the hash of the tree beside it, or every measurement taken with it (and the PMC
+    traffic bench.py reports) would be attributed to the wrong code."""
+    import sys
+
+    sys.path.insert(0, str(REPO / "mlff-preconditioner_amd"))
+    import build_native
+    from sgdml_amd import _native
+
+    assert len(_native.build_hash()) == 16
+    assert _native.build_hash() == build_native.src_hash(), \
+        "libmlffpcg.so is stale: rebuild with mlff-preconditioner_amd/build_native.py"
+
+
 def test_library_is_gfx950_code_object():
     import subprocess
 

@@ -47,6 +47,7 @@ def test_pmc_traffic_is_refused_when_stale(tmp_path, monkeypatch):
         "old/sym/gpus1": {"hbm_bytes_per_launch": 1.0, "csrc_sha": "0123456789abcdef"},
         "unstamped/sym/gpus1": {"hbm_bytes_per_launch": 1.0}}))
     real = bench.REPO
+    monkeypatch.setattr(bench, "library_hash", lambda: bench.csrc_hash())
     monkeypatch.setattr(bench, "REPO", tmp_path)
     (tmp_path / "mlff-preconditioner_amd").symlink_to(real / "mlff-preconditioner_amd")
     (tmp_path / "include").symlink_to(real / "include")
@@ -56,6 +57,10 @@ def test_pmc_traffic_is_refused_when_stale(tmp_path, monkeypatch):
         assert v is None and why.startswith("stale")
     v, why = bench.pmc_traffic("no_such/sym/gpus1")
     assert v is None and "no PMC entry" in why
+    # a binary built from other sources: refused whatever the entry says
+    monkeypatch.setattr(bench, "library_hash", lambda: "feedfacefeedface")
+    v, why = bench.pmc_traffic(key)
+    assert v is None and why.startswith("binary/source mismatch")
 
 
 def test_usable_cores_is_consistent():
@@ -124,3 +129,58 @@ def test_many_point_workload_arguments(monkeypatch):
     assert 27 * 583 in bench.REF_STEP_S_ETHANOL and 27 * 2777 in bench.REF_STEP_S_ETHANOL
     assert bench.REF_STEP_S_ETHANOL[27 * 5833] == 0.550
     assert _args(monkeypatch).mf_form is None          # the library's default form
+
+
+def test_self_launch_plan(monkeypatch):
+    """Plain `bench.py --gpus N` (no WORLD_SIZE): N rank processes of the same script and
+    arguments, rank r on device r, the torchrun variables set, rendezvous on 127.0.0.1."""
+    argv = ["--gpus", "4", "--steps", "3", "--warmup", "1"]
+    plans = bench.spawn_plan(argv, 4, 29511, {"KEEP": "1", "WORLD_SIZE": "9"})
+    assert len(plans) == 4
+    for r, (cmd, env) in enumerate(plans):
+        assert cmd[0] == sys.executable and cmd[-len(argv):] == argv
+        assert cmd[-len(argv) - 1].endswith("bench.py")
+        assert (env["RANK"], env["LOCAL_RANK"], env["WORLD_SIZE"]) == (str(r), str(r), "4")
+        assert env["LOCAL_WORLD_SIZE"] == "4" and env["KEEP"] == "1"
+        assert (env["MASTER_ADDR"], env["MASTER_PORT"]) == ("127.0.0.1", "29511")
+    assert 0 < bench.free_port() < 65536
+
+
+def test_main_self_launches_without_world_size(monkeypatch):
+    """main() hands `--gpus N > 1` without WORLD_SIZE to launch_ranks before it imports the
+    library, and exits with its status; under torchrun (WORLD_SIZE set) it does not."""
+    seen = {}
+
+    def fake_launch(plans, timeout):
+        seen["n"], seen["timeout"] = len(plans), timeout
+        return 7
+
+    monkeypatch.setattr(bench, "launch_ranks", fake_launch)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 7 and seen == {"n": 8, "timeout": 1800.0}
+
+
+def _plan(codes_sleep):
+    """Fake ranks: rank r sleeps s_r seconds, then exits with c_r."""
+    plans = []
+    for r, (c, s) in enumerate(codes_sleep):
+        plans.append(([sys.executable, "-c", f"import time, sys; time.sleep({s}); sys.exit({c})"],
+                      {"RANK": str(r), "PATH": "/usr/bin:/bin"}))
+    return plans
+
+
+def test_launch_ranks_propagates_exit_status():
+    import time
+
+    assert bench.launch_ranks(_plan([(0, 0), (0, 0.2), (0, 0)]), timeout=60) == 0
+    # rank 1 fails while rank 0 would run for a minute: rank 0 is stopped, its status returned
+    t0 = time.monotonic()
+    assert bench.launch_ranks(_plan([(0, 60), (3, 0.1)]), timeout=120) == 3
+    assert time.monotonic() - t0 < 30
+    # ranks past the timeout are stopped: 124
+    t0 = time.monotonic()
+    assert bench.launch_ranks(_plan([(0, 60), (0, 60)]), timeout=1) == 124
+    assert time.monotonic() - t0 < 30
