@@ -674,7 +674,24 @@ int resolve_storage(mlff_ctx *ctx) {
     // the measured rates (mf_seconds) puts first for this rank's share
     const double Np = (double)round_up(ctx->ld, kSymTile);
     const double t_tiles = 10e-6 + 4.0 * Np * Np / ctx->world / 6.9e12;  // 2 launches + stream
-    if (mf_seconds(ctx) < t_tiles) {
+    double t_mf = mf_seconds(ctx);
+    if (ctx->world > 1) {
+      // one decision for all ranks (each models its own share; the slowest rank paces the
+      // iteration): the modelled times are all-reduced as a world-long vector and every rank
+      // takes the same maximum -- ranks that chose differently would run mismatched collectives
+      if (ctx->world > kMaxPart) return set_error(ctx, MLFF_ERR_ARG, "world too large");
+      std::vector<double> t(ctx->world, 0.0);
+      t[ctx->rank] = t_mf;
+      double *buf = ctx->part + 3 * kMaxPart;
+      MLFF_HIP(ctx, hipMemcpyAsync(buf, t.data(), sizeof(double) * ctx->world, hipMemcpyHostToDevice,
+                                   ctx->stream));
+      MLFF_TRY(comm_allreduce(ctx, buf, ctx->world));
+      MLFF_HIP(ctx, hipMemcpyAsync(t.data(), buf, sizeof(double) * ctx->world, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+      MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      t_mf = *std::max_element(t.begin(), t.end());
+    }
+    if (t_mf < t_tiles) {
       ctx->use_sym = false;
       ctx->use_mf = true;
       return MLFF_OK;

@@ -1075,6 +1075,20 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   mf.nz = (int)((D + mf.dslice - 1) / mf.dslice);
   nz = mf.nz;
   MLFF_HIP(ctx, hipMalloc(&mf.part, sizeof(double) * nz * nic * MP));
+  // operator form: the pair-tile one where it exists (few atoms), else the record-factored one
+  // where the records fit, else the pair sums; MLFF_MF_FORM=pt|rec|pair asks for one (A/B, tests).
+  // Decided from the sizes every rank shares (not the local point count), so that the ranks of
+  // a sharded operator model the same form (mf_seconds, resolve_storage); a rank without
+  // points allocates nothing for it
+  const char *ef = std::getenv("MLFF_MF_FORM");
+  const std::string form = ef != nullptr ? ef : "";
+  if ((form.empty() || form == "pt") && !E && pt_supported(D)) {
+    mf.ptile = true;
+    if (mf.ni > 0) {
+      mf.pt_S = pt_chunks(D, mf.ni, MP);
+      MLFF_HIP(ctx, hipMalloc(&mf.ptpart, sizeof(double) * mf.pt_S * mf.ni * pt_padded_d(D)));
+    }
+  }
   // single-column path: the (r = i, s = j) pair records of the local points (3.5 MB for
   // the nanotube, M = 14; ni M n_perms (6 n + 2) doubles in general)
   const double col_bytes = 8.0 * (double)mf.ni * (double)MP * (double)(6 * n + 2);
@@ -1091,9 +1105,10 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
                                  hipMemcpyHostToDevice, s));
     launch_sgdml_records(mf.Rd, mf.Rdd, M, n, D, mf.i0, mf.ni, mf.Pt, mf.piinv_d, n_perms, sig,
                          mf.uvk, s);
-    // the record-factored operator (MLFF_MF_REC=0: the five-kernel pair/F/J^T path)
+    // the record-factored operator (MLFF_MF_REC=0: the five-kernel pair/F/J^T path); its
+    // tables only where that form runs (not under the pair-tile form or MLFF_MF_FORM=pair)
     const char *ev = std::getenv("MLFF_MF_REC");
-    if (ev == nullptr || std::atoi(ev) != 0) {
+    if ((ev == nullptr || std::atoi(ev) != 0) && !mf.ptile && form != "pair") {
       mf.rblk = (n + kRB - 1) / kRB;
       mf.ldw = round_up(mf.ni, kRG);
       const int64_t wrows = round_up(MP, kRJ);
@@ -1108,18 +1123,6 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
       mf.rec_rg = e3 != nullptr ? std::atoi(e3) : 8;
       const char *e4 = std::getenv("MLFF_REC_WC16");
       mf.rec_wc16 = e4 == nullptr || std::atoi(e4) != 0;
-    }
-  }
-  // operator form: the pair-tile one where it exists (few atoms), else the record-factored one
-  // where the records fit, else the pair sums; MLFF_MF_FORM=pt|rec|pair asks for one (A/B, tests)
-  {
-    const char *ef = std::getenv("MLFF_MF_FORM");
-    const std::string form = ef != nullptr ? ef : "";
-    if (form == "pair") mf.rec = false;
-    if ((form.empty() || form == "pt") && !E && mf.ni > 0 && pt_supported(D)) {
-      mf.ptile = true;
-      mf.pt_S = pt_chunks(D, mf.ni, MP);
-      MLFF_HIP(ctx, hipMalloc(&mf.ptpart, sizeof(double) * mf.pt_S * mf.ni * pt_padded_d(D)));
     }
   }
   if (mf.ni > 0) {

@@ -1324,8 +1324,10 @@ __global__ __launch_bounds__(256) void k_gemv_xr(const double *__restrict__ M, i
 
 bool xr_fold_fits(int64_t ncols, int splits, int64_t n) {
   const int64_t n2 = ncols / 2, cs2 = (n2 + splits - 1) / splits;
+  // the owner loop writes rr_part[b0 / 256] for every b0 < ncols (the padded block, which can
+  // exceed the last rank's row count n): both must fit the kVecGrid partial slots
   return ncols % 2 == 0 && (2 * cs2) % 256 == 0 && cs2 * 16 <= 64 * 1024 &&
-         n <= (int64_t)kVecGrid * 256;
+         n <= (int64_t)kVecGrid * 256 && ncols <= (int64_t)kVecGrid * 256;
 }
 
 void launch_gemv_xr(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,

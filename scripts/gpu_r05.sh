@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-5 GPU session: STEPS (space separated) from
+#   suite     driver-exact `pytest -m gpu` (per-test timeout, progress log)
+#   smoke     __graft_entry__.smoke()
+#   bench     default bench line (python bench.py)
+#   rehearse  MLFF_BENCH_REHEARSE=1 python bench.py --gpus 8: the self-launched 8-rank flow on
+#             one GPU (SOLO ranks, gloo; not a measurement)
+#   nt        nanotube bench line (configs[1])
+#   tests     pytest of $TESTS (-v -s)
+#   prof      rocprofv3 --kernel-trace --stats of the default bench command
+#   pmc       scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes)
+#   cmd       $CMD (one free-form step, $LIM seconds)
+# every GPU step runs under its own timeout; the first failure ends the script
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r05
+mkdir -p $O
+step() {
+  local name=$1 lim=$2; shift 2
+  echo "== $name $(date +%T)" | tee -a $O/steps.log
+  timeout -k 10 $lim "$@" > $O/$name.txt 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)" | tee -a $O/steps.log
+  if [ $rc -ne 0 ]; then tail -30 $O/$name.txt; exit $rc; fi
+}
+for s in ${STEPS:-suite smoke bench}; do
+  case $s in
+    suite) step suite 1100 python -u -m pytest tests -x -q -m gpu --timeout 900 --timeout-method thread ${PYTEST_EXTRA:-} ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench_default 600 python bench.py ;;
+    rehearse) step rehearse_w8 600 env MLFF_BENCH_REHEARSE=1 python bench.py --gpus 8 --steps 20 --warmup 3 --launch-timeout 500 ;;
+    nt) step bench_nanotube 300 python bench.py --workload nanotube ;;
+    tests) step tests 1100 python -u -m pytest -x -v -s --timeout 600 --timeout-method thread ${TESTS} ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
+    pmc) step pmc 900 python scripts/pmc_head.py ;;
+    cmd) step ${NAME:-cmd} ${LIM:-600} bash -c "$CMD" ;;
+  esac
+done
+echo "== all steps ok"

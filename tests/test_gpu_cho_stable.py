@@ -58,7 +58,8 @@ CASES = [(1, 0.5, 0.5, None), (2, 1e-3, 1.0, None), (5, 1e-8, 2.0, None),
 @pytest.mark.parametrize("m,lo,hi,lo_eig", CASES + [(17, 1e-6, 1.0, None), (520, 1e-9, 1.0, 2e-13)])
 def test_sym_min_eig_vs_lapack(sg, monkeypatch, m, lo, hi, lo_eig, blocked):
     """Both reductions of kernels_syev.hip: per column (dsytd2) and blocked in 16-column panels
-    with the trailing update as one GEMM per panel (dsytrd / dlatrd; the default from m = 512),
+    with the trailing update as one GEMM per panel (dsytrd / dlatrd; opt-in with
+    MLFF_SYEV_BLOCKED=1, the per-column form is the default: it measured faster),
     partial last panels included (m = 5, 17, 100, 129, 300, 520, 700)."""
     monkeypatch.setenv("MLFF_SYEV_BLOCKED", blocked)
     M = spd_with_spectrum(m, lo, hi, seed=m, lo_eig=lo_eig)
