@@ -697,7 +697,7 @@ int resolve_storage(mlff_ctx *ctx) {
       return MLFF_OK;
     }
   }
-  if (ctx->storage == MLFF_STORAGE_DENSE) {
+  if (ctx->storage == MLFF_STORAGE_DENSE || ctx->exact_sums) {  // the exact-sum anchor: rows
     MLFF_TRY(ensure_rows(ctx));
     ctx->use_sym = false;
     return MLFF_OK;
@@ -754,6 +754,14 @@ int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const do
   hipStream_t s = ctx->stream;
   if (ctx->use_mf) {
     launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part, pf);
+    return MLFF_OK;
+  }
+  if (ctx->exact_sums) {  // measurement anchor (kernels_dd.hip): dense rows, one rank
+    if (ctx->use_sym || ctx->world > 1)
+      return set_error(ctx, MLFF_ERR_STATE, "MLFF_EXACT_SUMS: dense-row storage on one rank only");
+    launch_dd_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->N, v_full, y_loc, ctx->sigma_K, ctx->lam,
+                        v_loc, status, s);
+    if (pq_part != nullptr) launch_dot_part(v_loc, y_loc, ctx->nrows, pq_part, status, s);
     return MLFF_OK;
   }
   if (!ctx->use_sym) {
@@ -987,7 +995,12 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
   const double *zsrc;
   if (lowrank) {
     const size_t pm = mark_begin(ctx, marks);
-    if (ctx->lr_rows) {
+    if (ctx->exact_sums) {  // measurement anchor: two double-double passes, rho separately
+      if (fold.st != nullptr) launch_stoptest(rr_part(ctx), ctx->st, ctx->trace, it - 1, s);
+      launch_dd_lowrank(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
+                        1.0 / ctx->lam, ctx->tpart, status, s);
+      launch_dot_part(ctx->r, ctx->z, ctx->nrows, rho_part(ctx), status, s);
+    } else if (ctx->lr_rows) {
       launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
                            1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold, xf);
     } else if (ctx->lr_cluster) {
@@ -1172,6 +1185,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1)
     return set_error(nullptr, MLFF_ERR_HIP, "no HIP device available");
   if (device < 0 || device >= ndev) return set_error(nullptr, MLFF_ERR_ARG, "bad device id");
+  if (world > 1 && std::getenv("MLFF_EXACT_SUMS") != nullptr && std::atoi(std::getenv("MLFF_EXACT_SUMS")) != 0)
+    return set_error(nullptr, MLFF_ERR_ARG, "MLFF_EXACT_SUMS runs on one rank");
   mlff_ctx *ctx = new mlff_ctx();
   ctx->device = device;
   for (auto [name, flag] : {std::pair<const char *, bool *>{"MLFF_FUSE_P", &ctx->fuse_p},
@@ -1183,6 +1198,7 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_NYS_REFINE")) ctx->nys_refine = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_EXACT_SUMS")) ctx->exact_sums = std::atoi(e) != 0;
   ctx->rank = rank;
   ctx->world = world;
   ctx->N = n_global;
@@ -1783,6 +1799,15 @@ int mlff_precon_apply(mlff_ctx *ctx, const double *r_local, double *z_local) {
     MLFF_HIP(ctx, hipMemcpyAsync(zd, rd, sizeof(double) * ctx->blk, hipMemcpyDeviceToDevice, s));
   } else {
     ctx->spec_t = false;  // tpart is reused below
+    if (ctx->exact_sums) {  // the measurement anchor's apply (kernels_dd.hip)
+      launch_dd_lowrank(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p, 1.0 / ctx->lam,
+                        ctx->tpart, nullptr, s);
+      MLFF_HIP(ctx, hipGetLastError());
+      if (ctx->nrows > 0)
+        MLFF_HIP(ctx, hipMemcpyAsync(z_local, zd, sizeof(double) * ctx->nrows, hipMemcpyDeviceToHost, s));
+      MLFF_HIP(ctx, hipStreamSynchronize(s));
+      return MLFF_OK;
+    }
     if (ctx->lr_rows || ctx->lr_cluster) {
       if (ctx->lr_rows) {
         launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, rd, zd, ctx->nrows, ctx->sigma_p,

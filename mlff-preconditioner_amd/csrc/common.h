@@ -348,6 +348,9 @@ struct mlff_ctx {
   // Nystrom panel (MLFF_NYS_REFINE)
   bool wb_refine = true;
   bool nys_refine = false;
+  // exact-sum anchor (MLFF_EXACT_SUMS=1, kernels_dd.hip): dense-row operator and two-pass low-rank
+  // apply with double-double dot products rounded once per entry; one rank; measurement only
+  bool exact_sums = false;
   bool lr_cluster = false;     // the same for long rows (launch_lr_apply_cluster)
   int lr_q = 0;                // its clusters
   double *lr_zpart = nullptr;  // lr_rows_groups(k) (or lr_q) x blk partials
@@ -534,6 +537,13 @@ void launch_update_xr_shares(double *x, double *r, const double *p, const double
 // and T r_new, the bits of the two launches; xr_fold_fits: the split / row-count shapes it
 // covers
 bool xr_fold_fits(int64_t ncols, int splits, int64_t n);
+// kernels_dd.hip (MLFF_EXACT_SUMS): y = sigma fl(M v) + lam vloc with double-double row sums;
+// z = sigma_p lam_inv (r - fl(T^T fl(T r))) with double-double dot products (t: k doubles)
+void launch_dd_gemv_rows(const double *M, int64_t ld, int64_t rows, int64_t ncols, const double *v,
+                         double *y, double sigma, double lam, const double *vloc, const int *status,
+                         hipStream_t s);
+void launch_dd_lowrank(const double *T, int64_t ldt, int64_t k, const double *r, double *z, int64_t n,
+                       double sigma_p, double lam_inv, double *t, const int *status, hipStream_t s);
 void launch_gemv_xr(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
                     const double *r, double *r_out, double *x, const double *p, const double *y,
                     const double *shares, int world, int64_t n, double sigma, double lam,

@@ -1,0 +1,126 @@
+"""The exact-sum anchor (MLFF_EXACT_SUMS=1, csrc/kernels_dd.hip) and what it says about the
+headline system's iteration count.
+
+At lambda = 1e-6 the configs[2] PCG (iterative_solver.py:995-1005, Nystrom random_scores) is
+chaotic under the summation order of its mat-vec and panel apply: the oracle's six orders spread
+over 3.2 % of the count at N = 8192 and 4.3 % at 32768 (tests/golden/rbf_band_n*.json).  The
+anchor removes that source: every dot product of the operator and of the apply is carried in
+double-double and rounded once, as tests/golden/make_rbf_band.py --ld does with np.longdouble on
+the CPU (rbf_ld_n8192.json: 2847 iterations, rbf_ld_n16384.json: 4474).
+* the anchor's outputs ARE the correctly rounded exact sums (checked against Python's exact
+  rational arithmetic on a small case);
+* its solve lands on the long-double oracle's count at N = 8192 and 16384;
+* at N = 65536 (configs[2] itself, no CPU long-double run: ~40 h) its count is the reference
+  point the fp64 solves are held to (tests/golden/rbf_dd_n65536.json, make_dd_anchor.py).
+"""
+import json
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LAM, ELL, K, TOL = 1e-6, 0.2, 256, 1e-6
+
+
+@pytest.fixture
+def exact(monkeypatch):
+    monkeypatch.setenv("MLFF_EXACT_SUMS", "1")
+
+
+def _exact_dot(a, b):
+    """The correctly rounded fp64 value of sum_i a_i b_i (exact rationals)."""
+    return float(sum((Fraction(float(x)) * Fraction(float(y)) for x, y in zip(a, b)), Fraction(0)))
+
+
+def test_exact_sums_are_correctly_rounded(exact):
+    """Operator rows and both panel passes of the anchor equal fl(exact sum) -- bit for bit on
+    all but (at most) a handful of entries, and within one ulp on every entry."""
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    n, k = 300, 24
+    X, _ = synthetic.rbf_points(n, 3, 3)
+    rng = np.random.default_rng(1)
+    v = rng.standard_normal(n) * np.exp(rng.uniform(-8, 8, n))   # wide dynamic range: cancellation
+    T = rng.standard_normal((k, n))
+    r = rng.standard_normal(n)
+    with sgdml_amd.KernelSolver(n) as s:
+        s.gen_rbf(X, ELL)
+        s.set_operator(1.0, LAM)
+        s.set_storage("dense")
+        Kd = s.get_matrix_rows()
+        y = s.matvec(v)
+        s.precon_lowrank(T)
+        z = s.precon_apply(r)
+    y_ex = np.array([_exact_dot(Kd[i], v) for i in range(n)]) + LAM * v
+    t_ex = np.array([_exact_dot(T[j], r) for j in range(k)])
+    u_ex = np.array([_exact_dot(T[:, i], t_ex) for i in range(n)])
+    z_ex = 1.0 * ((1.0 / LAM) * (r - u_ex))
+    for got, ref in ((y, y_ex), (z, z_ex)):
+        ulp = np.abs(got - ref) / np.spacing(np.abs(ref))
+        assert ulp.max() <= 1.0, ulp.max()
+        assert np.count_nonzero(got != ref) <= 3, np.count_nonzero(got != ref)
+    # and an fp64 summation order is NOT the exact sum (the test can tell the two apart)
+    assert np.count_nonzero(Kd @ v + LAM * v != y_ex) > 0
+
+
+def exact_solve(n, maxiter):
+    import sgdml_amd
+    from sgdml_amd import synthetic
+
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, K, replace=False))
+    with sgdml_amd.KernelSolver(n) as s:
+        s.gen_rbf(X, ELL)
+        s.set_operator(1.0, LAM)
+        s.set_storage("dense")
+        s.precon_nystrom(idx)
+        return s.pcg(b, tol=TOL, maxiter=maxiter)
+
+
+@pytest.mark.parametrize("n", [8192, 16384])
+def test_anchor_matches_long_double_oracle(golden_dir, exact, n):
+    """The GPU anchor against the CPU oracle in np.longdouble (make_rbf_band.py --ld): two
+    independent near-exact evaluations of the same solve (different K and panel roundings, a
+    64-bit vs a ~106-bit significand, fp64 recurrences in different orders) land together, far
+    inside the fp64 band (b_it 95 / 176)."""
+    ld = json.loads((golden_dir / f"rbf_ld_n{n}.json").read_text())
+    bd = json.loads((golden_dir / f"rbf_band_n{n}.json").read_text())
+    r = exact_solve(n, 5 * n)
+    print(f"N={n}: exact-sum GPU {r.iters} vs long-double oracle {ld['iters']} iterations; fp64 "
+          f"orders {sorted(v['iters'] for v in bd['variants'].values())}")
+    assert r.info == 0
+    assert abs(r.iters - ld["iters"]) <= max(8, bd["band_iters"] // 8), (r.iters, ld["iters"])
+
+
+@pytest.mark.timeout(900)
+def test_configs2_fp64_count_held_to_exact_anchor(golden_dir, monkeypatch):
+    """configs[2] (N = 65536): the anchor's count (recomputed here and equal to the committed
+    rbf_dd_n65536.json) and the fp64 GPU solve held to it.  The fp64 tolerance is the largest
+    distance of an fp64 order from the near-exact count MEASURED at the smaller sizes (oracle
+    orders and GPU vs rbf_ld_n8192 / 16384), as a fraction of the count, times this count."""
+    import sgdml_amd  # noqa: F401
+
+    from tests.test_gpu_rbf_band import gpu_solve
+
+    path = golden_dir / "rbf_dd_n65536.json"
+    if not path.exists():
+        pytest.fail("tests/golden/rbf_dd_n65536.json missing (tests/golden/make_dd_anchor.py)")
+    fx = json.loads(path.read_text())
+    n = 65536
+    monkeypatch.setenv("MLFF_EXACT_SUMS", "1")
+    ra = exact_solve(n, 20000)
+    monkeypatch.delenv("MLFF_EXACT_SUMS")
+    assert ra.info == 0
+    assert ra.iters == fx["iters"], (ra.iters, fx["iters"])
+    _, _, _, r = gpu_solve(n, 20000)
+    frac = max(fx["fp64_distance_fraction"].values())
+    tol = int(np.ceil(frac * ra.iters)) + 2
+    print(f"N={n}: fp64 GPU {r.iters} vs exact-sum anchor {ra.iters} (tolerance {tol}, "
+          f"{frac:.4f} of the count); oracle orders {fx['oracle_fp64_iters']}")
+    assert r.info == 0
+    assert abs(r.iters - ra.iters) <= tol, (r.iters, ra.iters, tol)
+    rel = np.linalg.norm(r.x - ra.x) / np.linalg.norm(ra.x)
+    assert rel <= 1e-5, rel
