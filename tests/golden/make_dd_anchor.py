@@ -83,8 +83,9 @@ def main():
             if name == "rbf_solve_n65536.npz":
                 out["oracle_rel_dx"] = float(np.linalg.norm(f["x"] - ra.x) / np.linalg.norm(ra.x))
     out["oracle_fp64_iters"] = orc
-    np.savez_compressed(GOLDEN / "rbf_dd_n65536_trace.npz", trace=ra.trace, x=ra.x)
-    (GOLDEN / "rbf_dd_n65536.json").write_text(json.dumps(out, indent=1, sort_keys=True))
+    dest = Path(os.environ.get("MLFF_GOLDEN_OUT", GOLDEN))  # gpurun: a gpurun_out/ directory
+    dest.mkdir(parents=True, exist_ok=True)
+    (dest / "rbf_dd_n65536.json").write_text(json.dumps(out, indent=1, sort_keys=True))
     print(json.dumps(out), flush=True)
 
 

@@ -44,7 +44,7 @@ def test_exact_sums_are_correctly_rounded(exact):
     X, _ = synthetic.rbf_points(n, 3, 3)
     rng = np.random.default_rng(1)
     v = rng.standard_normal(n) * np.exp(rng.uniform(-8, 8, n))   # wide dynamic range: cancellation
-    T = rng.standard_normal((k, n))
+    L = rng.standard_normal((k, n))
     r = rng.standard_normal(n)
     with sgdml_amd.KernelSolver(n) as s:
         s.gen_rbf(X, ELL)
@@ -52,7 +52,8 @@ def test_exact_sums_are_correctly_rounded(exact):
         s.set_storage("dense")
         Kd = s.get_matrix_rows()
         y = s.matvec(v)
-        s.precon_lowrank(T)
+        s.precon_lowrank(L)          # Woodbury panel T of L (built on the device, fp64)
+        T = s.precon_panel()
         z = s.precon_apply(r)
     y_ex = np.array([_exact_dot(Kd[i], v) for i in range(n)]) + LAM * v
     t_ex = np.array([_exact_dot(T[j], r) for j in range(k)])
