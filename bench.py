@@ -469,6 +469,12 @@ def rbf_band():
     return bd, full
 
 
+def exact_anchor():
+    """The configs[2] exact-sum anchor (tests/golden/rbf_dd_n65536.json) or None."""
+    p = REPO / "tests" / "golden" / "rbf_dd_n65536.json"
+    return json.loads(p.read_text()) if p.exists() else None
+
+
 def parity_small(n, k, lam, ell, tol=1e-6):
     """Same generator at N = 8192: GPU vs CPU-oracle iterations to relres 1e-6, with the
     measured noise band of that count (|d iters| <= 2 b_it + 2 is in band, tests/parity.py)."""
@@ -819,24 +825,31 @@ def main():
         bd, full = rbf_band()
         if sg_info is None and n == 65536 and k == 256 and full is not None and bd is not None:
             # the CPU oracle's solve of this very system (committed fixture, ~2 h of CPU time:
-            # make_rbf_band.py --full), held to the N = 8192 band scaled by the count
-            scale = full["iters"] / bd["ref_iters"]
-            b_it = int(np.ceil(bd["band_iters"] * scale))
-            # the band's growth measured at 8192 / 16384 / 32768 (b_it / iters linear in
-            # log2 N, tests/golden/make_rbf_band.py), extrapolated to this N
-            g = REPO / "tests" / "golden"
-            pts = [(np.log2(m), json.loads((g / f"rbf_band_n{m}.json").read_text()))
-                   for m in (8192, 16384, 32768) if (g / f"rbf_band_n{m}.json").exists()]
-            if len(pts) >= 2:
-                c = np.polyfit([p[0] for p in pts],
-                               [p[1]["band_iters"] / p[1]["ref_iters"] for p in pts], 1)
-                solve["band_fraction_extrapolated"] = float(np.polyval(c, np.log2(n)))
-                b_it = max(b_it, int(np.ceil(solve["band_fraction_extrapolated"] * full["iters"])))
+            # make_rbf_band.py --full; a second summation order beside it)
             x_cpu = full.pop("_x")
             solve["cpu_ref"] = dict(full, source="tests/golden/rbf_solve_n65536.npz")
-            solve["band_iters_scaled"] = b_it
-            ok = abs(res.iters - full["iters"]) <= 2 * b_it + 2
+            anchor = exact_anchor()
+            if anchor is not None:
+                # the count with exact sums (double-double operator and apply, measured on the
+                # GPU: make_dd_anchor.py); an fp64 order is in band when it lands within the
+                # distance fp64 orders were MEASURED to land from the exact count at N = 8192 /
+                # 16384 (the oracle's six orders against its long-double solve, the GPU's)
+                frac = max(anchor["fp64_distance_fraction"].values())
+                tol_it = int(np.ceil(frac * anchor["iters"])) + 2
+                solve["exact_anchor"] = {
+                    "iters": anchor["iters"], "source": "tests/golden/rbf_dd_n65536.json",
+                    "tolerance_iters": tol_it, "fp64_distance_fraction": frac,
+                    "gpu_minus_anchor": int(res.iters) - anchor["iters"],
+                    "oracle_minus_anchor": [full["iters"] - anchor["iters"]]
+                    + ([full["second_order_iters"] - anchor["iters"]]
+                       if "second_order_iters" in full else [])}
+                ok = abs(res.iters - anchor["iters"]) <= tol_it
+            else:  # no anchor committed: the oracle's count with the N = 8192 band scaled
+                b_it = int(np.ceil(bd["band_iters"] * full["iters"] / bd["ref_iters"]))
+                solve["band_iters_scaled"] = b_it
+                ok = abs(res.iters - full["iters"]) <= 2 * b_it + 2
             if world == 1:  # ||dx|| / ||x|| against the oracle's x, and its scaled band
+                scale = full["iters"] / bd["ref_iters"]
                 solve["rel_dx_vs_cpu_ref"] = float(np.linalg.norm(res.x - x_cpu) /
                                                    np.linalg.norm(x_cpu))
                 solve["band_rel_dx_scaled"] = float(bd["band_rel_dx"] * max(1.0, scale))

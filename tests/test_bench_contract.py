@@ -184,3 +184,19 @@ def test_launch_ranks_propagates_exit_status():
     t0 = time.monotonic()
     assert bench.launch_ranks(_plan([(0, 60), (0, 60)]), timeout=1) == 124
     assert time.monotonic() - t0 < 30
+
+
+def test_exact_anchor_fixture_is_consistent():
+    """tests/golden/rbf_dd_n65536.json (make_dd_anchor.py, GPU): the anchor the bench's
+    solve_to_1e-6 holds the configs[2] count to; its oracle fractions restate the committed
+    long-double and six-order band files."""
+    a = bench.exact_anchor()
+    assert a is not None and a["n"] == 65536 and a["k"] == 256 and a["info"] == 0
+    g = bench.REPO / "tests" / "golden"
+    for n in (8192, 16384):
+        ld = json.loads((g / f"rbf_ld_n{n}.json").read_text())["iters"]
+        bd = json.loads((g / f"rbf_band_n{n}.json").read_text())
+        assert a["anchors"][str(n)]["oracle_long_double"] == ld
+        frac = max(abs(v["iters"] - ld) for v in bd["variants"].values()) / ld
+        assert a["fp64_distance_fraction"][f"oracle_fp64_n{n}"] == pytest.approx(frac)
+    assert a["oracle_fp64_iters"]["rbf_solve_n65536.npz"] == 8528
