@@ -475,6 +475,45 @@ def exact_anchor():
     return json.loads(p.read_text()) if p.exists() else None
 
 
+SGDML_FIXTURES = {("nanotube", 15540): "nanotube_n15540", ("ethanol", 15741): "ethanol_n15741"}
+
+
+def first_below(trace, tol) -> int | None:
+    """First iteration j >= 1 whose stop-test residual is <= tol * ||r_0|| (x0 = 0: ||b||)."""
+    tr = np.asarray(trace)
+    hit = np.nonzero(tr[1:] <= tol * tr[0])[0]
+    return int(hit[0]) + 1 if hit.size else None
+
+
+def sgdml_parity(workload, n, k, res):
+    """The sGDML solve against the CPU oracle's run of the same system at full size, when one is
+    committed (make_nanotube_full.py / make_ethanol_full.py): iterations to tol 1e-6 and (where
+    recorded) 1e-4 -- the reference's training tolerance, train.py:309 -- held to the band the
+    oracle measured over its own summation orders (|d it| <= 2 b_it + 2, tests/parity.py)."""
+    name = SGDML_FIXTURES.get((workload, n))
+    g = REPO / "tests" / "golden"
+    if name is None or not (g / f"{name}_band.json").exists():
+        return None
+    fx = json.loads((g / f"{name}_band.json").read_text())
+    out = {"source": f"tests/golden/{name}_band.json"}
+    if "bands" in fx:
+        cases = {t: fx["bands"].get(f"k{k}_tol{t:g}") for t in (1e-4, 1e-6)}
+    else:  # the nanotube fixture: one rank, tol 1e-6
+        cases = {1e-6: fx if fx.get("k") == k else None}
+    ok = True
+    for tol, b in cases.items():
+        if b is None:
+            continue
+        it = first_below(res.trace, tol)
+        e = {"gpu_iters": it, "cpu_ref_iters": b["ref_iters"], "band_iters": b["band_iters"],
+             "oracle_orders": {o: v["iters"] for o, v in b["variants"].items()}}
+        e["in_band"] = bool(it is not None and abs(it - b["ref_iters"]) <= 2 * b["band_iters"] + 2)
+        ok = ok and e["in_band"]
+        out[f"tol_{tol:g}"] = e
+    out["in_band"] = ok
+    return out
+
+
 def parity_small(n, k, lam, ell, tol=1e-6):
     """Same generator at N = 8192: GPU vs CPU-oracle iterations to relres 1e-6, with the
     measured noise band of that count (|d iters| <= 2 b_it + 2 is in band, tests/parity.py)."""
@@ -524,7 +563,9 @@ def sgdml_workload(args, rank, world, local, pg):
         name = "nanotube"
     else:
         M = args.m or 111
-        ds = synthetic.ethanol_like(M, seed=0)
+        # energy-consistent labels (F = -grad E of a pair-harmonic potential): random force
+        # labels put relres 1e-6 at the system's attainable-accuracy floor
+        ds = synthetic.ethanol_harmonic(M, seed=0)
         name = "ethanol"
     n_atoms = ds["R"].shape[1]
     n = 3 * n_atoms * M
@@ -822,6 +863,8 @@ def main():
         t_solve = max_over_ranks(pg, time.perf_counter() - t1)
         solve = {"tol": 1e-6, "iters": int(res.iters), "info": int(res.info),
                  "seconds": t_solve, "final_relres": float(res.resid / np.linalg.norm(b))}
+        if sg_info is not None:
+            solve["cpu_ref"] = sgdml_parity(args.workload, n, k, res)
         bd, full = rbf_band()
         if sg_info is None and n == 65536 and k == 256 and full is not None and bd is not None:
             # the CPU oracle's solve of this very system (committed fixture, ~2 h of CPU time:

@@ -194,6 +194,12 @@ struct Timing {
 };
 
 
+// the search direction of the fused forms: p = z at ITER 1, else fma(beta, p_old, z)
+// (k_update_p's arithmetic)
+__device__ __forceinline__ double fused_p(double pold, double z, double beta, bool first) {
+  return first ? z : fma(beta, pold, z);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
@@ -689,16 +695,22 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
                         const double *x_loc, const int *status, double sigma, double lam,
                         double *pq_part = nullptr, const PFuse *pf = nullptr);
 int mf_diag(mlff_ctx *ctx, double *out);
-// Zt = (J_j x_j)[P_p] of every (j, p) (k_mf_z), status gated
-void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s);
+// Zt = (J_j x_j)[P_p] of every (j, p) (k_mf_z), status gated.  pf: the operand is the search
+// direction p = z + beta p_old formed on the fly from xc = p_old (k_update_p's arithmetic, the
+// same bits), and the previous iteration's stop test runs in its first workgroup (pf->sf)
+void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s,
+                  const PFuse *pf = nullptr);
 // pair-tile form (kernels_pt.hip): available for D <= 288; its (j, p) chunks, padded D and the
 // operator y_loc = sigma K x + lam x_loc (+ the x_loc . y_loc partials when pq_part is set)
 bool pt_supported(int64_t D);
 int pt_chunks(int64_t D, int64_t ni, int64_t MP);
 int64_t pt_padded_d(int64_t D);
+// pf (one rank, every row here): the search-direction update fused (k_mf_z forms p on the fly,
+// k_pt_fin writes it) and the previous iteration's stop test folded into k_mf_z
 void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, int64_t row0,
                         int64_t nrows, const double *x_loc, double *y_loc, const int *status,
-                        double sigma, double lam, double *pq_part, hipStream_t s);
+                        double sigma, double lam, double *pq_part, hipStream_t s,
+                        const PFuse *pf = nullptr);
 // operator form in use: 0 pair sums (k_mf_pair ...), 1 record-factored, 2 pair-tile
 int mf_form(const mlff_ctx *ctx);
 // sigma K_op columns through the single-column path (mf.uvk); false when it is not set up

@@ -97,6 +97,10 @@ __device__ __forceinline__ double z_entry(const ZSrc &zs, int64_t D, int64_t jp,
   return z;
 }
 
+// FP: the operand is the search direction p = fused_p(x, pf.z) (beta = rho / rho1 with rho the
+// fixed-order sum of the rho partials: k_update_p's bits), and block (0, 0) runs the previous
+// iteration's stop test (pf.sf, as k_rec_g does) and publishes rho for k_pt_fin
+template <bool FP = false>
 __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               const int32_t *__restrict__ Pt,
                                               const int32_t *__restrict__ ps,
@@ -104,12 +108,41 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               int n, int n_perms, int64_t D,
                                               const double *__restrict__ x,
                                               double *__restrict__ Zt,
-                                              const int *__restrict__ status) {
+                                              const int *__restrict__ status, PFuse pf = PFuse{}) {
   if (status != nullptr && *status != ST_RUNNING) return;
   const int64_t jp = blockIdx.y;
   const ZSrc zs{Rdd, Pt, ps, pt, n, n_perms, x, Zt};
-  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)
-    Zt[jp * D + d] = z_entry(zs, D, jp, d);
+  if (!FP) {
+    for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)
+      Zt[jp * D + d] = z_entry(zs, D, jp, d);
+    return;
+  }
+  __shared__ double shp[8];
+  const bool first = pf.it <= 1, sfold = pf.sf.rr_part != nullptr;
+  // rho1 as the (folded) stop test of the previous iteration leaves it
+  const double rho1 = sfold ? pf.st->rho : pf.st->rho1;
+  const double rho = parts_bcast(parts_thread_sum(pf.rho_part, kVecGrid), shp);
+  const double beta = rho / rho1;
+  if (blockIdx.x == 0 && blockIdx.y == 0) {
+    if (threadIdx.x == 0) pf.st->rho_new = rho;
+    if (sfold) stop_decide(pf.sf, reduce_parts_bcast(pf.sf.rr_part, kVecGrid, shp));
+  }
+  const int64_t j = jp / zs.n_perms, p = jp % zs.n_perms;
+  const int64_t g0 = j * 3 * zs.n;
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
+    const int64_t e = zs.Pt != nullptr ? (int64_t)zs.Pt[p * D + d] : d;
+    const int sa = zs.ps[e], ta = zs.pt[e];
+    const double *r = zs.Rdd + (j * D + e) * 3;
+    double z = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int64_t it_ = g0 + 3 * ta + c, is_ = g0 + 3 * sa + c;
+      const double xt = fused_p(x[it_], pf.z[it_], beta, first);
+      const double xs = fused_p(x[is_], pf.z[is_], beta, first);
+      z = fma(r[c], xt - xs, z);
+    }
+    Zt[jp * D + d] = z;
+  }
 }
 
 // Partial pair sums over the descriptor slice z of this workgroup for a tile of
@@ -568,9 +601,6 @@ struct RecArgs {
 };
 
 // the operand entry of a fused update (k_update_p: p = fma(beta, p_old, z), p = z at ITER 1)
-__device__ __forceinline__ double fused_p(double pold, double z, double beta, bool first) {
-  return first ? z : fma(beta, pold, z);
-}
 
 // wt: w transposed, round_up(MP, kRJ) rows of ldw = ngrp kRG entries, zero padded, so
 // the accumulation runs unguarded over whole batches and point groups
@@ -1140,11 +1170,15 @@ int mf_setup(mlff_ctx *ctx, const double *R_desc, const double *R_d_desc, int64_
   return MLFF_OK;
 }
 
-// the fused p update runs in the default record-factored form only: one rank, one identity
-// permutation, <= 16 local points, w in one 16-slot chunk (the nanotube configs[1] system)
+// the fused p update: one rank holding every row, in the pair-tile form (few atoms) or in the
+// default record-factored form with one identity permutation, <= 16 local points, w in one
+// 16-slot chunk (the nanotube configs[1] system)
 bool mf_can_fuse_p(const mlff_ctx *ctx) {
   const MfData &mf = ctx->mf;
-  return ctx->fuse_p && ctx->world == 1 && mf.rec && !mf.ptile && mf.ident && mf.ni > 0 && mf.ni <= kRG &&
+  if (!ctx->fuse_p || ctx->world != 1 || mf.ni <= 0 || ctx->nrows != ctx->N) return false;
+  // the pair-tile form: k_mf_z forms p, k_pt_fin writes it (any permutation set)
+  if (mf.ptile) return !mf.E;
+  return mf.rec && mf.ident && mf.ni <= kRG &&
          mf.rec_rg == 8 && round_up(mf.M * mf.n_perms, kRJ) <= 16 && mf.rec_wc16 &&
          ctx->nrows == ctx->N;
 }
@@ -1171,7 +1205,7 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
   }
   if (mf.ptile) {
     launch_pt_operator(mf, mf.ident ? mf.Rd : mf.Rt, xc, ctx->row0, ctx->nrows, x_loc, y_loc, status,
-                       sigma, lam, pq_part, s);
+                       sigma, lam, pq_part, s, pf);
     return;
   }
 #ifdef MLFF_REC_TRACE
@@ -1195,9 +1229,9 @@ void launch_mf_operator(const mlff_ctx *ctx, const double *x_full, double *y_loc
     const double *wt = mf.wt;
     if (ngrp > 1) {  // Zt once (k_mf_z), read by every point group
       const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
-      hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd,
+      hipLaunchKernelGGL(k_mf_z<false>, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd,
                          mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt, mf.ps, mf.pt,
-                         mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
+                         mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status, PFuse{});
       hipLaunchKernelGGL(k_rec_g<kZStored>, grid, dim3(256), 0, s, ra, wt, nbp, ngrp, nsw8, status);
     } else if (mf.ident) {
       if (mf.rec_rg == 8 || mf.rec_rg == 4) {
@@ -1316,8 +1350,8 @@ int mf_energies(mlff_ctx *ctx, const double *alphas, double *E_pairs_host) {
   MLFF_HIP(ctx, hipMalloc(&da, sizeof(double) * ctx->N));
   MLFF_HIP(ctx, hipMemcpyAsync(da, alphas, sizeof(double) * ctx->N, hipMemcpyHostToDevice, s));
   const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
-                     mf.M, mf.n, mf.n_perms, mf.D, da, mf.Zt, (const int *)nullptr);
+  hipLaunchKernelGGL(k_mf_z<false>, dim3(gx, (unsigned)MP), dim3(256), 0, s, mf.Rdd, mf.Pt, mf.ps, mf.pt,
+                     mf.M, mf.n, mf.n_perms, mf.D, da, mf.Zt, (const int *)nullptr, PFuse{});
   if (mf.ni > 0) {
     hipLaunchKernelGGL(k_mf_pair<1>, dim3((unsigned)((MP + kPT - 1) / kPT),
                        (unsigned)((mf.ni + kPT - 1) / kPT), (unsigned)mf.nz), dim3(256), 0, s,
@@ -1357,11 +1391,17 @@ bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double 
   return true;
 }
 
-void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s) {
+void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s,
+                  const PFuse *pf) {
   const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_mf_z, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
-                     mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt, mf.ps, mf.pt,
-                     mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status);
+  const int32_t *Pt = mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt;
+  if (pf != nullptr)
+    hipLaunchKernelGGL(k_mf_z<true>, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
+                       Pt, mf.ps, mf.pt, mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status, *pf);
+  else
+    hipLaunchKernelGGL(k_mf_z<false>, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
+                       Pt, mf.ps, mf.pt, mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status,
+                       PFuse{});
 }
 
 double mf_seconds(const mlff_ctx *ctx) {

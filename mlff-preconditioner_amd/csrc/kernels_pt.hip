@@ -222,64 +222,90 @@ struct PtFin {
   int64_t D, DP, i0, ni, row0, nrows;
   int S, n;
   double sigma, lam;
-  const double *xloc;   // this rank's operand rows (nullptr: no lam term)
+  const double *xloc;   // this rank's operand rows (nullptr: no lam term); p_old when fused
   double *y;
   double *pq_part;      // kVecGrid partials of x . y (nullptr: none)
+  // fused search-direction update (launch_pt_operator's pf): the operand rows are
+  // p = fused_p(xloc, z) with k_mf_z's rho (st->rho_new) and rho1, written back to xloc here
+  // (k_mf_z, the only other reader of p_old, has finished); rho stored in the state
+  const double *z = nullptr;
+  DevState *st = nullptr;
+  long long it = 0;
 };
 
-// a workgroup per block of P = 256 / D points (grid-stride over the blocks): F of the block
-// summed over the chunks by one thread per (point, entry) into LDS, then one thread per row of
-// the block forms J_i^T F_i
-constexpr int kPtFinMaxF = 512;  // LDS doubles of F per block (P D <= 512)
+// a workgroup per training point (grid-stride over the points): F_i = sum of the S chunk
+// partials, the chunks split over Q = 256 / D groups of D threads (each group sums its
+// contiguous run of chunks in chunk order -- batches of 8 predicated loads in flight, the padding
+// adds exact zeros -- and the Q group sums are then added in group order: a fixed order, one
+// dependent load round for S <= 8 Q instead of S / 8); the point's Rdd row is staged in LDS in the
+// same round; then one thread per row forms J_i^T F_i (partners b in increasing order),
+// sigma y + lam x and the x . y partials
+constexpr int kPtFinMaxF = 512;  // LDS doubles of the group partials (Q D <= 256, or D <= 288)
 __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__ status) {
   if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sP[kPtFinMaxF];
   __shared__ double sF[kPtFinMaxF];
+  __shared__ double sR[3 * 288];
   __shared__ double sh[8];
   const int n3 = 3 * a.n;
-  const int64_t P = a.D <= 256 ? 256 / a.D : 1;  // points per block (D <= 288: P >= 1)
-  const int64_t nblk = (a.ni + P - 1) / P;
+  const int D = (int)a.D;
+  const int Q = D <= 256 ? 256 / D : 1;           // chunk groups
   const int64_t zs = a.ni * a.DP;                 // stride between chunks
+  const bool fp = a.z != nullptr, first = a.it <= 1;
+  double beta = 0.0;
+  if (fp) {  // rho as k_mf_z summed it, rho1 as its folded stop test left it: k_update_p's beta
+    const double rho = a.st->rho_new;
+    beta = rho / a.st->rho1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.st->rho = rho;
+  }
   double pq = 0.0;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    const int64_t p0 = blk * P;
-    const int64_t np = (a.ni - p0) < P ? (a.ni - p0) : P;
-    // F: the chunk partials of (point p0 + e / D, entry e % D) in chunk order, 8 in flight
-    for (int64_t e = threadIdx.x; e < np * a.D; e += 256) {
-      const int64_t q = e / a.D, d = e % a.D;
-      const double *src = a.part + (p0 + q) * a.DP + d;
+  for (int64_t il = blockIdx.x; il < a.ni; il += gridDim.x) {
+    const int64_t i = a.i0 + il;
+    const double *src = a.part + il * a.DP;
+    for (int e = threadIdx.x; e < 3 * D; e += 256) sR[e] = a.Rdd[i * a.D * 3 + e];
+    for (int e = threadIdx.x; e < Q * D; e += 256) {  // D > 256: Q = 1, two entries per thread
+      const int g = e / D, d = e % D;
+      const int z0 = (int)(((int64_t)a.S * g) / Q), z1 = (int)(((int64_t)a.S * (g + 1)) / Q);
       double sum = 0.0;
-      int z = 0;
-      for (; z + 7 < a.S; z += 8) {
+      for (int z = z0; z < z1; z += 8) {
         double t[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) t[u] = src[(int64_t)(z + u) * zs];
+        for (int u = 0; u < 8; ++u) t[u] = z + u < z1 ? src[(int64_t)(z + u) * zs + d] : 0.0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) sum += t[u];
       }
-      for (; z < a.S; ++z) sum += src[(int64_t)z * zs];
-      sF[e] = sum;
+      sP[e] = sum;
     }
     __syncthreads();
-    for (int64_t e = threadIdx.x; e < np * n3; e += 256) {
-      const int64_t q = e / n3;
-      const int r = (int)(e % n3);
-      const int64_t i = a.i0 + p0 + q;
+    for (int d = threadIdx.x; d < D; d += 256) {
+      double f = sP[d];
+      for (int g = 1; g < Q; ++g) f += sP[g * D + d];
+      sF[d] = f;
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < n3; r += 256) {
       const int64_t rl = i * n3 + r - a.row0;
       if (rl < 0 || rl >= a.nrows) continue;
-      const double *Ri = a.Rdd + i * a.D * 3;
-      const double *Fq = sF + q * a.D;
       const int at = r / 3, c = r % 3;
+      double xv = 0.0;
+      if (a.xloc != nullptr) {  // requested before the J^T sum
+        xv = a.xloc[rl];
+        if (fp) xv = fused_p(xv, a.z[rl], beta, first);
+      }
       double acc = 0.0;
       for (int b = 0; b < a.n; ++b) {
         if (b == at) continue;
         const int64_t d = pt_pair(at, b);
-        const double rv = Ri[d * 3 + c];
-        acc = fma(at > b ? -rv : rv, Fq[d], acc);
+        const double rv = sR[d * 3 + c];
+        acc = fma(at > b ? -rv : rv, sF[d], acc);
       }
       double yv = a.sigma * acc;
-      if (a.xloc != nullptr) yv = fma(a.lam, a.xloc[rl], yv);
+      if (a.xloc != nullptr) {
+        if (fp) const_cast<double *>(a.xloc)[rl] = xv;
+        yv = fma(a.lam, xv, yv);
+        if (a.pq_part != nullptr) pq = fma(xv, yv, pq);
+      }
       a.y[rl] = yv;
-      if (a.pq_part != nullptr) pq = fma(a.xloc[rl], yv, pq);
     }
     __syncthreads();
   }
@@ -365,11 +391,12 @@ int64_t pt_padded_d(int64_t D) {
 
 void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, int64_t row0,
                         int64_t nrows, const double *x_loc, double *y_loc, const int *status,
-                        double sigma, double lam, double *pq_part, hipStream_t s) {
+                        double sigma, double lam, double *pq_part, hipStream_t s,
+                        const PFuse *pf) {
   const PtVariant *v = pt_variant(mf.D);
   const int64_t MP = mf.M * mf.n_perms;
-  // Zt = (J_j x_j)[P_p] once per application (k_mf_z, kernels_mf.hip)
-  launch_mf_zt(mf, xc, status, s);
+  // Zt = (J_j x_j)[P_p] once per application (k_mf_z, kernels_mf.hip); fused: of p = z + beta x
+  launch_mf_zt(mf, xc, status, s, pf);
   PtArgs a;
   a.Rd = mf.Rd;
   a.Rt = Rt;
@@ -403,9 +430,13 @@ void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, in
   fa.xloc = x_loc;
   fa.y = y_loc;
   fa.pq_part = pq_part;
-  const int64_t P = mf.D <= 256 ? 256 / mf.D : 1;
+  if (pf != nullptr) {  // one rank holding every row (mf_can_fuse_p): x_loc is p_old
+    fa.z = pf->z;
+    fa.st = pf->st;
+    fa.it = pf->it;
+  }
   const unsigned grid = pq_part != nullptr ? (unsigned)kVecGrid
-                                           : (unsigned)std::min<int64_t>((mf.ni + P - 1) / P, 2048);
+                                           : (unsigned)std::min<int64_t>(mf.ni, 2048);
   hipLaunchKernelGGL(k_pt_fin, dim3(std::max(grid, 1u)), dim3(256), 0, s, fa, status);
 }
 

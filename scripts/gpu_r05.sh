@@ -10,6 +10,7 @@
 #   prof      rocprofv3 --kernel-trace --stats of the default bench command
 #   pmc       scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes)
 #   cmd       $CMD (one free-form step, $LIM seconds)
+#   eth583    ethanol N = 15741 bench lines, k = 1264 / 554, refined vs one-step Woodbury panel
 # every GPU step runs under its own timeout; the first failure ends the script
 set -u
 export TMPDIR=/tmp
@@ -34,6 +35,19 @@ for s in ${STEPS:-suite smoke bench}; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o bench --output-format csv -- python3 bench.py ;;
     pmc) step pmc 900 python scripts/pmc_head.py ;;
     cmd) step ${NAME:-cmd} ${LIM:-600} bash -c "$CMD" ;;
+    profnt)  # kernel split of the nanotube (configs[1]) and ethanol N = 15741 iterations
+      step profnt 300 rocprofv3 --kernel-trace --stats -d $O/profnt -o nt --output-format csv -- python3 bench.py --workload nanotube --no-cpu --no-solve --steps 200 --warmup 10
+      step profeth 300 rocprofv3 --kernel-trace --stats -d $O/profeth -o eth --output-format csv -- python3 bench.py --workload ethanol --m 583 --no-cpu --no-solve --steps 200 --warmup 10 ;;
+    ethpt)  # the ethanol published points with the pair-tile operator (fused iteration at one rank)
+      for m in 583 2777 5833; do
+        step ethpt_m$m 300 python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 50 --warmup 5
+      done ;;
+    eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
+             # refined (default) and one-step Woodbury panel
+      for k in 1264 554; do
+        step eth583_k${k} 300 python bench.py --workload ethanol --m 583 --k $k --no-cpu --steps 30 --warmup 3
+        step eth583_k${k}_onestep 300 env MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --k $k --no-cpu --steps 30 --warmup 3
+      done ;;
   esac
 done
 echo "== all steps ok"

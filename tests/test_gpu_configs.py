@@ -237,3 +237,53 @@ def test_config1_full_size_against_oracle_fixture(sg, golden_dir):
     assert_pcg_parity(res.iters, res.trace[1:], -res.x, int(f["iters"]), f["trace"][1:],
                       f["alphas"], band=band)
 
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("k", [1264, 554])
+def test_ethanol_full_size_against_oracle_fixture(sg, golden_dir, k):
+    """Ethanol at the reference's published size (N = 15741, M = 583; BASELINE.md:22) on
+    energy-consistent labels, against the CPU oracle's run of it (tests/golden/
+    make_ethanol_full.py -> ethanol_n15741.npz / _band.json): the pivoted Cholesky on the
+    matrix-free operator to the rule-of-thumb k = 1264 and the published k = 554
+    (incomplete_cholesky.py:24-93, iterative_cholesky.py:152-156), then the PCG to the reference's
+    training tolerance 1e-4 (train.py:309) and to 1e-6 (iterative_solver.py:995-1009).  Pivots
+    identical up to the oracle's first near-tie; each solve held to the band the oracle measured
+    over three operator and two Woodbury-Gram summation orders (tests/parity.py rule)."""
+    import json
+
+    from oracle.sgdml import descriptors
+
+    path = golden_dir / "ethanol_n15741.npz"
+    if not path.exists():
+        pytest.fail("tests/golden/ethanol_n15741.npz missing (make_ethanol_full.py)")
+    f = np.load(path, allow_pickle=False)
+    fx = json.loads((golden_dir / "ethanol_n15741_band.json").read_text())
+    Rd, Rdd = descriptors(f["R"])
+    y = f["y"]
+    n = y.size
+    res = {}
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, np.arange(9)[None, :], SIG)
+        s.set_operator(-1.0, LAM)
+        piv, _ = s.precon_pivchol(k)
+        for tol in (1e-4, 1e-6):
+            if f"k{k}_tol{tol:g}" in fx["bands"]:
+                res[tol] = s.pcg(y, tol=tol, maxiter=12000)
+    ref_piv, gap = f["index_columns"][:k], f["pivot_gap"][:k]
+    diff = np.nonzero(piv[:k] != ref_piv)[0]
+    first_tie = np.nonzero(gap < 1e-12)[0]
+    limit = int(first_tie[0]) if first_tie.size else k
+    print(f"ethanol k={k} pivots: first difference at {diff[0] if diff.size else None}, "
+          f"first oracle near-tie at {limit if first_tie.size else None}")
+    assert diff.size == 0 or diff[0] >= limit, (diff[:5], limit)
+    assert res, "no band recorded for this k"
+    for tol, r in res.items():
+        key = f"k{k}_tol{tol:g}"
+        b = fx["bands"][key]
+        print(f"ethanol k={k} tol={tol:g}: GPU {r.iters} vs oracle {int(f[key + '_iters'])} "
+              f"iterations (band {b['band_iters']}, orders "
+              f"{ {o: v['iters'] for o, v in b['variants'].items()} })")
+        assert r.info == int(f[key + "_info"]) == 0
+        assert_pcg_parity(r.iters, r.trace[1:], -r.x, int(f[key + "_iters"]), f[key + "_trace"][1:],
+                          f[key + "_alphas"], band=b)

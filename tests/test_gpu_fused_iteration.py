@@ -146,3 +146,40 @@ def test_fused_dropin_checkpoints(sg, nanotube, monkeypatch):
             assert s.pcg_result()[0] == j
             np.testing.assert_array_equal(mod["alphas_F"], -s.pcg_x())
             assert mod["solver_resid"] == s.pcg_trace()[j]
+
+
+@pytest.mark.parametrize("perms", ["identity", "group2"])
+@pytest.mark.parametrize("chunk", [0, 7])
+def test_pair_tile_fused_iteration_matches_separate_launches(sg, chunk, perms):
+    """The few-atom iteration (pair-tile operator) with the same folds: k_mf_z
+    forms p = z + beta p_old for the entries it reads and runs the previous iteration's stop test,
+    k_pt_fin writes p (k_update_p's bits), and k_update_xr moves into the next rows apply -- four
+    launches fewer per iteration than the seven-launch form (MLFF_FUSE_P=0), the same iterates,
+    counts and stop decisions (chunk 7: a chunk boundary every seventh iteration).  A
+    two-element permutation group exercises the permuted Zt gathers."""
+    from sgdml_amd import synthetic
+
+    ds = synthetic.ethanol_harmonic(200, seed=4)
+    P = np.arange(9)[None, :] if perms == "identity" else np.array([np.arange(9),
+                                                                     [0, 1, 2, 4, 3, 5, 6, 7, 8]])
+    Rd, Rdd = sg.sgdml_descriptors(ds["R"])
+    y, _ = synthetic.labels(ds["F"])
+    n = y.size
+    out = {}
+    for name, env in FORMS.items():
+        with _env(**env), sg.KernelSolver(n) as s:
+            s.sgdml_operator(Rd, Rdd, P, 10.0)
+            s.set_operator(-1.0, 1e-10)
+            assert s.storage_info()[0] == "matfree" and s.operator_form() == "pt"
+            s.precon_pivchol(800)
+            assert s.precon_apply_traffic()[0] == 1  # rows apply: the x / r fold applies
+            out[name] = s.pcg(y, tol=1e-8, maxiter=3000, chunk=chunk)
+    ref = out["six"]
+    assert ref.info == 0
+    for name in ("four", "five"):
+        r = out[name]
+        assert r.iters == ref.iters and r.info == ref.info, (name, r.iters, ref.iters)
+        t, tr = np.asarray(r.trace), np.asarray(ref.trace)
+        assert t.shape == tr.shape
+        assert np.max(np.abs(t - tr) / np.abs(tr)) <= 1e-12, name
+        assert np.linalg.norm(r.x - ref.x) <= 1e-12 * np.linalg.norm(ref.x), name
