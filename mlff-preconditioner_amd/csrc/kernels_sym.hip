@@ -460,6 +460,14 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
 // into rank blocks of stride `bstride` (= blk + tail: the reduce-scatter operand).
 // PQ: also the partial p.y_g (all rows) + (lam/sigma-free) ||p_loc||^2 partials, one
 // pair per workgroup (fixed order), for k_pq_publish.
+// PQ: the last workgroup to finish (arrival counter ticket[1], reset by it) also does
+// k_pq_publish's work -- the same sums in the same order, so the same share bits -- one launch
+// less per sharded iteration (the publish was a 4.9 us single-workgroup launch at W = 8)
+struct PqPublish {
+  double sigma = 0.0, lam = 0.0;
+  int world = 0;
+};
+
 template <bool PQ>
 __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__ P,
                                                       const double *__restrict__ Pq,
@@ -474,10 +482,11 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
                                                       double *__restrict__ pp_part,
                                                       unsigned long long *__restrict__ ticket,
                                                       const int *__restrict__ status,
-                                                      PGather pg) {
+                                                      PGather pg, PqPublish pub) {
   if (status != nullptr && *status != ST_RUNNING) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   __shared__ double sh[8];
+  __shared__ int s_last;
   double apq = 0.0, app = 0.0;
   // fused p update: rho as k_symv_dyn summed it, p written here (every tile has read p_old)
   double beta = 0.0;
@@ -546,7 +555,35 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
     if (threadIdx.x == 0) {
       pq_part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
       pp_part[blockIdx.x] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      s_last = atomicAdd(ticket + 1, 1ull) == (unsigned long long)(gridDim.x - 1);
     }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // k_pq_publish: s_rank = sigma sum(pq_part) + lam sum(pp_part), into tail slot `rank` of
+    // every rank block of the reduce-scatter operand
+    const int np = (int)gridDim.x;
+    double a = 0.0, b = 0.0;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      a += pq_part[i];
+      b += pp_part[i];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, 64);
+      b += __shfl_down(b, o, 64);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      sh[w] = a;
+      sh[4 + w] = b;
+    }
+    __syncthreads();
+    const double share = pub.sigma * ((sh[0] + sh[1]) + (sh[2] + sh[3])) +
+                         pub.lam * ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+    for (int g = threadIdx.x; g < pub.world; g += 256) yg[(int64_t)g * bstride + blk + rank] = share;
+    if (threadIdx.x == 0) ticket[1] = 0ull;
   }
 }
 
@@ -726,13 +763,24 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (1 << sp.lsub) - 1, (int)sp.nb, rank,
                        sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
-                       sp.ticket, status, PGather{});
+                       sp.ticket, status, PGather{}, PqPublish{});
+    return;
+  }
+  static const bool separate = [] {  // MLFF_PQ_PUBLISH=1: the separate launch (A/B)
+    const char *e = std::getenv("MLFF_PQ_PUBLISH");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  if (!separate) {
+    hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
+                       (1 << sp.lsub) - 1, (int)sp.nb, rank,
+                       sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
+                       sp.ticket, status, pg, PqPublish{sigma, lam, world});
     return;
   }
   hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                      (1 << sp.lsub) - 1, (int)sp.nb, rank,
                      sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
-                     sp.ticket, status, pg);
+                     sp.ticket, status, pg, PqPublish{sigma, lam, 0});
   hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
                      rank, world, blk, sp.ystride, sp.yg, status);
 }
@@ -817,8 +865,9 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
     sp.pq_planes = nq;
     MLFF_HIP(ctx, hipMalloc(&sp.split, (size_t)nb * nb));
     MLFF_HIP(ctx, hipMalloc(&sp.own, sizeof(int) * (size_t)nb * (nb + 1)));
-    MLFF_HIP(ctx, hipMalloc(&sp.ticket, sizeof(unsigned long long)));
-    MLFF_HIP(ctx, hipMemsetAsync(sp.ticket, 0, sizeof(unsigned long long), s));
+    // [k_symv_dyn's work counter, k_sym_reduce_w's arrival counter]
+    MLFF_HIP(ctx, hipMalloc(&sp.ticket, 2 * sizeof(unsigned long long)));
+    MLFF_HIP(ctx, hipMemsetAsync(sp.ticket, 0, 2 * sizeof(unsigned long long), s));
     if (ctx->world > 1) {
       // reduce-scatter operand: rank blocks of blk rows + a tail of p.q shares
       sp.ystride = ctx->blk + round_up(ctx->world, kPad);

@@ -42,6 +42,13 @@ for s in ${STEPS:-suite smoke bench}; do
       for m in 583 2777 5833; do
         step ethpt_m$m 300 python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 50 --warmup 5
       done ;;
+    solo)  # per-rank compute floor of the sharded configs[2] / configs[3] iteration (SOLO transport),
+           # the p.q publish folded (default) vs its separate launch, two interleaved rounds
+      for rep in 1 2; do
+        step solo_w8_r$rep 300 python bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5
+        step solo_w8_pub_r$rep 300 env MLFF_PQ_PUBLISH=1 python bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5
+      done
+      step solo_w8_n131072 300 python bench.py --solo-world 8 --n 131072 --steps 40 --warmup 5 ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do
