@@ -28,6 +28,10 @@ same arrays, so both sides start from identical bits).
    reference's formula without the rounding of its one-step fp64 evaluation (at cond([L; sqrt(lam)
    I]) ~ 6e3 the one-step LAPACK panel is far from the formula's value).  Stored as
    bands[key]["accurate"] (reference order: qr / mf) and the arrays <key>_accurate_*.
+4. --rows (after 1-3): the accurate panels once more with the device's one-pass apply order
+   (groups of ceil(k / 256) rows, group partials added in order: rows_apply) merged into the
+   accurate bands -- at lam = 1e-10 the count of an accurately evaluated preconditioner is set by
+   the apply's rounding (the refined panel: 773 iterations with BLAS's order, 839 with this one).
 
 Writes tests/golden/ethanol_n15741.npz and ethanol_n15741_band.json.  CPU only (~35 min on 7
 processes, one BLAS thread each, after the 5-min pivoted Cholesky; --cache keeps L).
@@ -92,6 +96,27 @@ def accurate_panel(L, lam, kind):
     return scipy.linalg.solve_triangular(C, T1, lower=True)
 
 
+# rows per workgroup of the device's one-pass apply at these ranks (lr_rows_per_wg: ceil(k / 256))
+ROWS_PER_GROUP = {1264: 5, 554: 3}
+
+
+def rows_apply(T, rpw):
+    """z = (r - T^T T r) / lam summed as the device's one-pass rows apply orders it (k_lr_rows /
+    k_lr_fin): t_i row by row, the partial T_g^T t_g of each group of rpw consecutive rows, the
+    group partials added in group order, then lam_inv (r - u) -- another summation order of the
+    same formula."""
+    k = T.shape[0]
+    groups = [np.ascontiguousarray(T[a:min(a + rpw, k)]) for a in range(0, k, rpw)]
+    lam_inv = 1.0 / LAM
+
+    def f(r):
+        u = np.zeros_like(r)
+        for g in groups:
+            u = u + g.T @ (g @ r)
+        return lam_inv * (r - u)
+    return f
+
+
 def _solve(job):
     """One CG solve: (k, operator order, panel order, tol) -> trace, x, info, iters."""
     import threadpoolctl
@@ -107,12 +132,17 @@ def _solve(job):
             T = accurate_panel(Lk, LAM, po)
         else:
             T = woodbury_gram_order(Lk, LAM, po)
-        panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}[order]
         mvK = kop_variant(Rd, Rdd, perms, SIG, order)
-        mvT = make_gemv(T, panel_order)
-        mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order)
+        if order == "mf_rows":  # the device's one-pass apply order (rows_apply)
+            mvK = kop_variant(Rd, Rdd, perms, SIG, "mf")
+            psolve = rows_apply(T, ROWS_PER_GROUP[k])
+        else:
+            panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}[order]
+            mvT = make_gemv(T, panel_order)
+            mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order)
+            psolve = lambda r: (r - mvTt(mvT(r))) / LAM  # noqa: E731
         x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=tol, maxiter=MAXITER,
-                                    psolve=lambda r: (r - mvTt(mvT(r))) / LAM)
+                                    psolve=psolve)
     name = order if not po else f"panel_{po}" if po not in ("qr", "refined") else f"{po}_{order}"
     print(f"k={k} tol={tol:g} {name:10s} iters {it} info {info} ({time.time() - t0:.0f} s)",
           flush=True)
@@ -135,6 +165,42 @@ def band_of(runs, ref_name, tol):
             "band_iters": int(max(abs(e["d_iters"]) for e in v)),
             "band_crossing": int(max(e["max_d_crossing"] for e in v)),
             "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v))}
+
+
+def merge_rows(cache, procs):
+    """--rows: the accurate panels with the device's apply order ('refined_mf_rows', 'qr_mf_rows'),
+    merged into the committed fixture's accurate bands (the reference solve of each band, qr / mf,
+    is stored, so d_iters, crossings and d_alpha are measured against it as for the others)."""
+    R, Rd, Rdd, perms, y = problem()
+    c = np.load(cache, allow_pickle=False)
+    _G.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, L=c["L"])
+    out = json.loads((GOLDEN / "ethanol_n15741_band.json").read_text())
+    with np.load(GOLDEN / "ethanol_n15741.npz", allow_pickle=False) as f:
+        arrays = {name: f[name] for name in f.files}
+    jobs = [(k, "mf_rows", po, tol) for k in K_RANKS for tol in TOLS for po in ("refined", "qr")]
+    jobs.sort(key=lambda j: (j[3] > 1e-5, -j[0]))
+    with mp.get_context("fork").Pool(procs) as pool:
+        results = pool.map(_solve, jobs, chunksize=1)
+    for (k, order, po, tol), x, info, tr, it in results:
+        key = f"k{k}_tol{tol:g}"
+        b = out["bands"][key]["accurate"]
+        x0 = -arrays[f"{key}_accurate_alphas"]
+        tr0, it0 = arrays[f"{key}_accurate_trace"], int(arrays[f"{key}_accurate_iters"])
+        top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+        cr0, cr = half_decade_crossings(tr0[1:], top), half_decade_crossings(tr[1:], top)
+        dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+        b["variants"][f"{po}_{order}"] = {
+            "iters": int(it), "info": int(info), "d_iters": int(it - it0),
+            "max_d_crossing": int(max(dc) if dc else 0),
+            "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+        v = b["variants"].values()
+        b["band_iters"] = int(max(abs(e["d_iters"]) for e in v))
+        b["band_crossing"] = int(max(e["max_d_crossing"] for e in v))
+        b["band_rel_dalpha"] = float(max(e["rel_dalpha"] for e in v))
+        print(key, "accurate", json.dumps({q: b[q] for q in ("ref_iters", "band_iters",
+                                                            "band_crossing", "band_rel_dalpha")}),
+              flush=True)
+    (GOLDEN / "ethanol_n15741_band.json").write_text(json.dumps(out, indent=1, sort_keys=True))
 
 
 def main(cache=None, procs=8):
@@ -218,5 +284,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--cache", default=None, help=".npz outside the repository for L (160 MB)")
     ap.add_argument("--procs", type=int, default=int(os.environ.get("PROCS", "8")))
+    ap.add_argument("--rows", action="store_true",
+                    help="merge the device-apply-order accurate solves into the committed fixture")
     a = ap.parse_args()
-    main(a.cache, a.procs)
+    if a.rows:
+        merge_rows(a.cache, a.procs)
+    else:
+        main(a.cache, a.procs)
