@@ -509,7 +509,11 @@ int cho_factor_stable(mlff_ctx *ctx, double *A, int64_t k, double *lo_eig_out,
 // from L2 L2^T = X^T X + mu I: W is the top block of Q1 = [X; sqrt(mu) I] L2^-T, so
 // G2 = Q1^T Q1 = W W^T + mu L2^-1 L2^-T (= I in exact arithmetic), C C^T = G2, W <- C^-1 W.
 // L2: the lower factor (k x k, the same on every rank).
-int reorthogonalise_panel(mlff_ctx *ctx, double *W, const double *L2, int64_t k, double mu) {
+// steps > 1 (MLFF_WB_REFINE=<steps>): CholeskyQR3 and beyond -- step s uses the accumulated
+// factor (L2 C_1 ... C_{s-1}), whose inverse is C_{s-1}^-1 ... C_1^-1 L2^-1 (Li updated by one
+// k x k triangular solve per step)
+int reorthogonalise_panel(mlff_ctx *ctx, double *W, const double *L2, int64_t k, double mu,
+                          int steps = 1) {
   ScratchScope scope(ctx);
   hipStream_t s = ctx->stream;
   double *Li = nullptr, *G2 = nullptr;
@@ -518,11 +522,14 @@ int reorthogonalise_panel(mlff_ctx *ctx, double *W, const double *L2, int64_t k,
   MLFF_HIP(ctx, hipMemsetAsync(Li, 0, sizeof(double) * k * k, s));
   launch_add_diag(Li, k, 1.0, s);
   MLFF_TRY(trsm_lower_wide(ctx, L2, k, Li, k, k));  // Li = L2^-1
-  MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G2));
-  MLFF_TRY(allreduce(ctx, G2, (size_t)(k * k)));
-  launch_gemm(false, true, k, k, k, mu, Li, k, Li, k, 1.0, G2, k, s);  // + mu Li Li^T
-  MLFF_TRY(potrf_lower(ctx, G2, k));
-  MLFF_TRY(trsm_lower_wide(ctx, G2, k, W, ctx->blk, ctx->blk));
+  for (int st = 0; st < steps; ++st) {
+    MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G2));
+    MLFF_TRY(allreduce(ctx, G2, (size_t)(k * k)));
+    launch_gemm(false, true, k, k, k, mu, Li, k, Li, k, 1.0, G2, k, s);  // + mu Li Li^T
+    MLFF_TRY(potrf_lower(ctx, G2, k));
+    MLFF_TRY(trsm_lower_wide(ctx, G2, k, W, ctx->blk, ctx->blk));
+    if (st + 1 < steps) MLFF_TRY(trsm_lower_wide(ctx, G2, k, Li, k, k));  // Li <- C^-1 Li
+  }
   return MLFF_OK;
 }
 
@@ -536,7 +543,7 @@ int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
   launch_add_diag(G, k, ctx->lam, s);
   MLFF_TRY(potrf_lower(ctx, G, k));
   MLFF_TRY(trsm_lower_wide(ctx, G, k, W, ctx->blk, ctx->blk));
-  if (ctx->wb_refine) MLFF_TRY(reorthogonalise_panel(ctx, W, G, k, ctx->lam));
+  if (ctx->wb_refine > 0) MLFF_TRY(reorthogonalise_panel(ctx, W, G, k, ctx->lam, ctx->wb_refine));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   return MLFF_OK;
 }
@@ -1196,7 +1203,7 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
     *flag = e == nullptr || std::atoi(e) != 0;
   }
   if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
-  if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("MLFF_NYS_REFINE")) ctx->nys_refine = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_EXACT_SUMS")) ctx->exact_sums = std::atoi(e) != 0;
   ctx->rank = rank;

@@ -352,7 +352,7 @@ struct mlff_ctx {
   // Woodbury panel re-orthogonalised by a second CholeskyQR step (MLFF_WB_REFINE, woodbury_inplace;
   // configs[1] at full size: 571 -> 366 iterations, the oracle's 367) and the same for the
   // Nystrom panel (MLFF_NYS_REFINE)
-  bool wb_refine = true;
+  int wb_refine = 1;  // re-orthogonalisation steps (MLFF_WB_REFINE=0 / 1 / 2 ...)
   bool nys_refine = false;
   // exact-sum anchor (MLFF_EXACT_SUMS=1, kernels_dd.hip): dense-row operator and two-pass low-rank
   // apply with double-double dot products rounded once per entry; one rank; measurement only

@@ -63,7 +63,7 @@ def gemm_bias():
     return res
 
 
-def main(M=583, k=1264):
+def main(M=583, k=int(os.environ.get("DIAG_K", "1264"))):
     ds = synthetic.ethanol_harmonic(M, seed=0)
     y, _ = synthetic.labels(ds["F"])
     n = y.size
@@ -77,13 +77,13 @@ def main(M=583, k=1264):
     panels = {}
     rng = np.random.default_rng(3)
     rtest = rng.standard_normal(n)
-    for refine in ("0", "1"):
+    for refine in ("0", "1", "2"):
         os.environ["MLFF_WB_REFINE"] = refine
         with sgdml_amd.KernelSolver(n) as s:
             s.sgdml_operator(Rd, Rdd, np.arange(9)[None, :], 10.0)
             s.set_operator(-1.0, LAM)
             s.precon_pivchol(k)
-            name = "device_" + ("refined" if refine == "1" else "onestep")
+            name = "device_" + {"0": "onestep", "1": "refined", "2": "refined2"}[refine]
             T = s.precon_panel()
             panels[name] = T
             zd = s.precon_apply(rtest)
