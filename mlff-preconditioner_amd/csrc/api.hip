@@ -523,7 +523,10 @@ int reorthogonalise_panel(mlff_ctx *ctx, double *W, const double *L2, int64_t k,
   launch_add_diag(Li, k, 1.0, s);
   MLFF_TRY(trsm_lower_wide(ctx, L2, k, Li, k, k));  // Li = L2^-1
   for (int st = 0; st < steps; ++st) {
-    MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G2));
+    if (ctx->wb_gram_dd)
+      MLFF_TRY(gram_wide_dd(ctx, W, k, ctx->blk, ctx->blk, G2, ctx->wb_gram_dd == 2));
+    else
+      MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G2));
     MLFF_TRY(allreduce(ctx, G2, (size_t)(k * k)));
     launch_gemm(false, true, k, k, k, mu, Li, k, Li, k, 1.0, G2, k, s);  // + mu Li Li^T
     MLFF_TRY(potrf_lower(ctx, G2, k));
@@ -538,7 +541,10 @@ int woodbury_inplace(mlff_ctx *ctx, double *W, int64_t k) {
   hipStream_t s = ctx->stream;
   double *G = nullptr;
   MLFF_TRY(scratch_alloc(ctx, &G, k * k));
-  MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
+  if (ctx->wb_gram_dd)  // L^T L rounded once per entry (DESIGN.md 2, configs[1])
+    MLFF_TRY(gram_wide_dd(ctx, W, k, ctx->blk, ctx->blk, G, ctx->wb_gram_dd == 2));
+  else
+    MLFF_TRY(syrk_wide(ctx, W, k, ctx->blk, ctx->blk, G));
   MLFF_TRY(allreduce(ctx, G, (size_t)(k * k)));
   launch_add_diag(G, k, ctx->lam, s);
   MLFF_TRY(potrf_lower(ctx, G, k));
@@ -1205,6 +1211,7 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
   if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("MLFF_NYS_REFINE")) ctx->nys_refine = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_WB_GRAM")) ctx->wb_gram_dd = std::max(0, std::min(2, std::atoi(e)));
   if (const char *e = std::getenv("MLFF_EXACT_SUMS")) ctx->exact_sums = std::atoi(e) != 0;
   ctx->rank = rank;
   ctx->world = world;

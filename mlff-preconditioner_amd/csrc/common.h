@@ -353,6 +353,10 @@ struct mlff_ctx {
   // configs[1] at full size: 571 -> 366 iterations, the oracle's 367) and the same for the
   // Nystrom panel (MLFF_NYS_REFINE)
   int wb_refine = 1;  // re-orthogonalisation steps (MLFF_WB_REFINE=0 / 1 / 2 ...)
+  // the Woodbury Gram matrices L^T L (and the refinement's T T^T): 0 the fp64 matrix-core GEMM,
+  // 1 chunked double-double on the matrix cores, 2 exact products in double-double
+  // (MLFF_WB_GRAM; kernels_dd.hip gram_wide_dd)
+  int wb_gram_dd = 1;
   bool nys_refine = false;
   // exact-sum anchor (MLFF_EXACT_SUMS=1, kernels_dd.hip): dense-row operator and two-pass low-rank
   // apply with double-double dot products rounded once per entry; one rank; measurement only
@@ -550,6 +554,12 @@ void launch_dd_gemv_rows(const double *M, int64_t ld, int64_t rows, int64_t ncol
                          hipStream_t s);
 void launch_dd_lowrank(const double *T, int64_t ldt, int64_t k, const double *r, double *z, int64_t n,
                        double sigma_p, double lam_inv, double *t, const int *status, hipStream_t s);
+// G = W W^T (k x k, symmetric) of a wide k x ncols panel, each entry rounded once from a
+// double-double sum: exact_products -- every product exact (correctly rounded but for ties);
+// else 64-column chunks summed in fp64 on the matrix cores and the chunk partials added in
+// double-double.  The Woodbury panel's Gram matrices (MLFF_WB_GRAM)
+int gram_wide_dd(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int64_t ldw, double *G,
+                 bool exact_products);
 void launch_gemv_xr(const double *T, int64_t ldt, int64_t k, int64_t ncols, int splits,
                     const double *r, double *r_out, double *x, const double *p, const double *y,
                     const double *shares, int world, int64_t n, double sigma, double lam,

@@ -49,6 +49,29 @@ for s in ${STEPS:-suite smoke bench}; do
         step solo_w8_pub_r$rep 300 env MLFF_PQ_PUBLISH=1 python bench.py --solo-world 8 --n 65536 --steps 40 --warmup 5
       done
       step solo_w8_n131072 300 python bench.py --solo-world 8 --n 131072 --steps 40 --warmup 5 ;;
+    ptchunks)  # ethanol M = 583: pair-tile chunk count (37 = default: 185 workgroups on 256 CUs)
+      for rep in 1 2; do
+        for S in 37 52 74; do
+          step ptS${S}_r$rep 300 env MLFF_PT_CHUNKS=$S python bench.py --workload ethanol --m 583 --no-cpu --no-solve --steps 200 --warmup 10
+        done
+      done ;;
+    gramab)  # the one-step Woodbury panel with its Gram / POTRF / TRSM GEMMs on the VALU instead
+             # of the matrix cores (MLFF_GEMM_VALU=1): nanotube configs[1] and ethanol N = 15741
+      step gram_nt_mfma 300 env MLFF_WB_REFINE=0 python bench.py --workload nanotube --no-cpu --steps 20 --warmup 3
+      step gram_nt_valu 300 env MLFF_WB_REFINE=0 MLFF_GEMM_VALU=1 python bench.py --workload nanotube --no-cpu --steps 20 --warmup 3
+      step gram_nt_valu_ref 300 env MLFF_GEMM_VALU=1 python bench.py --workload nanotube --no-cpu --steps 20 --warmup 3
+      step gram_eth_valu 300 env MLFF_WB_REFINE=0 MLFF_GEMM_VALU=1 python bench.py --workload ethanol --m 583 --no-cpu --steps 20 --warmup 3
+      step gram_eth_valu_ref 300 env MLFF_GEMM_VALU=1 python bench.py --workload ethanol --m 583 --no-cpu --steps 20 --warmup 3
+      step gram_diag_valu 600 env MLFF_GEMM_VALU=1 python -u scripts/dev/diag_config1_gram.py ;;
+    gramdd)  # the Woodbury Gram in double-double (MLFF_WB_GRAM=1), one-step and refined panels
+      for g in ${GRAMS:-1 0}; do
+        step gdd${g}_nt_onestep 300 env MLFF_WB_GRAM=$g MLFF_WB_REFINE=0 python bench.py --workload nanotube --no-cpu --steps 20 --warmup 3
+        step gdd${g}_nt_refined 300 env MLFF_WB_GRAM=$g python bench.py --workload nanotube --no-cpu --steps 20 --warmup 3
+        step gdd${g}_eth_onestep 300 env MLFF_WB_GRAM=$g MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --no-cpu --steps 20 --warmup 3
+        step gdd${g}_eth_refined 300 env MLFF_WB_GRAM=$g python bench.py --workload ethanol --m 583 --no-cpu --steps 20 --warmup 3
+        step gdd${g}_eth554_refined 300 env MLFF_WB_GRAM=$g python bench.py --workload ethanol --m 583 --k 554 --no-cpu --steps 20 --warmup 3
+        step gdd${g}_eth554_onestep 300 env MLFF_WB_GRAM=$g MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --k 554 --no-cpu --steps 20 --warmup 3
+      done ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do
