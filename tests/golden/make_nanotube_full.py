@@ -18,6 +18,9 @@ both sides start from identical bits).
    and the panel apply (make_noise_band.kop_variant: mf, mf_rev, mf_split): the 'mf' solve is the
    reference trajectory (trace, alpha = -x), the spread of the others its noise band.
 
+4. --compute-cache then --accurate (round 5): the accurate-panel band (QR / two-step panels in
+   several summation orders) merged into the committed fixture as band["accurate"].
+
 3. --panel-orders: more solves of the 'mf' operator with the Woodbury panel rounded another way
    (woodbury_gram_order): 'rev' / 'blk8' (Gram matrix in other orders) join the band; 'inverse',
    'noise', 'rownoise' (explicit triangular inverse; 2e-15 perturbations) are recorded beside it
@@ -147,6 +150,78 @@ def band_json(n, it0, variants, gap):
     return band
 
 
+_A = {}  # shared with the forked accurate-panel workers
+
+
+def _accurate_solve(job):
+    """(panel kind, operator order) -> the solve of an accurately evaluated Woodbury panel
+    (make_ethanol_full.accurate_panel: Householder QR or two CholeskyQR steps), with the
+    operator order's apply order or the device's rows apply order ('mf_rows')."""
+    import threadpoolctl
+
+    from make_ethanol_full import accurate_panel, rows_apply
+
+    kind, order = job
+    Rd, Rdd, perms, y, L = _A["Rd"], _A["Rdd"], _A["perms"], _A["y"], _A["L"]
+    t0 = time.time()
+    with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+        T = accurate_panel(L, LAM, kind)
+        if order == "mf_rows":
+            mvK = kop_variant(Rd, Rdd, perms, SIG, "mf")
+            psolve = rows_apply(T, (K_RANK + 255) // 256)
+        else:
+            mvK = kop_variant(Rd, Rdd, perms, SIG, order)
+            po = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}[order]
+            mvT, mvTt = make_gemv(T, po), make_gemv(np.ascontiguousarray(T.T), po)
+            psolve = lambda r: (r - mvTt(mvT(r))) / LAM  # noqa: E731
+        x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, _A["y"], tol=TOL,
+                                    maxiter=5 * y.size, psolve=psolve)
+    print(f"accurate {kind}_{order}: iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
+    return job, x, info, tr, it
+
+
+def accurate(cache, procs=5):
+    """--accurate (needs --cache of a full run): the configs[1] solve with the Woodbury panel
+    evaluated accurately (QR in three orders, the two-step panel with BLAS's and the device's
+    apply order), recorded as band["accurate"] and the arrays accurate_* -- the band the device's
+    default panel (two CholeskyQR steps on a double-double Gram) is held to beside
+    the one-step LAPACK band."""
+    import multiprocessing as mp
+
+    _, Rd, Rdd, perms, y = problem()
+    c = np.load(cache, allow_pickle=False)
+    _A.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, L=np.ascontiguousarray(c["L"][:, :K_RANK]))
+    jobs = [("qr", "mf"), ("qr", "mf_rev"), ("qr", "mf_split"), ("qr", "mf_rows"),
+            ("refined", "mf"), ("refined", "mf_rows")]
+    with mp.get_context("fork").Pool(procs) as pool:
+        results = pool.map(_accurate_solve, jobs, chunksize=1)
+    runs = {f"{kind}_{order}": (x, info, tr, it) for (kind, order), x, info, tr, it in results}
+    x0, info0, tr0, it0 = runs["qr_mf"]
+    top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+    cr0 = half_decade_crossings(tr0[1:], top)
+    variants = {}
+    for name, (x, info, tr, it) in runs.items():
+        cr = half_decade_crossings(tr[1:], top)
+        dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+        variants[name] = {"iters": int(it), "info": int(info), "d_iters": int(it - it0),
+                          "max_d_crossing": int(max(dc) if dc else 0),
+                          "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+    v = variants.values()
+    band = json.loads((GOLDEN / "nanotube_n15540_band.json").read_text())
+    band["accurate"] = {"ref_order": "qr_mf", "ref_iters": int(it0), "variants": variants,
+                        "band_iters": int(max(abs(e["d_iters"]) for e in v)),
+                        "band_crossing": int(max(e["max_d_crossing"] for e in v)),
+                        "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v))}
+    with np.load(GOLDEN / "nanotube_n15540.npz", allow_pickle=False) as f:
+        arrays = {name: f[name] for name in f.files}
+    arrays.update(accurate_trace=tr0, accurate_alphas=-x0, accurate_iters=np.int64(it0),
+                  accurate_info=np.int64(info0))
+    np.savez_compressed(GOLDEN / "nanotube_n15540.npz", **arrays)
+    (GOLDEN / "nanotube_n15540_band.json").write_text(json.dumps(band, indent=1, sort_keys=True))
+    print(json.dumps({q: band["accurate"][q] for q in ("ref_iters", "band_iters", "band_crossing",
+                                                      "band_rel_dalpha")}), flush=True)
+
+
 def main(cache=None, panel_orders=()):
     """cache: .npz path (outside the repository: 336 MB) holding L and the pivot log, written
     on the first run and read by later ones; panel_orders: Gram-matrix orders of the Woodbury
@@ -218,5 +293,24 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--cache", default=None)
     ap.add_argument("--panel-orders", nargs="*", default=[], choices=PANEL_ORDERS)
+    ap.add_argument("--accurate", action="store_true",
+                    help="the accurate-panel band only (needs --cache from a full run)")
+    ap.add_argument("--compute-cache", action="store_true",
+                    help="compute the factor into --cache (no solves)")
     a = ap.parse_args()
-    main(a.cache, a.panel_orders)
+    if a.compute_cache:
+        _, Rd, Rdd, perms, y = problem()
+        mv0 = kop_variant(Rd, Rdd, perms, SIG, "mf")
+
+        def get_col(i):
+            e = np.zeros(y.size)
+            e[i] = 1.0
+            return -mv0(e) + LAM * e
+
+        L, piv, piv_val, gap = pivoted_cholesky_logged(get_col, -kernel_diag(Rd, Rdd, perms, SIG),
+                                                       K_RANK)
+        np.savez(a.cache, L=L, piv=piv, piv_val=piv_val, gap=gap)
+    elif a.accurate:
+        accurate(a.cache)
+    else:
+        main(a.cache, a.panel_orders)
