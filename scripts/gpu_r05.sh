@@ -72,6 +72,13 @@ for s in ${STEPS:-suite smoke bench}; do
         step gdd${g}_eth554_refined 300 env MLFF_WB_GRAM=$g python bench.py --workload ethanol --m 583 --k 554 --no-cpu --steps 20 --warmup 3
         step gdd${g}_eth554_onestep 300 env MLFF_WB_GRAM=$g MLFF_WB_REFINE=0 python bench.py --workload ethanol --m 583 --k 554 --no-cpu --steps 20 --warmup 3
       done ;;
+    headlines)  # every bench line at HEAD: nanotube configs[1] and N = 156510, ethanol at the
+                # reference's published sizes
+      step head_nt 300 python bench.py --workload nanotube
+      step head_nt141 600 python bench.py --workload nanotube --m 141 --no-cpu --steps 20 --warmup 3
+      for m in 583 2777 5833; do
+        step head_eth_m$m 600 python bench.py --workload ethanol --m $m --no-cpu --steps 30 --warmup 3
+      done ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do
