@@ -190,6 +190,12 @@ int mlff_spectrum(mlff_ctx *ctx, int preconditioned, double *eig_out);
 int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha,
                    const double *A, int64_t lda, const double *B, int64_t ldb, double beta,
                    double *C, int64_t ldc, int splits);
+/* Gram matrix G = W W^T (k x k, row-major) of a host k x ncols panel W (row-major) as the
+ * Woodbury build forms L^T L (iterative_cholesky.py:141-142, `kernel = lam I + L^T L`):
+ * mode 0 the fp64 matrix-core SYRK, 1 fp64 64-column chunks summed in double-double (the
+ * default, MLFF_WB_GRAM=1), 2 every product exact and summed in double-double.  Test hook. */
+int mlff_test_gram(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int mode,
+                   double *G_out);
 /* Iterative._cho_factor_stable (src/sGDML/sgdml/solvers/iterative_solver.py:555-583): the
  * smallest eigenvalue of the lower triangle of the host m x m matrix M (row-major) --
  * eigh(M, eigvals_only=True, eigvals=(0, 0)) at :577, computed on the device by Householder

@@ -1481,6 +1481,27 @@ int mlff_test_gemm(mlff_ctx *ctx, int ta, int tb, int64_t M, int64_t N, int64_t 
   MLFF_API_END(ctx)
 }
 
+int mlff_test_gram(mlff_ctx *ctx, const double *W, int64_t k, int64_t ncols, int mode,
+                   double *G_out) {
+  MLFF_API_BEGIN
+  MLFF_ENTER(ctx);
+  if (W == nullptr || G_out == nullptr || k < 1 || ncols < 1 || mode < 0 || mode > 2)
+    return set_error(ctx, MLFF_ERR_ARG, "test_gram: bad arguments");
+  ScratchScope scope(ctx);
+  double *dW = nullptr, *dG = nullptr;
+  MLFF_TRY(scratch_alloc(ctx, &dW, (size_t)(k * ncols)));
+  MLFF_TRY(scratch_alloc(ctx, &dG, (size_t)(k * k)));
+  MLFF_HIP(ctx, hipMemcpyAsync(dW, W, sizeof(double) * k * ncols, hipMemcpyHostToDevice, ctx->stream));
+  if (mode == 0)
+    MLFF_TRY(syrk_wide(ctx, dW, k, ncols, ncols, dG));
+  else
+    MLFF_TRY(gram_wide_dd(ctx, dW, k, ncols, ncols, dG, mode == 2));
+  MLFF_HIP(ctx, hipMemcpyAsync(G_out, dG, sizeof(double) * k * k, hipMemcpyDeviceToHost, ctx->stream));
+  MLFF_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MLFF_OK;
+  MLFF_API_END(ctx)
+}
+
 int mlff_sym_min_eig(mlff_ctx *ctx, const double *M, int64_t m, double *lo_eig_out,
                      double *d_out, double *e_out) {
   MLFF_API_BEGIN

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mlff_spectrum": (_int, [_c_ctx, _int, _p_dbl]),
     "mlff_test_gemm": (_int, [_c_ctx, _int, _int, _i64, _i64, _i64, _dbl, _p_dbl, _i64, _p_dbl,
                               _i64, _dbl, _p_dbl, _i64, _int]),
+    "mlff_test_gram": (_int, [_c_ctx, _p_dbl, _i64, _i64, _int, _p_dbl]),
     "mlff_sgdml_energies": (_int, [_c_ctx, _p_dbl, _p_dbl, _p_i64, _p_i64]),
     "mlff_sgdml_descriptors": (_int, [_p_dbl, _i64, _int, _p_dbl, _p_dbl]),
     "mlff_set_operator": (_int, [_c_ctx, _dbl, _dbl]),

@@ -52,3 +52,60 @@ def test_gemm_layouts(solver, ta, tb, shape):
 def test_gemm_split_k_slabs(solver, ta, tb):
     run(solver, ta, tb, 64, 1000, 700, 1.0, 1.0, splits=4)
     run(solver, ta, tb, 150, 260, 100, 0.5, 1.0, splits=3)
+
+
+def _two_prod(a, b):
+    """Exact a * b = p + e (Dekker / Veltkamp, no fma needed), elementwise."""
+    p = a * b
+    c = 134217729.0  # 2^27 + 1
+    def split(x):
+        t = c * x
+        hi = t - (t - x)
+        return hi, x - hi
+    ah, al = split(a)
+    bh, bl = split(b)
+    e = ((ah * bh - p) + ah * bl + al * bh) + al * bl
+    return p, e
+
+
+@pytest.mark.parametrize("k, ncols", [(70, 3001), (130, 1000), (9, 200)])
+def test_woodbury_gram_modes(solver, k, ncols):
+    """The Woodbury Gram matrix L^T L (mlff_test_gram): mode 2 (exact products,
+    double-double sums) is the correctly rounded exact sum on every entry (within one ulp, exact
+    on nearly all); mode 1 (the default: fp64 64-column chunks on the matrix cores, chunk sums in
+    double-double) errs by at most a few ulps of its chunks' partial sums -- not of the full-length
+    fp64 running sum, which is what the plain fp64 SYRK (mode 0) pays on the small entries; every
+    mode is exactly symmetric.  Data with cancellation (mixed signs, a common offset)."""
+    import math
+
+    from sgdml_amd import _native as nat
+
+    rng = np.random.default_rng(k)
+    W = rng.standard_normal((k, ncols)) * np.exp(rng.uniform(-3, 3, (k, 1))) + 0.3
+    W = np.ascontiguousarray(W)
+    G = {}
+    for mode in (0, 1, 2):
+        out = np.zeros((k, k))
+        solver._call("mlff_test_gram", nat.dptr(W), k, ncols, mode, nat.dptr(out))
+        np.testing.assert_array_equal(out, out.T)
+        G[mode] = out
+    exact = np.empty((k, k))
+    chunk_abs = np.empty((k, k))
+    for i in range(k):
+        for j in range(i + 1):
+            p, e = _two_prod(W[i], W[j])
+            exact[i, j] = exact[j, i] = math.fsum(np.concatenate([p, e]))
+            cs = [abs(math.fsum(np.concatenate([p[c:c + 64], e[c:c + 64]])))
+                  for c in range(0, ncols, 64)]
+            chunk_abs[i, j] = chunk_abs[j, i] = sum(cs)
+    ulp = np.spacing(np.abs(exact))
+    err2 = np.abs(G[2] - exact)
+    assert np.all(err2 <= ulp), (err2 / ulp).max()
+    assert np.count_nonzero(err2) <= max(2, k * k // 200)
+    err1 = np.abs(G[1] - exact)
+    # a chunk boundary may sit anywhere inside a split-K slab: allow two chunks' worth per chunk
+    assert np.all(err1 <= 8 * np.finfo(float).eps * chunk_abs + ulp), \
+        (err1 / (np.finfo(float).eps * chunk_abs + ulp)).max()
+    err0 = np.abs(G[0] - exact)
+    print(f"k={k} n={ncols}: max error / ulp of the entry: fp64 {np.max(err0 / ulp):.1f}, "
+          f"chunked double-double {np.max(err1 / ulp):.1f}, exact products {np.max(err2 / ulp):.1f}")
