@@ -236,6 +236,12 @@ def test_config1_full_size_against_oracle_fixture(sg, golden_dir):
           f"{ {o: v['iters'] for o, v in band['variants'].items()} })")
     assert_pcg_parity(res.iters, res.trace[1:], -res.x, int(f["iters"]), f["trace"][1:],
                       f["alphas"], band=band)
+    if "accurate" in band:  # and the oracle's accurately evaluated panels (round 5: 363-366)
+        acc = band["accurate"]
+        print(f"configs[1] solve: GPU {res.iters} vs oracle accurate {acc['ref_iters']} "
+              f"(band {acc['band_iters']}, {({o: v['iters'] for o, v in acc['variants'].items()})})")
+        assert_pcg_parity(res.iters, res.trace[1:], -res.x, int(f["accurate_iters"]),
+                          f["accurate_trace"][1:], f["accurate_alphas"], band=acc)
 
 
 
