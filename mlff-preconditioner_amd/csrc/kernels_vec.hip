@@ -388,7 +388,18 @@ constexpr int kLrThreads = 512;
 constexpr int64_t kLrMaxCols = 16 * 2 * kLrThreads;  // M <= 16 double2 per thread
 
 bool lr_rows_fits(int64_t ldt) { return ldt > 0 && ldt % 2 == 0 && ldt <= kLrMaxCols; }
-int lr_rows_per_wg(int64_t k) { return (int)((k + 255) / 256); }
+// at least 7 rows per workgroup: fewer partial z vectors (16 N bytes each) for small k
+// (ethanol N = 15741, k = 1264: 5 -> 7 rows, 253 -> 181 workgroups, apply 39.3 -> 38.1 us; 10 rows:
+// 39.0 us; nanotube k = 2701 keeps its 11 (14: 69.3-70.5 vs 68.4-69.0 us), profiles/r04/rpw_ab/;
+// round 4 kept 5 only because the golden nanotube drop-in moved 322 -> 321, which the
+// double-double Woodbury Gram of round 5 gives either way).  MLFF_LR_MIN_RPW overrides (A/B)
+int lr_rows_per_wg(int64_t k) {
+  static const int min_rpw = [] {
+    const char *e = std::getenv("MLFF_LR_MIN_RPW");
+    return e != nullptr ? std::max(1, std::atoi(e)) : 7;
+  }();
+  return std::max((int)((k + 255) / 256), min_rpw);
+}
 int lr_rows_groups(int64_t k) {
   const int rpw = lr_rows_per_wg(k);
   return (int)((k + rpw - 1) / rpw);

@@ -79,6 +79,13 @@ for s in ${STEPS:-suite smoke bench}; do
       for m in 583 2777 5833; do
         step head_eth_m$m 600 python bench.py --workload ethanol --m $m --no-cpu --steps 30 --warmup 3
       done ;;
+    rpwab)  # rows apply: at least 7 rows per workgroup (default) vs ceil(k / 256) (MLFF_LR_MIN_RPW=1)
+      for rep in 1 2; do
+        for r in 7 1; do
+          step rpw${r}_eth_r$rep 300 env MLFF_LR_MIN_RPW=$r python bench.py --workload ethanol --m 583 --no-cpu --no-solve --steps 200 --warmup 10
+          step rpw${r}_nt_r$rep 300 env MLFF_LR_MIN_RPW=$r python bench.py --workload nanotube --no-cpu --no-solve --steps 200 --warmup 10
+        done
+      done ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do

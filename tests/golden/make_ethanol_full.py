@@ -96,7 +96,9 @@ def accurate_panel(L, lam, kind):
     return scipy.linalg.solve_triangular(C, T1, lower=True)
 
 
-# rows per workgroup of the device's one-pass apply at these ranks (lr_rows_per_wg: ceil(k / 256))
+# rows per workgroup of the device's one-pass apply at these ranks when the fixture was made
+# (lr_rows_per_wg was ceil(k / 256); round 5 later raised it to at least 7 -- another order of the
+# same sums, which the band already samples)
 ROWS_PER_GROUP = {1264: 5, 554: 3}
 
 
