@@ -42,6 +42,7 @@ WORKLOADS = {
     # the many-point ethanol shape (pair-tile operator): configs[0]'s M = 111 and the
     # reference's N = 74979 point
     "ethanol_m111": ["--workload", "ethanol", "--m", "111", "--storage", "matfree"],
+    "ethanol_m583": ["--workload", "ethanol", "--m", "583", "--storage", "matfree"],
     "ethanol_m2777": ["--workload", "ethanol", "--m", "2777", "--storage", "matfree"],
 }
 GROUPS = {
