@@ -86,13 +86,13 @@ for s in ${STEPS:-suite smoke bench}; do
           step rpw${r}_nt_r$rep 300 env MLFF_LR_MIN_RPW=$r python bench.py --workload nanotube --no-cpu --no-solve --steps 200 --warmup 10
         done
       done ;;
-    final)  # evidence at the final library: smoke, default bench + its rocprof kernel stats, PMC
-            # traffic of the bench's kernel groups, the default bench again (traffic stamped), the
-            # nanotube and ethanol N = 15741 lines with their CPU baselines
+    final1)  # evidence at the final library (1/2): smoke, the default bench under rocprofv3
+             # --kernel-trace --stats, PMC traffic of the bench's kernel groups
       step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
       step final_bench_prof 600 rocprofv3 --kernel-trace --stats -d $O/final_prof -o bench --output-format csv -- python3 bench.py
-      step final_pmc 1100 python scripts/pmc_head.py --out $O/pmc_head
-      cp $O/pmc_head/pmc_traffic.json profiles/pmc_traffic.json
+      step final_pmc 1000 python scripts/pmc_head.py --out $O/pmc_head ;;
+    final2)  # (2/2): the default bench (traffic from the committed PMC table), the nanotube and
+             # ethanol N = 15741 lines with their CPU baselines
       step final_bench 600 python bench.py
       step final_nt 300 python bench.py --workload nanotube
       step final_eth583 600 python bench.py --workload ethanol --m 583 ;;
