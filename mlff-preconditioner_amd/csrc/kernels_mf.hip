@@ -108,10 +108,59 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               int n, int n_perms, int64_t D,
                                               const double *__restrict__ x,
                                               double *__restrict__ Zt,
-                                              const int *__restrict__ status, PFuse pf = PFuse{}) {
+                                              const int *__restrict__ status, PFuse pf = PFuse{},
+                                              int rows = 1) {
   if (status != nullptr && *status != ST_RUNNING) return;
-  const int64_t jp = blockIdx.y;
   const ZSrc zs{Rdd, Pt, ps, pt, n, n_perms, x, Zt};
+  if (rows > 1) {
+    // short descriptors (D <= 128: few atoms): `rows` (j, p) rows per workgroup, one thread per
+    // (row, entry) -- a full workgroup instead of D of 256 threads, and (fused) one rho sum per
+    // `rows` rows; the operands are requested before the rho sum
+    const int tid = threadIdx.x;
+    const int64_t jp = (int64_t)blockIdx.x * rows + tid / D, d = tid % D;
+    const bool ok = tid < rows * D && jp < M * n_perms;
+    double r[3] = {0.0, 0.0, 0.0}, xt[3] = {0.0, 0.0, 0.0}, xs[3] = {0.0, 0.0, 0.0};
+    double zt[3] = {0.0, 0.0, 0.0}, zsv[3] = {0.0, 0.0, 0.0};
+    if (ok) {
+      const int64_t j = jp / n_perms, p = jp % n_perms, g0 = j * 3 * n;
+      const int64_t e = Pt != nullptr ? (int64_t)Pt[p * D + d] : d;
+      const int sa = ps[e], ta = pt[e];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        r[c] = Rdd[(j * D + e) * 3 + c];
+        xt[c] = x[g0 + 3 * ta + c];
+        xs[c] = x[g0 + 3 * sa + c];
+        if (FP) {
+          zt[c] = pf.z[g0 + 3 * ta + c];
+          zsv[c] = pf.z[g0 + 3 * sa + c];
+        }
+      }
+    }
+    double beta = 0.0;
+    const bool first = FP && pf.it <= 1;
+    if (FP) {
+      __shared__ double shq[8];
+      const bool sfold = pf.sf.rr_part != nullptr;
+      const double rho1 = sfold ? pf.st->rho : pf.st->rho1;
+      const double rho = parts_bcast(parts_thread_sum(pf.rho_part, kVecGrid), shq);
+      beta = rho / rho1;
+      if (blockIdx.x == 0) {
+        if (tid == 0) pf.st->rho_new = rho;
+        if (sfold) stop_decide(pf.sf, reduce_parts_bcast(pf.sf.rr_part, kVecGrid, shq));
+      }
+    }
+    if (!ok) return;
+    double z = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double a = FP ? fused_p(xt[c], zt[c], beta, first) : xt[c];
+      const double b = FP ? fused_p(xs[c], zsv[c], beta, first) : xs[c];
+      z = fma(r[c], a - b, z);
+    }
+    Zt[jp * D + d] = z;
+    return;
+  }
+  const int64_t jp = blockIdx.y;
   if (!FP) {
     for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)
       Zt[jp * D + d] = z_entry(zs, D, jp, d);
@@ -1393,15 +1442,18 @@ bool mf_columns(const mlff_ctx *ctx, const int64_t *cols, int64_t ncols, double 
 
 void launch_mf_zt(const MfData &mf, const double *xc, const int *status, hipStream_t s,
                   const PFuse *pf) {
-  const unsigned gx = (unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024);
+  const int64_t MP = mf.M * mf.n_perms;
   const int32_t *Pt = mf.ident ? (const int32_t *)nullptr : (const int32_t *)mf.Pt;
+  // D <= 128: several (j, p) rows per workgroup (ethanol D = 36: 7), else a row per grid row
+  const int rows = mf.D <= 128 ? (int)(256 / mf.D) : 1;
+  const dim3 grid = rows > 1 ? dim3((unsigned)((MP + rows - 1) / rows))
+                             : dim3((unsigned)std::min<int64_t>((mf.D + 255) / 256, 1024), (unsigned)MP);
   if (pf != nullptr)
-    hipLaunchKernelGGL(k_mf_z<true>, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
-                       Pt, mf.ps, mf.pt, mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status, *pf);
+    hipLaunchKernelGGL(k_mf_z<true>, grid, dim3(256), 0, s, mf.Rdd, Pt, mf.ps, mf.pt, mf.M, (int)mf.n,
+                       (int)mf.n_perms, mf.D, xc, mf.Zt, status, *pf, rows);
   else
-    hipLaunchKernelGGL(k_mf_z<false>, dim3(gx, (unsigned)(mf.M * mf.n_perms)), dim3(256), 0, s, mf.Rdd,
-                       Pt, mf.ps, mf.pt, mf.M, (int)mf.n, (int)mf.n_perms, mf.D, xc, mf.Zt, status,
-                       PFuse{});
+    hipLaunchKernelGGL(k_mf_z<false>, grid, dim3(256), 0, s, mf.Rdd, Pt, mf.ps, mf.pt, mf.M, (int)mf.n,
+                       (int)mf.n_perms, mf.D, xc, mf.Zt, status, PFuse{}, rows);
 }
 
 double mf_seconds(const mlff_ctx *ctx) {
