@@ -212,6 +212,178 @@ void k_pt_pair(PtArgs a, const int *__restrict__ status) {
     *reinterpret_cast<double2 *>(out + 2 * (l + L * e)) = make_double2(f[2 * e], f[2 * e + 1]);
 }
 
+// k_pt_mfma<DR, NT, DZM>: the force sum on the matrix cores.  |diff|^2 stays on the VALU with
+// direct differences (no |a|^2 + |b|^2 - 2 a.b cancellation: the self pair keeps nrm = 0), each
+// pair formed by ONE lane (no butterfly, no redundant sqrt / exp); the accumulation
+//   F_i = sum_jp c (Rd_i - Rt_jp) - w Zt_jp = Rd'_i sum_jp c  -  sum_jp [c | w] [Rt' ; Zt]
+// is a (points x 2 rows) x (2 rows x D) product on v_mfma_f64_16x16x4f64, and with DZM so is
+//   diff . Zt_jp = Rd'_i . Zt_jp - Rt'_jp . Zt_jp      (rows x D) x (D x points), minus q_jp,
+// with the descriptors centred on training point 0 (Rd' = Rd - mu, Rt' = Rt - mu: for
+// geometries of one molecule every entry lies within a factor 2 of mu's, so the centring is
+// exact (Sterbenz) and Rd' - Rt' has the bits of Rd - Rt, while |Rd'| ~ |diff| keeps the
+// expansions' cancellation at O(1): their error is eps |Rd'| |Zt| per product, the size of the
+// direct form's own rounding against the operator's scale).  A wave holds 16 query points
+// (lane & 15; Rd' row in registers); lane kk = lane >> 4 forms the pairs with rows 4 r + kk of
+// each 16-row block -- the A operand layout of the force MFMA's k-step r and the output layout
+// of the (rows x points) diff . Zt product, so dz, c and w never change lanes.  The four waves
+// of a workgroup (64 points) share the LDS tiles of Rt' / Zt (32 rows, stride DS); q_jp is
+// summed while the tile is staged (8 threads per row, DPP butterfly: fixed order).
+constexpr int kMfPts = 64;
+constexpr int kMfTJ = 32;
+typedef double v4d __attribute__((ext_vector_type(4)));
+template <int DR, int NT, bool DZM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_pt_mfma(PtArgs a, const int *__restrict__ status) {
+  static_assert(DR % 4 == 0 && DR <= 16 * NT, "register row within the n-tiles");
+  constexpr int DC = 16 * NT;        // staged columns (zero past D)
+  constexpr int DS = DC + 2;         // LDS row stride: the 4 rows a wave reads sit in 4 bank groups
+  constexpr int EPT = DC / 8;        // staged entries per thread: 8 threads per row, 32 rows
+  static_assert(DC % 8 == 0 && kMfTJ * 8 == 256, "staging");
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sR[kMfTJ * DS];
+  __shared__ double sZ[kMfTJ * DS];
+  __shared__ double sQ[kMfTJ];
+  __shared__ double sMu[DC];
+  __shared__ double sC[4][16];
+  __shared__ double sCW[4][2][4][64];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int pi = lane & 15, kk = lane >> 4;
+  for (int d = tid; d < DC; d += 256) sMu[d] = d < a.D ? a.Rd[d] : 0.0;
+  __syncthreads();
+  const int64_t ib = (int64_t)blockIdx.x * kMfPts + wv * 16;
+  const int64_t il = ib + pi;
+  const bool live = il < a.ni;
+  double rd[DR];
+  {
+    const double *row = a.Rd + (a.i0 + (live ? il : 0)) * a.D;
+#pragma unroll
+    for (int d = 0; d < DR; ++d) rd[d] = (live && d < a.D) ? row[d] - sMu[d] : 0.0;
+  }
+  double rdB[DR / 4];  // B operand of the diff . Zt product: Rd'[pi][4 s + kk]
+  if (DZM) {
+#pragma unroll
+    for (int s4 = 0; s4 < DR / 4; ++s4)
+      rdB[s4] = kk == 0 ? rd[4 * s4] : kk == 1 ? rd[4 * s4 + 1] : kk == 2 ? rd[4 * s4 + 2] : rd[4 * s4 + 3];
+  }
+  const int64_t s = blockIdx.y;
+  const int64_t jb0 = (a.MP * s) / a.S, jb1 = (a.MP * (s + 1)) / a.S;
+  const int64_t ntile = (jb1 - jb0 + kMfTJ - 1) / kMfTJ;
+  const int srow = tid >> 3, sd0 = (tid & 7) * EPT;  // staging: row, first entry
+  double vr[EPT], vz[EPT];
+  auto load_tile = [&](int64_t t) {
+    const int64_t jp = jb0 + t * kMfTJ + srow;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int d = sd0 + u;
+      const bool ok = jp < jb1 && d < a.D;
+      vr[u] = ok ? a.Rt[jp * a.D + d] : 0.0;
+      vz[u] = ok ? a.Zt[jp * a.D + d] : 0.0;
+    }
+  };
+  v4d acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  double csum = 0.0;
+  if (ntile > 0) load_tile(0);
+  for (int64_t t = 0; t < ntile; ++t) {
+    __syncthreads();  // the previous tile is consumed
+    {
+      const bool rok = jb0 + t * kMfTJ + srow < jb1;
+      double q = 0.0;
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        const int d = sd0 + u;
+        // padded rows stay zero (not -mu): diff . 0 = 0 gives c = 0, and w meets Zt = 0
+        const double rv = (rok && d < a.D) ? vr[u] - sMu[d] : 0.0;
+        sR[srow * DS + d] = rv;
+        sZ[srow * DS + d] = vz[u];
+        q = fma(rv, vz[u], q);
+      }
+      if (DZM) {
+        q = group_sum<8>(q);
+        if ((tid & 7) == 0) sQ[srow] = q;
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ntile) load_tile(t + 1);  // in flight during this tile's pairs
+#pragma unroll 1
+    for (int b = 0; b < kMfTJ / 16; ++b) {
+      if (DZM) {  // dz[q] of rows b 16 + kk + 4 q, point pi
+        v4d dz = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < DR / 4; ++s4)
+          dz = __builtin_amdgcn_mfma_f64_16x16x4f64(sZ[(b * 16 + pi) * DS + 4 * s4 + kk], rdB[s4], dz,
+                                                    0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sCW[wv][0][r][lane] = dz[r] - sQ[b * 16 + 4 * r + kk];
+      }
+      // one pair row at a time (one inlined exp; dz, c, w through this lane's LDS slots)
+#pragma unroll 2
+      for (int r = 0; r < 4; ++r) {
+        const double *rr = sR + (b * 16 + 4 * r + kk) * DS;
+        const double *zr = sZ + (b * 16 + 4 * r + kk) * DS;
+        double r2a = 0.0, r2b = 0.0, aa = 0.0, ab = 0.0;
+#pragma unroll
+        for (int e = 0; e < DR / 2; ++e) {
+          const double2 tv = *reinterpret_cast<const double2 *>(rr + 2 * e);
+          const double d0 = rd[2 * e] - tv.x, d1 = rd[2 * e + 1] - tv.y;
+          r2a = fma(d0, d0, r2a);
+          r2b = fma(d1, d1, r2b);
+          if (!DZM) {
+            const double2 zv = *reinterpret_cast<const double2 *>(zr + 2 * e);
+            aa = fma(d0, zv.x, aa);
+            ab = fma(d1, zv.y, ab);
+          }
+        }
+        const double dz = DZM ? sCW[wv][0][r][lane] : aa + ab;
+        const double nrm = kSqrt5 * sqrt(r2a + r2b);
+        const double m = exp(-nrm * a.inv_sig) * a.k5;
+        const double c = 5.0 * m * dz;
+        sCW[wv][0][r][lane] = -c;
+        sCW[wv][1][r][lane] = -(fma(a.sig, nrm, a.sig2) * m);
+        csum += c;
+      }
+      double cA[4], wA[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // the lane's own slots: no barrier
+        cA[r] = sCW[wv][0][r][lane];
+        wA[r] = sCW[wv][1][r][lane];
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+              cA[r], sR[(b * 16 + 4 * r + kk) * DS + 16 * nt + pi], acc[nt], 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+              wA[r], sZ[(b * 16 + 4 * r + kk) * DS + 16 * nt + pi], acc[nt], 0, 0, 0);
+      }
+    }
+  }
+  // sum_jp c of point pi: the four row-lanes' partials in a commutative pair order
+  csum += __shfl_xor(csum, 16);
+  csum += __shfl_xor(csum, 32);
+  if (kk == 0) sC[wv][pi] = csum;
+  __syncthreads();
+  // acc[nt][q] = F'[point kk + 4 q][entry 16 nt + pi]
+  constexpr int64_t DP = DR;  // chunk partial stride: the variant's L * DL (pt_padded_d)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int pq = kk + 4 * q;
+    const int64_t ilq = ib + pq;
+    if (ilq >= a.ni) continue;
+    const double cs = sC[wv][pq];
+    const double *row = a.Rd + (a.i0 + ilq) * a.D;
+    double *out = a.part + (s * a.ni + ilq) * DP;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int d = 16 * nt + pi;
+      if (d < a.D) out[d] = fma(row[d] - sMu[d], cs, acc[nt][q]);
+    }
+  }
+}
+
 __device__ __forceinline__ int64_t pt_pair(int a, int b) {
   return a > b ? (int64_t)a * (a - 1) / 2 + b : (int64_t)b * (b - 1) / 2 + a;
 }
@@ -320,33 +492,40 @@ using PairFn = void (*)(PtArgs, const int *);
 struct PtVariant {
   int L, DL;
   PairFn fn;
+  int G;  // query points per workgroup
 };
 
 // L lanes per point (partial sums joined by the DPP butterfly), DL entries per lane; the
 // first variant that covers D is the default.  MLFF_PT_VARIANT=<index> forces one (sweeps; it
 // must cover D)
 const PtVariant kPtVariants[] = {
-    {2, 18, k_pt_pair<2, 18, 1, true, true>},    // D <= 36  (n <= 9: ethanol)
-    {4, 18, k_pt_pair<4, 18, 1, true, false>},   // D <= 72  (n <= 12: uracil)
-    {4, 28, k_pt_pair<4, 28, 1, false, false>},  // D <= 112 (n <= 15: toluene)
-    {8, 28, k_pt_pair<8, 28, 1, false, false>},  // D <= 224 (n <= 21: aspirin)
-    {8, 36, k_pt_pair<8, 36, 1, false, false>},  // D <= 288 (n <= 24: azobenzene)
+    {2, 18, k_pt_pair<2, 18, 1, true, true>, 128},    // D <= 36  (n <= 9: ethanol)
+    {4, 18, k_pt_pair<4, 18, 1, true, false>, 64},   // D <= 72  (n <= 12: uracil)
+    {4, 28, k_pt_pair<4, 28, 1, false, false>, 64},  // D <= 112 (n <= 15: toluene)
+    {8, 28, k_pt_pair<8, 28, 1, false, false>, 32},  // D <= 224 (n <= 21: aspirin)
+    {8, 36, k_pt_pair<8, 36, 1, false, false>, 32},  // D <= 288 (n <= 24: azobenzene)
     // sweep variants of the ethanol shape (MLFF_PT_VARIANT)
-    {2, 18, k_pt_pair<2, 18, 2, true, false>},
-    {2, 18, k_pt_pair<2, 18, 2, true, true>},
-    {4, 10, k_pt_pair<4, 10, 2, true, true>},
-    {4, 10, k_pt_pair<4, 10, 1, true, true>},
-    {1, 36, k_pt_pair<1, 36, 2, false, false>},
-    {2, 18, k_pt_pair<2, 18, 1, true, false, 3>},   // 10: 3 waves per SIMD
-    {2, 18, k_pt_pair<2, 18, 1, true, true, 3>},
-    {2, 18, k_pt_pair<2, 18, 1, false, false, 3>},
-    {2, 18, k_pt_pair<2, 18, 1, false, false, 4>},
+    {2, 18, k_pt_pair<2, 18, 2, true, false>, 128},
+    {2, 18, k_pt_pair<2, 18, 2, true, true>, 128},
+    {4, 10, k_pt_pair<4, 10, 2, true, true>, 64},
+    {4, 10, k_pt_pair<4, 10, 1, true, true>, 64},
+    {1, 36, k_pt_pair<1, 36, 2, false, false>, 256},
+    {2, 18, k_pt_pair<2, 18, 1, true, false, 3>, 128},   // 10: 3 waves per SIMD
+    {2, 18, k_pt_pair<2, 18, 1, true, true, 3>, 128},
+    {2, 18, k_pt_pair<2, 18, 1, false, false, 3>, 128},
+    {2, 18, k_pt_pair<2, 18, 1, false, false, 4>, 128},
+    // 14, 15: the force sum (and 15: diff . Zt) on the matrix cores (D <= 36; MLFF_PT_MFMA=1 / 2)
+    {1, 36, k_pt_mfma<36, 3, false>, kMfPts},
+    {1, 36, k_pt_mfma<36, 3, true>, kMfPts},
 };
 
 const PtVariant *pt_variant(int64_t D) {
   const char *ev = std::getenv("MLFF_PT_VARIANT");
-  const int forced = ev != nullptr ? std::atoi(ev) : -1;
+  int forced = ev != nullptr ? std::atoi(ev) : -1;
   constexpr int nv = (int)(sizeof(kPtVariants) / sizeof(kPtVariants[0]));
+  if (forced < 0 && D <= 36)
+    if (const char *em = std::getenv("MLFF_PT_MFMA"); em != nullptr && std::atoi(em) != 0)
+      forced = std::atoi(em) == 1 ? nv - 2 : nv - 1;
   if (forced >= 0 && forced < nv && D <= (int64_t)kPtVariants[forced].L * kPtVariants[forced].DL)
     return &kPtVariants[forced];
   for (int i = 0; i < 5; ++i)
@@ -364,7 +543,7 @@ bool pt_supported(int64_t D) { return pt_variant(D) != nullptr; }
 int pt_chunks(int64_t D, int64_t ni, int64_t MP) {
   const PtVariant *v = pt_variant(D);
   if (v == nullptr || ni <= 0) return 1;
-  const int64_t G = kPtThreads / v->L, blocks = (ni + G - 1) / G;
+  const int64_t G = v->G, blocks = (ni + G - 1) / G;
   // one round of resident workgroups: the chip holds CUs x (workgroups per CU at this
   // kernel's registers) at once, and a grid one workgroup past that runs a second round of
   // the same length (M = 2777: 528 workgroups on 512 slots took 120 us, 506 take ~60)
@@ -411,7 +590,7 @@ void launch_pt_operator(const MfData &mf, const double *Rt, const double *xc, in
   a.inv_sig = 1.0 / mf.sig;
   a.k5 = 5.0 / (3.0 * mf.sig * mf.sig * mf.sig * mf.sig);
   a.part = mf.ptpart;
-  const int64_t G = kPtThreads / v->L;
+  const int64_t G = v->G;
   hipLaunchKernelGGL(v->fn, dim3((unsigned)((mf.ni + G - 1) / G), (unsigned)mf.pt_S), dim3(kPtThreads),
                      0, s, a, status);
   PtFin fa;

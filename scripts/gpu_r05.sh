@@ -96,6 +96,15 @@ for s in ${STEPS:-suite smoke bench}; do
       step final_bench 600 python bench.py
       step final_nt 300 python bench.py --workload nanotube
       step final_eth583 600 python bench.py --workload ethanol --m 583 ;;
+    ptmfma)  # pair-tile force sum on the matrix cores (MLFF_PT_MFMA=1) vs the VALU default, interleaved
+      for m in ${PTM:-583 2777 5833}; do
+        for r in 1 2; do
+          step ptv_m${m}_r$r 300 python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 50 --warmup 5
+          for v in ${PTMV:-1 2}; do
+            step ptm${v}_m${m}_r$r 300 env MLFF_PT_MFMA=$v python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 50 --warmup 5
+          done
+        done
+      done ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do

@@ -410,9 +410,14 @@ def test_pair_tile_operator_matches_pair_path(sg, golden_dir, monkeypatch, n_ato
     np.testing.assert_allclose(run("pt"), ref, rtol=0, atol=tol)
     np.testing.assert_allclose(run("pt", world=3), ref, rtol=0, atol=tol)
     np.testing.assert_allclose(run("pt", {"MLFF_PT_CHUNKS": "1"}), ref, rtol=0, atol=tol)
-    # every entry of kernels_pt.hip's variant table (one that does not cover D runs the default)
-    for i in range(14):
+    # every entry of kernels_pt.hip's variant table (one that does not cover D runs the default;
+    # 14, 15 = k_pt_mfma, the force sum (15: and diff . Zt) on the matrix cores, D <= 36)
+    for i in range(16):
         np.testing.assert_allclose(run("pt", {"MLFF_PT_VARIANT": str(i)}), ref, rtol=0, atol=tol)
+    if n_atoms <= 9:
+        for extra, world in (({"MLFF_PT_MFMA": "1"}, 3), ({"MLFF_PT_MFMA": "2"}, 3),
+                             ({"MLFF_PT_MFMA": "2", "MLFF_PT_CHUNKS": "1"}, 1)):
+            np.testing.assert_allclose(run("pt", extra, world=world), ref, rtol=0, atol=tol)
 
 
 def test_pair_tile_pcg_in_noise_band(sg, golden_dir):
