@@ -384,6 +384,162 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
   }
 }
 
+// k_pt_mfma_sp<DR, NT>: k_pt_mfma<DR, NT, false> software-pipelined so that the matrix pipe and
+// the VALU work at once: the force MFMAs of 16-row group g - 1 are issued between the VALU pair
+// rows of group g (row r of g, then group g - 1's k-step r: 2 NT MFMAs, independent of the row's
+// VALU chain), so each wave keeps both pipes busy instead of alternating VALU and MFMA phases.
+// Groups of 16 (j, p) rows are staged one per step into a 3-slot LDS ring (g - 1 read by the
+// MFMAs, g by the VALU, g + 1 written by the next step: one barrier per step orders them); c, w
+// of group g go to this lane's slots of a 2-deep buffer.  The (0 x zero rows) MFMAs of the first
+// step add exact zeros.  Same pairs, same operands as k_pt_mfma; the force sum's k-steps in
+// (group, row, c then w) order.
+template <int DR, int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_pt_mfma_sp(PtArgs a, const int *__restrict__ status) {
+  static_assert(DR % 2 == 0 && DR <= 16 * NT, "register row within the n-tiles");
+  constexpr int DC = 16 * NT;        // staged columns (zero past D)
+  constexpr int DS = DC + 2;         // LDS row stride
+  constexpr int kG = 16;             // rows per group
+  constexpr int EPT = kG * DC / 256; // staged entries per thread and array
+  static_assert(kG * DC % 256 == 0 && DC % EPT == 0, "staging");
+  if (status != nullptr && *status != ST_RUNNING) return;
+  __shared__ double sR[3][kG * DS];
+  __shared__ double sZ[3][kG * DS];
+  __shared__ double sMu[DC];
+  __shared__ double sC[4][16];
+  __shared__ double sCW[2][4][2][4][64];
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int pi = lane & 15, kk = lane >> 4;
+  for (int d = tid; d < DC; d += 256) sMu[d] = d < a.D ? a.Rd[d] : 0.0;
+  // the step-0 MFMAs read group "-1": slot 2 rows and buffer 1 c, w, all zero
+  for (int e = tid; e < kG * DS; e += 256) sR[2][e] = sZ[2][e] = 0.0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) (&sCW[1][wv][0][0][0])[lane + 64 * u] = 0.0;
+  __syncthreads();
+  const int64_t ib = (int64_t)blockIdx.x * kMfPts + wv * 16;
+  const int64_t il = ib + pi;
+  const bool live = il < a.ni;
+  double rd[DR];
+  {
+    const double *row = a.Rd + (a.i0 + (live ? il : 0)) * a.D;
+#pragma unroll
+    for (int d = 0; d < DR; ++d) rd[d] = (live && d < a.D) ? row[d] - sMu[d] : 0.0;
+  }
+  const int64_t s = blockIdx.y;
+  const int64_t jb0 = (a.MP * s) / a.S, jb1 = (a.MP * (s + 1)) / a.S;
+  const int64_t ngr = (jb1 - jb0 + kG - 1) / kG;
+  const int srow = tid / (DC / EPT), sd0 = (tid % (DC / EPT)) * EPT;
+  double vr[EPT], vz[EPT];
+  auto load_group = [&](int64_t g) {
+    const int64_t jp = jb0 + g * kG + srow;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int d = sd0 + u;
+      const bool ok = g < ngr && jp < jb1 && d < a.D;
+      vr[u] = ok ? a.Rt[jp * a.D + d] : 0.0;
+      vz[u] = ok ? a.Zt[jp * a.D + d] : 0.0;
+    }
+  };
+  v4d acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  double csum = 0.0;
+  load_group(0);
+  for (int64_t g = 0; g <= ngr; ++g) {
+    const int cur = (int)(g % 3), prv = (int)((g + 2) % 3);
+    const int cb = (int)(g & 1), pb = cb ^ 1;
+    if (g < ngr) {
+      const bool rok = jb0 + g * kG + srow < jb1;
+#pragma unroll
+      for (int u = 0; u < EPT; ++u) {
+        const int d = sd0 + u;
+        // padded rows stay zero (not -mu): diff . 0 = 0 gives c = 0, and w meets Zt = 0
+        sR[cur][srow * DS + d] = (rok && d < a.D) ? vr[u] - sMu[d] : 0.0;
+        sZ[cur][srow * DS + d] = vz[u];
+      }
+    }
+    __syncthreads();
+    if (g + 1 < ngr) load_group(g + 1);  // in flight during this step
+    if (g == ngr) {  // drain: the last group's force MFMAs
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double cp = sCW[pb][wv][0][r][lane], wp = sCW[pb][wv][1][r][lane];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(cp, sR[prv][(4 * r + kk) * DS + 16 * nt + pi],
+                                                         acc[nt], 0, 0, 0);
+          acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(wp, sZ[prv][(4 * r + kk) * DS + 16 * nt + pi],
+                                                         acc[nt], 0, 0, 0);
+        }
+      }
+      break;
+    }
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) {
+      // group g - 1's k-step r on the matrix pipe (its operands are ready), one MFMA after every
+      // few entries of pair row r of group g on the VALU: an MFMA the busy matrix pipe cannot
+      // take stalls the wave's in-order issue, so back-to-back MFMAs would idle the VALU
+      const double cp = sCW[pb][wv][0][r][lane], wp = sCW[pb][wv][1][r][lane];
+      double bR[NT], bZ[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        bR[nt] = sR[prv][(4 * r + kk) * DS + 16 * nt + pi];
+        bZ[nt] = sZ[prv][(4 * r + kk) * DS + 16 * nt + pi];
+      }
+      constexpr int kStep = DR / 2 / (2 * NT) > 0 ? DR / 2 / (2 * NT) : 1;
+      const double *rr = sR[cur] + (4 * r + kk) * DS;
+      const double *zr = sZ[cur] + (4 * r + kk) * DS;
+      double r2a = 0.0, r2b = 0.0, aa = 0.0, ab = 0.0;
+#pragma unroll
+      for (int e = 0; e < DR / 2; ++e) {
+        const double2 tv = *reinterpret_cast<const double2 *>(rr + 2 * e);
+        const double2 zv = *reinterpret_cast<const double2 *>(zr + 2 * e);
+        const double d0 = rd[2 * e] - tv.x, d1 = rd[2 * e + 1] - tv.y;
+        r2a = fma(d0, d0, r2a);
+        r2b = fma(d1, d1, r2b);
+        aa = fma(d0, zv.x, aa);
+        ab = fma(d1, zv.y, ab);
+        if (e % kStep == kStep - 1 && e / kStep < 2 * NT) {
+          const int i = e / kStep, nt = i >> 1;
+          acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64((i & 1) ? wp : cp, (i & 1) ? bZ[nt] : bR[nt],
+                                                         acc[nt], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int i = DR / 2 / kStep; i < 2 * NT; ++i) {  // short rows: the remaining k-steps
+        const int nt = i >> 1;
+        acc[nt] = __builtin_amdgcn_mfma_f64_16x16x4f64((i & 1) ? wp : cp, (i & 1) ? bZ[nt] : bR[nt],
+                                                       acc[nt], 0, 0, 0);
+      }
+      const double nrm = kSqrt5 * sqrt(r2a + r2b);
+      const double m = exp(-nrm * a.inv_sig) * a.k5;
+      const double c = 5.0 * m * (aa + ab);
+      sCW[cb][wv][0][r][lane] = -c;
+      sCW[cb][wv][1][r][lane] = -(fma(a.sig, nrm, a.sig2) * m);
+      csum += c;
+    }
+  }
+  csum += __shfl_xor(csum, 16);
+  csum += __shfl_xor(csum, 32);
+  if (kk == 0) sC[wv][pi] = csum;
+  __syncthreads();
+  constexpr int64_t DP = DR;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int pq = kk + 4 * q;
+    const int64_t ilq = ib + pq;
+    if (ilq >= a.ni) continue;
+    const double cs = sC[wv][pq];
+    const double *row = a.Rd + (a.i0 + ilq) * a.D;
+    double *out = a.part + (s * a.ni + ilq) * DP;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const int d = 16 * nt + pi;
+      if (d < a.D) out[d] = fma(row[d] - sMu[d], cs, acc[nt][q]);
+    }
+  }
+}
+
 __device__ __forceinline__ int64_t pt_pair(int a, int b) {
   return a > b ? (int64_t)a * (a - 1) / 2 + b : (int64_t)b * (b - 1) / 2 + a;
 }
@@ -517,6 +673,9 @@ const PtVariant kPtVariants[] = {
     // 14, 15: the force sum (and 15: diff . Zt) on the matrix cores (D <= 36; MLFF_PT_MFMA=1 / 2)
     {1, 36, k_pt_mfma<36, 3, false>, kMfPts},
     {1, 36, k_pt_mfma<36, 3, true>, kMfPts},
+    // 16: 14 software-pipelined (the force MFMAs of one row group beside the next one's VALU rows;
+    // MLFF_PT_MFMA=3)
+    {1, 36, k_pt_mfma_sp<36, 3>, kMfPts},
 };
 
 const PtVariant *pt_variant(int64_t D) {
@@ -525,7 +684,7 @@ const PtVariant *pt_variant(int64_t D) {
   constexpr int nv = (int)(sizeof(kPtVariants) / sizeof(kPtVariants[0]));
   if (forced < 0 && D <= 36)
     if (const char *em = std::getenv("MLFF_PT_MFMA"); em != nullptr && std::atoi(em) != 0)
-      forced = std::atoi(em) == 1 ? nv - 2 : nv - 1;
+      forced = nv - 4 + std::min(std::max(std::atoi(em), 1), 3);
   if (forced >= 0 && forced < nv && D <= (int64_t)kPtVariants[forced].L * kPtVariants[forced].DL)
     return &kPtVariants[forced];
   for (int i = 0; i < 5; ++i)

@@ -411,11 +411,13 @@ def test_pair_tile_operator_matches_pair_path(sg, golden_dir, monkeypatch, n_ato
     np.testing.assert_allclose(run("pt", world=3), ref, rtol=0, atol=tol)
     np.testing.assert_allclose(run("pt", {"MLFF_PT_CHUNKS": "1"}), ref, rtol=0, atol=tol)
     # every entry of kernels_pt.hip's variant table (one that does not cover D runs the default;
-    # 14, 15 = k_pt_mfma, the force sum (15: and diff . Zt) on the matrix cores, D <= 36)
-    for i in range(16):
+    # 14, 15 = k_pt_mfma, the force sum (15: and diff . Zt) on the matrix cores, 16 = 14
+    # software-pipelined; D <= 36)
+    for i in range(17):
         np.testing.assert_allclose(run("pt", {"MLFF_PT_VARIANT": str(i)}), ref, rtol=0, atol=tol)
     if n_atoms <= 9:
         for extra, world in (({"MLFF_PT_MFMA": "1"}, 3), ({"MLFF_PT_MFMA": "2"}, 3),
+                             ({"MLFF_PT_MFMA": "3"}, 3), ({"MLFF_PT_MFMA": "3", "MLFF_PT_CHUNKS": "1"}, 1),
                              ({"MLFF_PT_MFMA": "2", "MLFF_PT_CHUNKS": "1"}, 1)):
             np.testing.assert_allclose(run("pt", extra, world=world), ref, rtol=0, atol=tol)
 
