@@ -590,6 +590,12 @@ __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__
   for (int64_t il = blockIdx.x; il < a.ni; il += gridDim.x) {
     const int64_t i = a.i0 + il;
     const double *src = a.part + il * a.DP;
+    // the operand entries of this thread's row (n3 <= 72 < 256), requested with the partials
+    // (not after the barriers: one dependent load round less)
+    const int64_t rl0 = i * n3 + threadIdx.x - a.row0;
+    const bool rown = threadIdx.x < n3 && rl0 >= 0 && rl0 < a.nrows && a.xloc != nullptr;
+    const double xpre = rown ? a.xloc[rl0] : 0.0;
+    const double zpre = rown && fp ? a.z[rl0] : 0.0;
     for (int e = threadIdx.x; e < 3 * D; e += 256) sR[e] = a.Rdd[i * a.D * 3 + e];
     for (int e = threadIdx.x; e < Q * D; e += 256) {  // D > 256: Q = 1, two entries per thread
       const int g = e / D, d = e % D;
@@ -616,9 +622,9 @@ __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__
       if (rl < 0 || rl >= a.nrows) continue;
       const int at = r / 3, c = r % 3;
       double xv = 0.0;
-      if (a.xloc != nullptr) {  // requested before the J^T sum
-        xv = a.xloc[rl];
-        if (fp) xv = fused_p(xv, a.z[rl], beta, first);
+      if (a.xloc != nullptr) {
+        xv = r < 256 ? xpre : a.xloc[rl];  // r < n3 <= 72: the prefetched entry
+        if (fp) xv = fused_p(xv, r < 256 ? zpre : a.z[rl], beta, first);
       }
       double acc = 0.0;
       for (int b = 0; b < a.n; ++b) {
