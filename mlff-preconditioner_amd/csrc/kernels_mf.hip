@@ -110,7 +110,9 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
                                               double *__restrict__ Zt,
                                               const int *__restrict__ status, PFuse pf = PFuse{},
                                               int rows = 1) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+  // the status word is read here and tested once the operand loads are in flight (it only
+  // has to hold back the stores of an iteration past convergence)
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   const ZSrc zs{Rdd, Pt, ps, pt, n, n_perms, x, Zt};
   if (rows > 1) {
     // short descriptors (D <= 128: few atoms): `rows` (j, p) rows per workgroup, one thread per
@@ -138,11 +140,13 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
     }
     double beta = 0.0;
     const bool first = FP && pf.it <= 1;
+    const double rshare = FP ? parts_thread_sum(pf.rho_part, kVecGrid) : 0.0;
+    if (st0 != ST_RUNNING) return;  // uniform: before the first barrier
     if (FP) {
       __shared__ double shq[8];
       const bool sfold = pf.sf.rr_part != nullptr;
       const double rho1 = sfold ? pf.st->rho : pf.st->rho1;
-      const double rho = parts_bcast(parts_thread_sum(pf.rho_part, kVecGrid), shq);
+      const double rho = parts_bcast(rshare, shq);
       beta = rho / rho1;
       if (blockIdx.x == 0) {
         if (tid == 0) pf.st->rho_new = rho;
@@ -160,6 +164,7 @@ __global__ __launch_bounds__(256) void k_mf_z(const double *__restrict__ Rdd,
     Zt[jp * D + d] = z;
     return;
   }
+  if (st0 != ST_RUNNING) return;
   const int64_t jp = blockIdx.y;
   if (!FP) {
     for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256)

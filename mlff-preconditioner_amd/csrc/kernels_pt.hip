@@ -85,7 +85,8 @@ void k_pt_pair(PtArgs a, const int *__restrict__ status) {
   constexpr int kStage = TJ * DP;         // doubles per staged array
   constexpr int kPer = (kStage + kPtThreads - 1) / kPtThreads;
   constexpr int KD = KEEP_DF ? DL : 2, KZ = KEEP_Z ? DL : 2;
-  if (status != nullptr && *status != ST_RUNNING) return;
+  // the status word is tested once the point rows and the first tile are requested
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double sR[kStage];
   __shared__ double sZ[kStage];
   const int tid = threadIdx.x;
@@ -122,6 +123,7 @@ void k_pt_pair(PtArgs a, const int *__restrict__ status) {
     }
   };
   if (ntile > 0) load_tile(0);
+  if (st0 != ST_RUNNING) return;  // uniform: before the first barrier
   for (int64_t t = 0; t < ntile; ++t) {
     __syncthreads();  // the previous tile is consumed
 #pragma unroll
@@ -570,7 +572,9 @@ struct PtFin {
 // sigma y + lam x and the x . y partials
 constexpr int kPtFinMaxF = 512;  // LDS doubles of the group partials (Q D <= 256, or D <= 288)
 __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__ status) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+  // the status word gates the state write and the stores: tested once the first point's
+  // loads are issued
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double sP[kPtFinMaxF];
   __shared__ double sF[kPtFinMaxF];
   __shared__ double sR[3 * 288];
@@ -584,7 +588,7 @@ __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__
   if (fp) {  // rho as k_mf_z summed it, rho1 as its folded stop test left it: k_update_p's beta
     const double rho = a.st->rho_new;
     beta = rho / a.st->rho1;
-    if (blockIdx.x == 0 && threadIdx.x == 0) a.st->rho = rho;
+    if (st0 == ST_RUNNING && blockIdx.x == 0 && threadIdx.x == 0) a.st->rho = rho;
   }
   double pq = 0.0;
   for (int64_t il = blockIdx.x; il < a.ni; il += gridDim.x) {
@@ -610,6 +614,7 @@ __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__
       }
       sP[e] = sum;
     }
+    if (st0 != ST_RUNNING) return;  // uniform: before the first barrier and any global store
     __syncthreads();
     for (int d = threadIdx.x; d < D; d += 256) {
       double f = sP[d];
@@ -643,6 +648,7 @@ __global__ __launch_bounds__(256) void k_pt_fin(PtFin a, const int *__restrict__
     }
     __syncthreads();
   }
+  if (st0 != ST_RUNNING) return;  // uniform (a block without points)
   if (a.pq_part != nullptr) {
     const double t = block_sum256(pq, sh);
     if (threadIdx.x == 0) a.pq_part[blockIdx.x] = t;

@@ -488,7 +488,9 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
                                                         int cached_wgs,
                                                         const int *__restrict__ status,
                                                         StopFold fold, XrFold xf) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+  // the status word is read here and tested once r (and q) are requested: a stopped solver
+  // drops them unused, a running one does not wait a round trip for the gate first
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ d2 z_sh[M * kLrThreads];
   __shared__ double red[16];
   const int bytes = (int)(ldt * 8);
@@ -498,11 +500,13 @@ __global__ __launch_bounds__(kLrThreads) void k_lr_rows(const double *__restrict
   // (its partials' round trip then overlaps them; a stopped solver drops them unused)
   d2 rv[M];
   lr_load_row<M, 0>(rv, r, bytes);  // zeros beyond ldt
+  if (xf.x == nullptr && st0 != ST_RUNNING) return;  // uniform
   if (xf.x != nullptr) {
     // the residual of the previous iteration, r - alpha q (k_update_xr's arithmetic), before
     // the first row is requested (q, r and a row in registers at once would spill)
     d2 qv[M];
     lr_load_row<M, 0>(qv, xf.q, bytes);
+    if (st0 != ST_RUNNING) return;  // uniform: before the first barrier
     const double rho = xf.st->rho;
     const double pq = reduce_parts_bcast_wide(xf.pq_part, kVecGrid, red);
     const double alpha = rho / pq;
@@ -540,7 +544,8 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
                                                     double sigma_p, double lam_inv,
                                                     double *__restrict__ rho_part,
                                                     const int *__restrict__ status, XrFold xf) {
-  if (status != nullptr && *status != ST_RUNNING) return;
+  // the status word gates the stores only: tested once the first block's loads are issued
+  const int st0 = status != nullptr ? *status : ST_RUNNING;
   __shared__ double sh[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int g0 = (G * w) / NW, g1 = (G * (w + 1)) / NW;
@@ -572,6 +577,7 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
         for (int u = 0; u < 16; ++u) s += t[u];
       }
     }
+    if (st0 != ST_RUNNING) return;  // uniform: before the first barrier and any store
     __syncthreads();  // sh of the previous block
     sh[w][lane] = s;
     __syncthreads();
@@ -590,6 +596,7 @@ __global__ __launch_bounds__(64 * NW) void k_lr_fin(const double *__restrict__ z
       rho = fma(rv, zv, rho);
     }
   }
+  if (st0 != ST_RUNNING) return;  // uniform (a block without columns)
   if (w == 0) {
     const double tot = wave_sum(rho);
     if (lane == 0 && rho_part != nullptr) rho_part[blockIdx.x] = tot;
