@@ -729,7 +729,14 @@ int pt_chunks(int64_t D, int64_t ni, int64_t MP) {
   }
   const int64_t slots = (int64_t)cus * per_cu;
   int64_t S = std::max<int64_t>(1, slots / blocks);
-  S = std::min<int64_t>(S, (MP + 15) / 16);
+  // chunks of at least 16 rows -- unless that leaves the grid under a quarter of the CUs (few
+  // training points: configs[0]'s M = 111 ran 7 workgroups); then at least 4 rows (M = 111:
+  // 28 chunks, operator 20.3 -> 16.4 us, PCG step 38.7 -> 35.1 us; M = 583 keeps 37 x 5 = 185
+  // workgroups, where 52 / 74 chunks were slower; profiles/r05/pt_small/)
+  if (blocks * std::min<int64_t>(S, (MP + 15) / 16) < cus / 4)
+    S = std::min<int64_t>(S, (MP + 3) / 4);
+  else
+    S = std::min<int64_t>(S, (MP + 15) / 16);
   if (const char *e = std::getenv("MLFF_PT_CHUNKS")) S = std::atoi(e);  // sweeps
   return (int)std::max<int64_t>(1, std::min<int64_t>(S, MP));
 }

@@ -105,6 +105,24 @@ for s in ${STEPS:-suite smoke bench}; do
           done
         done
       done ;;
+    ptvar)  # pair-tile variant sweep at small M (MLFF_PT_VARIANT), interleaved
+      for m in ${PTM:-583}; do
+        for r in 1 2; do
+          for v in ${PTVS:-0 7 8}; do
+            step ptvar${v}_m${m}_r$r 300 env MLFF_PT_VARIANT=$v python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 100 --warmup 10
+          done
+        done
+      done ;;
+    ptch)  # pair-tile chunk count x variant at small M (MLFF_PT_CHUNKS, MLFF_PT_VARIANT), interleaved
+      for m in ${PTM:-111}; do
+        for r in 1 2; do
+          for v in ${PTVS:-0 8}; do
+            for c in ${PTCH:-7 14 28 56}; do
+              step ptch_v${v}_c${c}_m${m}_r$r 300 env MLFF_PT_VARIANT=$v MLFF_PT_CHUNKS=$c python bench.py --workload ethanol --m $m --no-cpu --no-solve --steps 100 --warmup 10
+            done
+          done
+        done
+      done ;;
     eth583)  # ethanol N = 15741 (harmonic labels) at the rule-of-thumb k and a published k, with the
              # refined (default) and one-step Woodbury panel
       for k in 1264 554; do
