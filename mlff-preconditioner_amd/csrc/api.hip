@@ -392,9 +392,14 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
   if (const char *e = std::getenv("MLFF_ZSPLIT"))  // sweeps
     ctx->zsplit = (int)std::min<int64_t>(std::max(1, std::atoi(e)), (k + 15) / 16);
   MLFF_HIP(ctx, hipMalloc(&ctx->zpart, sizeof(double) * ctx->zsplit * ctx->blk));
-  // one rank, rows that fit a workgroup's registers and at least 3 rows per workgroup (below
-  // that the G partial vectors cost as much traffic as the second panel pass they replace):
-  // the one-pass apply.  MLFF_LR_ROWS=0 / 1 forces the two-pass / one-pass apply (A/B, tests)
+  // one rank, rows that fit a workgroup's registers: the one-pass apply (at >= 7 rows per
+  // workgroup its G partial vectors are <= 2/7 of a panel pass) from k = 768, and at any k on
+  // short rows (N_loc <= 4096), where the launches it saves dominate the step: ethanol M = 111
+  // (N = 2997), k = 50 / 150 / 398: PCG step 33.7 / 33.2 / 35.3 -> 29.5 / 29.5 / 30.1 us; M = 23
+  // (N = 621), k = 30 / 132: 30.2 / 30.2 -> 28.7 / 28.4 us; at N = 15741, k = 300 the step is
+  // the same either way (52.3 / 52.0 us), and k = 554 keeps the two-pass order its golden
+  // fixture's crossings were measured with (profiles/r05/lr_small/).  MLFF_LR_ROWS=0 / 1
+  // forces the two-pass / one-pass apply (A/B, tests)
   for (void **p : {(void **)&ctx->lr_zpart, (void **)&ctx->lr_slots, (void **)&ctx->lr_fault})
     if (*p != nullptr) {
       (void)hipFree(*p);
@@ -402,7 +407,8 @@ int alloc_panel(mlff_ctx *ctx, int64_t k) {
     }
   const char *lr_env = std::getenv("MLFF_LR_ROWS");
   const bool lr_on = lr_env == nullptr || std::atoi(lr_env) != 0;
-  ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) && (lr_env ? lr_on : k >= 768);
+  ctx->lr_rows = ctx->world == 1 && lr_rows_fits(ctx->blk) &&
+                 (lr_env ? lr_on : (k >= 768 || ctx->blk <= 4096));
   // longer rows: clusters of workgroups share a row (lr_cluster_count of them resident);
   // worth it from ~4 rows per cluster (the Q partial vectors against the second pass)
   ctx->lr_cluster = false;
