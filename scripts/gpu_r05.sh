@@ -11,6 +11,10 @@
 #   pmc       scripts/pmc_head.py (FETCH_SIZE / WRITE_SIZE passes)
 #   cmd       $CMD (one free-form step, $LIM seconds)
 #   eth583    ethanol N = 15741 bench lines, k = 1264 / 554, refined vs one-step Woodbury panel
+#   ptmfma    pair-tile operator: matrix-core variants (MLFF_PT_MFMA=$PTMV) vs the VALU default
+#   ptvar     pair-tile variant sweep (MLFF_PT_VARIANT=$PTVS) at ethanol M = $PTM
+#   ptch      pair-tile chunk count x variant sweep (MLFF_PT_CHUNKS=$PTCH) at ethanol M = $PTM
+#   final1/2  evidence at the final library (smoke, rocprof, PMC table; bench lines)
 # every GPU step runs under its own timeout; the first failure ends the script
 set -u
 export TMPDIR=/tmp
