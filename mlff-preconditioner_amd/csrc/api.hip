@@ -676,6 +676,18 @@ int require_matrix(mlff_ctx *ctx) {
 // if they are to be used and not current.
 int resolve_storage(mlff_ctx *ctx) {
   ctx->use_mf = false;
+  if (ctx->exact_sums) {
+    // the exact-sum anchor (kernels_dd.hip) is a dense-row operator on one rank: refused for
+    // every other storage before any of them is chosen, so the fused matrix-free iteration
+    // (which moves the x / r update into the next apply) can never run beside its apply
+    if (ctx->world > 1 || ctx->storage == MLFF_STORAGE_MATFREE ||
+        ctx->storage == MLFF_STORAGE_SYMTILE || (!ctx->has_matrix && !ctx->rbf.ready))
+      return set_error(ctx, MLFF_ERR_STATE,
+                       "MLFF_EXACT_SUMS: dense-row storage (a matrix or RBF points) on one rank only");
+    MLFF_TRY(ensure_rows(ctx));
+    ctx->use_sym = false;
+    return MLFF_OK;
+  }
   if (ctx->storage == MLFF_STORAGE_MATFREE) {
     if (!ctx->mf.ready)
       return set_error(ctx, MLFF_ERR_STATE, "MLFF_STORAGE_MATFREE needs mlff_sgdml_operator / mlff_assemble_sgdml");
@@ -716,7 +728,7 @@ int resolve_storage(mlff_ctx *ctx) {
       return MLFF_OK;
     }
   }
-  if (ctx->storage == MLFF_STORAGE_DENSE || ctx->exact_sums) {  // the exact-sum anchor: rows
+  if (ctx->storage == MLFF_STORAGE_DENSE) {
     MLFF_TRY(ensure_rows(ctx));
     ctx->use_sym = false;
     return MLFF_OK;
@@ -771,16 +783,16 @@ int resolve_storage(mlff_ctx *ctx) {
 int launch_operator(mlff_ctx *ctx, const double *v_full, double *y_loc, const double *v_loc,
                     const int *status, double *pq_part = nullptr, const PFuse *pf = nullptr) {
   hipStream_t s = ctx->stream;
-  if (ctx->use_mf) {
-    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part, pf);
-    return MLFF_OK;
-  }
   if (ctx->exact_sums) {  // measurement anchor (kernels_dd.hip): dense rows, one rank
-    if (ctx->use_sym || ctx->world > 1)
+    if (ctx->use_mf || ctx->use_sym || ctx->world > 1)
       return set_error(ctx, MLFF_ERR_STATE, "MLFF_EXACT_SUMS: dense-row storage on one rank only");
     launch_dd_gemv_rows(ctx->K, ctx->ld, ctx->nrows, ctx->N, v_full, y_loc, ctx->sigma_K, ctx->lam,
                         v_loc, status, s);
     if (pq_part != nullptr) launch_dot_part(v_loc, y_loc, ctx->nrows, pq_part, status, s);
+    return MLFF_OK;
+  }
+  if (ctx->use_mf) {
+    launch_mf_operator(ctx, v_full, y_loc, v_loc, status, ctx->sigma_K, ctx->lam, pq_part, pf);
     return MLFF_OK;
   }
   if (!ctx->use_sym) {
@@ -935,7 +947,8 @@ int launch_iteration_ranks(mlff_ctx *ctx, long long it, std::vector<GemvMark> *m
     SymPack &sp = ctx->sym;
     launch_symv(sp, ctx->p_full, sp.P, status, s, pg);
     launch_sym_reduce_ranks(sp, ctx->rank, ctx->world, ctx->blk, ctx->p_full, pq_part(ctx),
-                            pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s, pg);
+                            pq_part(ctx) + kVecGrid, ctx->sigma_K, ctx->lam, status, s, pg,
+                            ctx->pq_publish);
     mark_end(ctx, marks, e0, it);
     c0 = mark_begin(ctx, marks);
     MLFF_TRY(comm_reduce_scatter(ctx, sp.yg, sp.yr, (size_t)sp.ystride));
@@ -1215,6 +1228,7 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
     *flag = e == nullptr || std::atoi(e) != 0;
   }
   if (const char *e = std::getenv("MLFF_FUSE_XR_RANKS")) ctx->fuse_xr_ranks = std::atoi(e) != 0;
+  if (const char *e = std::getenv("MLFF_PQ_PUBLISH")) ctx->pq_publish = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_WB_REFINE")) ctx->wb_refine = std::max(0, std::atoi(e));
   if (const char *e = std::getenv("MLFF_NYS_REFINE")) ctx->nys_refine = std::atoi(e) != 0;
   if (const char *e = std::getenv("MLFF_WB_GRAM")) ctx->wb_gram_dd = std::max(0, std::min(2, std::atoi(e)));

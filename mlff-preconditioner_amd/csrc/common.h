@@ -349,6 +349,8 @@ struct mlff_ctx {
   // sharded tiled iteration: k_update_xr_shares folded into the next T r pass (MLFF_FUSE_XR_RANKS=1;
   // off by default: SOLO floors 4.5 us slower at W = 4, equal at W = 8)
   bool fuse_xr_ranks = false;
+  bool pq_publish = false;
+  bool piv_persist_off = false;  // the persistent pivoted Cholesky timed out once (kernels_pivchol.hip)  // MLFF_PQ_PUBLISH=1: the separate k_pq_publish launch (A/B)
   // Woodbury panel re-orthogonalised by a second CholeskyQR step (MLFF_WB_REFINE, woodbury_inplace;
   // configs[1] at full size: 571 -> 366 iterations, the oracle's 367) and the same for the
   // Nystrom panel (MLFF_NYS_REFINE)
@@ -680,7 +682,7 @@ void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double si
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
                              const double *p_full, double *pq_part, double *pp_part,
                              double sigma, double lam, const int *status, hipStream_t s,
-                             PGather pg = PGather{});
+                             PGather pg = PGather{}, bool separate_publish = false);
 // y = sigma * src + lam * vloc over n entries (src may alias y)
 void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, double lam,
                       const double *vloc, const int *status, hipStream_t s);

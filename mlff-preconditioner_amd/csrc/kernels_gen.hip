@@ -5,6 +5,7 @@
 // Column positions use the padded rank-block layout of the context:
 //   pos(g) = (g / rows_per) * blk + g % rows_per.
 #include "common.h"
+#include "sgdml_col.h"
 
 namespace mlff {
 
@@ -158,13 +159,7 @@ void launch_gather_mm(const double *W, int64_t ldw, const int64_t *idx, int64_t 
 // where every Jacobian row d = pair(s, t) (s > t) has only two non-zero atoms:
 // J[d, t] = +Rdd[d], J[d, s] = -Rdd[d] (desc.py:444-462).
 
-__device__ __forceinline__ int64_t pair_idx(int a, int b) {
-  // tril_indices(n, -1) ordering, a != b
-  return a > b ? (int64_t)a * (a - 1) / 2 + b : (int64_t)b * (b - 1) / 2 + a;
-}
-__device__ __forceinline__ double pair_sign(int a, int b) {  // sign of J[pair(a,b), atom a]
-  return a > b ? -1.0 : 1.0;
-}
+// pair_idx / pair_sign: sgdml_col.h
 
 // The reference assembles the lower block triangle and mirrors it
 // (train.py:172-210, exploit_sym): block (i, j) = Blk(r=i, s=j) for j < i and
@@ -595,7 +590,6 @@ int sgdml_diag(mlff_ctx *ctx, const double *dRd, const double *dRdd, int64_t M, 
 // diagonal atom of permutation p) need its partner series, which the wave sums
 // lane-parallel first when its rows include that atom; then every lane writes one row.
 // ~250 waves for the nanotube (14 points x 18 row chunks), two dependent load rounds each.
-constexpr int kColRows = 64;
 __global__ __launch_bounds__(64) void k_sgdml_col(const double *__restrict__ Rdd, int64_t M,
                                                   int n, int64_t D, int64_t i0,
                                                   const int32_t *__restrict__ pi,
@@ -607,59 +601,12 @@ __global__ __launch_bounds__(64) void k_sgdml_col(const double *__restrict__ Rdd
                                                   double *__restrict__ out, int64_t ldo) {
   const int64_t g = cols != nullptr ? cols[blockIdx.y] : (int64_t)st->m_pi;
   if (g < 0) return;
-  const int n3 = 3 * n;
-  const int chunks = (n3 + kColRows - 1) / kColRows;
-  const int64_t il = blockIdx.x / chunks;  // local query point
-  const int t0 = (int)(blockIdx.x % chunks) * kColRows;
-  const int64_t i = i0 + il;
-  const int lane = threadIdx.x;
-  const int t = t0 + lane;                  // row of the point's 3n block
-  const int64_t r = i * n3 + t - row0;      // local row
-  const int64_t j = g / n3;
-  const int a = (int)((g % n3) / 3), c = (int)(g % 3);
-  const int64_t rec_stride = 6 * n + 2;
-  const double *rdds = Rdd + j * D * 3;
-  const double *rddr = Rdd + i * D * 3;
-  const double *recs = uvk + (il * M + j) * n_perms * rec_stride;
-  const bool act = t < n3 && r >= 0 && r < nrows;
-  const int b = t / 3, cr = t % 3;
-  double acc = 0.0;
-  for (int p = 0; p < n_perms; ++p) {
-    const int32_t *pp = pi + (int64_t)p * n;
-    const int bd = piinv[(int64_t)p * n + a];  // the row atom whose image is a
-    double gdv = 0.0;
-    if (3 * bd + 2 >= t0 && 3 * bd < t0 + kColRows) {  // wave-uniform: this chunk holds bd
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-      for (int x = lane; x < n; x += 64) {
-        if (x == bd) continue;
-        const int64_t d = pair_idx(bd, x);
-        const int px = pp[x];
-        const double js = pair_sign(a, px) * rdds[pair_idx(a, px) * 3 + c];
-        const double sd = pair_sign(bd, x);
-        s0 = fma(sd * rddr[d * 3 + 0], js, s0);
-        s1 = fma(sd * rddr[d * 3 + 1], js, s1);
-        s2 = fma(sd * rddr[d * 3 + 2], js, s2);
-      }
-      s0 = wave_sum(s0);
-      s1 = wave_sum(s1);
-      s2 = wave_sum(s2);
-      const double s0b = __shfl(s0, 0, 64), s1b = __shfl(s1, 0, 64), s2b = __shfl(s2, 0, 64);
-      gdv = cr == 0 ? s0b : (cr == 1 ? s1b : s2b);
-    }
-    if (act) {
-      const double *rec = recs + (int64_t)p * rec_stride;
-      const double m5 = 5.0 * rec[6 * n];
-      const double w = rec[6 * n + 1];
-      const double tv = m5 * rec[3 * b + cr] * rec[n3 + 3 * a + c];
-      double gv = gdv;
-      if (b != bd) {
-        const int64_t d = pair_idx(b, bd);
-        const int pb = pp[b];
-        gv = pair_sign(b, bd) * rddr[d * 3 + cr] * (pair_sign(a, pb) * rdds[pair_idx(a, pb) * 3 + c]);
-      }
-      acc += tv - w * gv;
-    }
-  }
+  const int chunks = (3 * n + kColRows - 1) / kColRows;
+  bool act;
+  int64_t r;
+  const double acc = sgdml_col_acc(Rdd, M, n, D, i0, pi, piinv, n_perms, uvk, row0, nrows, g,
+                                   blockIdx.x / chunks, (int)(blockIdx.x % chunks) * kColRows,
+                                   threadIdx.x, act, r);
   if (act) out[(int64_t)blockIdx.y * ldo + r] = sigma * acc;
 }
 

@@ -11,8 +11,12 @@
 // Multi-rank: the argmax is an allgather of per-rank (value, position) winners,
 // the pivot row L[m_pi, :m] an allreduce of a vector only its owner fills.
 #include "common.h"
+#include "sgdml_col.h"
 
+#include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <vector>
 
 namespace mlff {
 
@@ -429,6 +433,386 @@ __global__ __launch_bounds__(256) void k_spec_gather(const double *__restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Persistent steps (one rank; round 6).  The launch sequence above spends 4 dependent launches
+// per pivot (finalise, column, Schur GEMV, finisher: ~21 us of kernels and ~13 us of launch gaps
+// per step on the nanotube).  k_piv_persist runs a whole speculative block of steps
+// in one launch: a grid of G resident workgroups (one per CU) synchronised by epoch-tagged
+// per-workgroup granules (data as flag, no contended counter), one synchronisation per step on a
+// speculation hit and two on a miss.  The arithmetic is the launch sequence's, operation for
+// operation (the same column code, the same Schur slices and their summation order, the same
+// finisher), so L, the pivots and the residual diagonal are bit-identical
+// (tests/test_gpu_pivchol_persist.py).
+//   step m: every workgroup reduces the G published (value, position, row) partials of step
+//   m - 1 to the same winner; the pivot's row owner swaps perm / iperm, writes sqrt(pivot); on a
+//   miss the whole grid runs k_colgemv_part's split-K slices (virtual workgroups) into `part`
+//   and synchronises; then each row's thread evaluates its column entry (k_sgdml_col's body, or
+//   the dense row), sums the Schur slices in k_piv_fin's order, writes L[m, i] and the residual
+//   diagonal, and the workgroup publishes its partial argmax of step m.
+struct PersistArgs {
+  int64_t N, nrows, blk, rows_per;
+  double *Lt;
+  double *dwork;
+  int *pivflag;
+  int64_t *perm, *iperm;
+  DevState *st;
+  // column source: K != nullptr -> the dense rows; else the sGDML single-column path
+  const double *K;
+  int64_t ld;
+  double sigma;
+  const double *Rdd;
+  int64_t M;
+  int n;
+  int64_t D, i0;
+  const int32_t *pi, *piinv;
+  int n_perms;
+  const double *uvk;
+  int chunks;   // sGDML: 64-row chunks per query point
+  int nrw;      // row waves
+  double *part;
+  int kmax_split;
+  const int64_t *Cspec;
+  const double *Gspec;
+  int64_t spec_m0;  // -1: no speculative block
+  // partials of step m_begin - 1 (npc entries; rows == nullptr: row = position, step 0)
+  const double *pv_in;
+  const long long *pp_in, *pr_in;
+  int npc;
+  double *pv_out;  // this launch's last step: G entries
+  long long *pp_out, *pr_out;
+  unsigned long long *slots;  // G x 4 granules (tag << 32 | payload): value lo, hi, position, row
+  unsigned long long *flags;  // G granules: the miss GEMV's arrival
+  int64_t m_begin, m_end;
+  int mute;  // test hook (MLFF_PIV_MUTE): this workgroup stops publishing after step m_begin
+  unsigned long long *trace;  // MLFF_PIV_TRACE: 4 wall-clock stamps per (step, workgroup)
+};
+
+__host__ __device__ inline int ksplit_of(int64_t k, int64_t ncols) {  // choose_ksplit
+  const int64_t slabs = (ncols + 511) / 512;
+  int64_t sk = (k + 95) / 96;
+  const int64_t fill = (256 + slabs - 1) / slabs;
+  if (fill > sk) sk = fill;
+  const int64_t cap = (k + 15) / 16;
+  if (sk > cap) sk = cap;
+  if (sk < 1) sk = 1;
+  if (sk > 256) sk = 256;
+  return (int)sk;
+}
+
+typedef double pd2 __attribute__((ext_vector_type(2)));
+
+// colgemv_slice<false> (kernels_vec.hip) with t from LDS: the same fma chains
+__device__ __forceinline__ pd2 persist_slice(const pd2 *__restrict__ w2, int64_t ld2, int64_t j0,
+                                             int64_t j1, const double *t_sh) {
+  pd2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+  int64_t j = j0;
+  for (; j + 7 < j1; j += 8) {
+    pd2 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = w2[(j + u) * ld2];
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      const double t0 = t_sh[j + u - j0], t1 = t_sh[j + u + 1 - j0];
+      acc0.x = fma(a[u].x, t0, acc0.x);
+      acc0.y = fma(a[u].y, t0, acc0.y);
+      acc1.x = fma(a[u + 1].x, t1, acc1.x);
+      acc1.y = fma(a[u + 1].y, t1, acc1.y);
+    }
+  }
+  for (; j < j1; ++j) {
+    const pd2 a0 = w2[j * ld2];
+    const double t0 = t_sh[j - j0];
+    acc0.x = fma(a0.x, t0, acc0.x);
+    acc0.y = fma(a0.y, t0, acc0.y);
+  }
+  return acc0 + acc1;
+}
+
+// one column's entry of colgemv_slice over rows [j0, j1) (the .x / .y lane of the same chains)
+__device__ __forceinline__ double persist_slice1(const double *__restrict__ Lt, int64_t ldl,
+                                                 int64_t i, int64_t j0, int64_t j1,
+                                                 const double *t_sh) {
+  double acc0 = 0.0, acc1 = 0.0;
+  int64_t j = j0;
+  for (; j + 7 < j1; j += 8) {
+    double a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = Lt[(j + u) * ldl + i];
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      acc0 = fma(a[u], t_sh[j + u - j0], acc0);
+      acc1 = fma(a[u + 1], t_sh[j + u + 1 - j0], acc1);
+    }
+  }
+  for (; j < j1; ++j) acc0 = fma(Lt[j * ldl + i], t_sh[j - j0], acc0);
+  return acc0 + acc1;
+}
+
+constexpr unsigned long long kPersistTimeout = 100000000ull;  // 1 s of the 100 MHz clock
+
+// thread t < count waits until granules g[t * per .. + per) all carry `tag`; false on timeout
+// (every thread returns the same verdict through `bail`)
+__device__ __forceinline__ bool persist_wait(unsigned long long *g, int count, int per, unsigned tag,
+                                             unsigned long long *vals, int *bail) {
+  const int t = threadIdx.x;
+  if (t < count) {
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+      bool ok = true;
+      for (int q = 0; q < per; ++q) {
+        vals[q] = __hip_atomic_load(g + (int64_t)t * per + q, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && (unsigned)(vals[q] >> 32) == tag;
+      }
+      if (ok) break;
+      if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
+        *bail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  const bool ok = *bail == 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ok;
+}
+
+__device__ __forceinline__ void persist_publish(unsigned long long *g, int per, unsigned tag,
+                                                const unsigned *payload) {
+  for (int q = 0; q < per; ++q)
+    __hip_atomic_store(g + q, ((unsigned long long)tag << 32) | payload[q], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool SG>
+__global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
+  extern __shared__ double t_sh[];  // the pivot row L[c, m_pi] of the step's Schur range
+  __shared__ double sv[256];
+  __shared__ long long sp[256], sr[256];
+  __shared__ long long s_C[kSpecC];
+  __shared__ int s_bail;
+  const int G = (int)gridDim.x, wg = (int)blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  if (tid == 0) s_bail = 0;
+  if (a.spec_m0 >= 0 && tid < kSpecC) s_C[tid] = a.Cspec[tid];
+  __syncthreads();
+  const int64_t ldl = a.blk;
+  long long mpi = -1;
+  double sq = 0.0;
+  for (int64_t m = a.m_begin; m < a.m_end; ++m) {
+    // ---- the winner of step m from the partials of step m - 1 (the same in every workgroup:
+    // a strict total order, value descending then position ascending)
+    double bv = -INFINITY;
+    long long bp = LLONG_MAX, br = -1;
+    if (m == a.m_begin) {
+      for (int t = tid; t < a.npc; t += 256)
+        if (better(a.pv_in[t], a.pp_in[t], bv, bp)) {
+          bv = a.pv_in[t];
+          bp = a.pp_in[t];
+          br = a.pr_in != nullptr ? a.pr_in[t] : bp;
+        }
+    } else {
+      unsigned long long g[4];
+      if (!persist_wait(a.slots, G, 4, (unsigned)m, g, &s_bail)) goto fault;  // tag of step m - 1
+      if (tid < G) {
+        bv = __builtin_bit_cast(double, (g[1] << 32) | (g[0] & 0xffffffffull));
+        bp = (long long)(unsigned)(g[2] & 0xffffffffull);
+        br = (long long)(int)(unsigned)(g[3] & 0xffffffffull);
+        if (br < 0) bp = LLONG_MAX;  // an empty partial
+      }
+    }
+    if (a.trace != nullptr && tid == 0) a.trace[(m * G + wg) * 4 + 0] = wall_clock64();
+    sv[tid] = bv;
+    sp[tid] = bp;
+    sr[tid] = br;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (tid < o && better(sv[tid + o], sp[tid + o], sv[tid], sp[tid])) {
+        sv[tid] = sv[tid + o];
+        sp[tid] = sp[tid + o];
+        sr[tid] = sr[tid + o];
+      }
+      __syncthreads();
+    }
+    bv = sv[0];
+    bp = sp[0];
+    br = sr[0];
+    __syncthreads();
+    const bool valid = bp >= m && bp < (long long)a.N && bv == bv && bv > -INFINITY && br >= 0;
+    mpi = valid ? br : -1;
+    sq = valid ? sqrt(bv) : 0.0;
+    if (wg == 0 && tid == 0 && (!valid || !(bv > 0.0))) a.st->pivot_err = 1;
+    int hit = -1;
+    if (a.spec_m0 >= 0 && mpi >= 0)
+      for (int j = 0; j < kSpecC; ++j)
+        if (s_C[j] == mpi) {
+          hit = j;
+          break;
+        }
+    const int ks = m > 0 ? min(a.kmax_split, ksplit_of(m, a.blk)) : 0;
+    const int64_t kslice = ks > 0 ? (m + ks - 1) / ks : 1;
+    const int64_t c_lo = hit >= 0 ? a.spec_m0 : 0;
+    if (mpi >= 0)
+      for (int64_t c = c_lo + tid; c < m; c += 256) t_sh[c - c_lo] = a.Lt[c * ldl + mpi];
+    __syncthreads();
+    // ---- a miss: k_colgemv_part's split-K slices over [0, m) by the whole grid
+    if (mpi >= 0 && hit < 0 && ks > 0) {
+      const int64_t nbx = (a.blk / 2 + 255) / 256, nvb = nbx * ks, ld2 = a.blk / 2;
+      for (int64_t vb = wg; vb < nvb; vb += G) {
+        const int64_t bx = vb % nbx, by = vb / nbx;
+        const int64_t j0 = by * kslice, j1 = j0 + kslice < m ? j0 + kslice : m;
+        const int64_t c2 = bx * 256 + tid;
+        if (2 * c2 < a.blk && j0 < j1) {
+          const pd2 acc = persist_slice(reinterpret_cast<const pd2 *>(a.Lt) + c2, ld2, j0, j1,
+                                        t_sh + j0);
+          reinterpret_cast<pd2 *>(a.part + by * a.blk)[c2] = acc;
+        } else if (2 * c2 < a.blk) {
+          reinterpret_cast<pd2 *>(a.part + by * a.blk)[c2] = pd2{0.0, 0.0};
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned zero = 0;
+        persist_publish(a.flags + wg, 1, (unsigned)m + 1, &zero);
+      }
+      unsigned long long g1[1];
+      if (!persist_wait(a.flags, G, 1, (unsigned)m + 1, g1, &s_bail)) goto fault;
+    }
+    // ---- rows: column entry, Schur sum, L[m, i], residual diagonal, partial argmax
+    if (a.trace != nullptr && tid == 0) a.trace[(m * G + wg) * 4 + 1] = wall_clock64();
+    {
+      double cbv = -INFINITY;
+      long long cbp = (long long)a.N, cbr = -1;
+      const int64_t pos = mpi >= 0 ? (mpi / a.rows_per) * a.blk + (mpi % a.rows_per) : 0;
+      for (int r = wg + G * w; r < a.nrw; r += 4 * G) {
+        bool act;
+        int64_t i;
+        double col = 0.0;
+        if (SG) {
+          double acc = 0.0;
+          if (mpi >= 0)
+            acc = sgdml_col_acc(a.Rdd, a.M, a.n, a.D, a.i0, a.pi, a.piinv, a.n_perms, a.uvk, 0,
+                                a.nrows, mpi, r / a.chunks, (r % a.chunks) * kColRows, lane, act, i);
+          else {
+            act = false;
+            i = 0;
+          }
+          col = a.sigma * acc;
+        } else {
+          i = (int64_t)r * 64 + lane;
+          act = i < a.nrows;
+          if (act && mpi >= 0) col = a.sigma * a.K[i * a.ld + pos];
+        }
+        if (!act || mpi < 0) continue;
+        if (i == mpi) {  // k_piv_finalize's writes for the pivot row
+          a.Lt[m * ldl + i] = sq;
+          a.pivflag[i] = 1;
+          a.iperm[i] = m;
+          a.perm[m] = i;
+          continue;
+        }
+        if (a.pivflag[i]) continue;
+        long long pos_i = a.iperm[i];
+        if (pos_i == m) {  // the row the swap moves from position m to bp
+          pos_i = bp;
+          a.iperm[i] = bp;
+          a.perm[bp] = i;
+        }
+        double s0 = 0.0;
+        if (hit >= 0) {  // the slices' parts from spec_m0 on, in slice order, then the G row
+          for (int64_t z = c_lo / kslice; z < ks; ++z) {
+            int64_t j0 = z * kslice;
+            const int64_t j1 = j0 + kslice < m ? j0 + kslice : m;
+            if (j0 < a.spec_m0) j0 = a.spec_m0 < j1 ? a.spec_m0 : j1;
+            if (j0 >= j1) continue;
+            s0 += persist_slice1(a.Lt, ldl, i, j0, j1, t_sh + (j0 - c_lo));
+          }
+          s0 += a.Gspec[(int64_t)hit * ldl + i];
+        } else {
+          int z = 0;
+          for (; z + 7 < ks; z += 8) {
+            double t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = a.part[(int64_t)(z + u) * a.blk + i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s0 += t[u];
+          }
+          for (; z < ks; ++z) s0 += a.part[(int64_t)z * a.blk + i];
+        }
+        const double v = (col - s0) / sq;
+        a.Lt[m * ldl + i] = v;
+        const double dn = a.dwork[i] - v * v;
+        a.dwork[i] = dn;
+        if (better(dn, pos_i, cbv, cbp)) {
+          cbv = dn;
+          cbp = pos_i;
+          cbr = i;
+        }
+      }
+      if (a.trace != nullptr && lane == 0)  // the slowest wave's row phase
+        atomicMax(&a.trace[(m * G + wg) * 4 + 2], (unsigned long long)wall_clock64());
+      sv[tid] = cbv;
+      sp[tid] = cbp;
+      sr[tid] = cbr;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o && better(sv[tid + o], sp[tid + o], sv[tid], sp[tid])) {
+          sv[tid] = sv[tid + o];
+          sp[tid] = sp[tid + o];
+          sr[tid] = sr[tid + o];
+        }
+        __syncthreads();
+      }
+      if (tid == 0) {
+        if (m + 1 < a.m_end) {
+          const unsigned long long vb = __builtin_bit_cast(unsigned long long, sv[0]);
+          const unsigned pl[4] = {(unsigned)(vb & 0xffffffffull), (unsigned)(vb >> 32),
+                                  (unsigned)(sr[0] >= 0 ? sp[0] : 0), (unsigned)(int)sr[0]};
+          if (wg != a.mute || m == a.m_begin)  // a muted workgroup: every wait times out
+            persist_publish(a.slots + (int64_t)wg * 4, 4, (unsigned)m + 1, pl);
+          if (a.trace != nullptr) a.trace[(m * G + wg) * 4 + 3] = wall_clock64();
+        } else {
+          a.pv_out[wg] = sv[0];
+          a.pp_out[wg] = sr[0] >= 0 ? sp[0] : (long long)a.N;
+          a.pr_out[wg] = sr[0];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (wg == 0 && tid == 0) {
+    a.st->m_pi = mpi;
+    a.st->sqrt_piv = sq;
+  }
+  return;
+fault:
+  if (tid == 0) a.st->pivot_err = 2;
+}
+
+// the persistent form applies: one rank, the dense rows or the sGDML single-column path, a panel
+// short enough for its pivot row to sit in LDS, and MLFF_PIVCHOL_PERSIST not 0
+static bool persist_grid(int64_t k, int *G_out) {
+  const char *e0 = std::getenv("MLFF_PIVCHOL_PERSIST");  // read per build: 0 = launch sequence
+  if ((e0 != nullptr && std::atoi(e0) == 0) || k > 12288) return false;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+  cus = prop.multiProcessorCount;
+  int per = 0;
+  const size_t shm = sizeof(double) * (size_t)std::max<int64_t>(k, 8);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(k_piv_persist<true>),
+                                                   256, shm) != hipSuccess || per < 1)
+    return false;
+  int G = std::min(64, cus);  // 64 / 128 / 256: 24.1 / 28.3 / 37.7 us per step (configs[1])
+  if (const char *e = std::getenv("MLFF_PIV_G")) G = std::max(1, std::min(cus * per, std::atoi(e)));
+  *G_out = G;
+  return G >= 1;
+}
+
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   hipStream_t s = ctx->stream;
   const int64_t N = ctx->N, nrows = ctx->nrows, blk = ctx->blk;
@@ -500,9 +884,162 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       stamps.push_back(e);
     }
   };
-  stamp();
+  std::vector<int64_t> stamp_col;  // the column each stamp precedes
+  stamp_col.reserve(stamps.capacity());
+  auto stamp_at = [&](int64_t m) {
+    stamp();
+    if (stamp_col.size() < stamps.size()) stamp_col.push_back(m);
+  };
+  // the persistent form (k_piv_persist): one launch per speculative block
+  int Gp = 0;
+  const bool persist = ctx->world == 1 && nrows > 0 && !rbfcols && !ctx->piv_persist_off &&
+                       (ctx->has_matrix || (mfcols && ctx->mf.uvk != nullptr)) &&
+                       persist_grid(k, &Gp);
+  if (persist) {
+    const bool sg = !ctx->has_matrix;
+    const MfData &mf = ctx->mf;
+    long long *pr = nullptr;
+    double *pv2 = nullptr;
+    long long *pp2 = nullptr, *pr2 = nullptr;
+    unsigned long long *slots = nullptr, *flags = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &pr, npart));
+    MLFF_TRY(scratch_alloc(ctx, &pv2, std::max(npart, Gp)));
+    MLFF_TRY(scratch_alloc(ctx, &pp2, std::max(npart, Gp)));
+    MLFF_TRY(scratch_alloc(ctx, &pr2, std::max(npart, Gp)));
+    MLFF_TRY(scratch_alloc(ctx, &slots, (size_t)Gp * 4));
+    MLFF_TRY(scratch_alloc(ctx, &flags, (size_t)Gp));
+    MLFF_HIP(ctx, hipMemsetAsync(slots, 0, sizeof(unsigned long long) * Gp * 4, s));
+    MLFF_HIP(ctx, hipMemsetAsync(flags, 0, sizeof(unsigned long long) * Gp, s));
+    if (npart < Gp) {  // the partial buffers hold G entries
+      MLFF_TRY(scratch_alloc(ctx, &pv, Gp));
+      MLFF_TRY(scratch_alloc(ctx, &pp, Gp));
+      MLFF_TRY(scratch_alloc(ctx, &pr, Gp));
+    }
+    PersistArgs pa{};
+    pa.N = N;
+    pa.nrows = nrows;
+    pa.blk = blk;
+    pa.rows_per = ctx->rows_per;
+    pa.Lt = ctx->T;
+    pa.dwork = ctx->dwork;
+    pa.pivflag = ctx->pivflag;
+    pa.perm = ctx->perm;
+    pa.iperm = iperm;
+    pa.st = ctx->st;
+    pa.K = sg ? nullptr : ctx->K;
+    pa.ld = ctx->ld;
+    pa.sigma = ctx->sigma_K;
+    if (sg) {
+      pa.Rdd = mf.Rdd;
+      pa.M = mf.M;
+      pa.n = mf.n;
+      pa.D = mf.D;
+      pa.i0 = mf.i0;
+      pa.pi = mf.pi_d;
+      pa.piinv = mf.piinv_d;
+      pa.n_perms = mf.n_perms;
+      pa.uvk = mf.uvk;
+      pa.chunks = (3 * mf.n + kColRows - 1) / kColRows;
+      const int64_t n3 = 3 * (int64_t)mf.n;
+      pa.nrw = (int)(((nrows + n3 - 1) / n3) * pa.chunks);  // one rank: row0 = 0, i0 = 0
+    } else {
+      pa.nrw = (int)((nrows + 63) / 64);
+    }
+    pa.part = part;
+    pa.kmax_split = kmax_split;
+    pa.Cspec = Cspec;
+    pa.Gspec = Gspec;
+    pa.mute = -1;
+    pa.trace = nullptr;
+    const bool want_trace = std::getenv("MLFF_PIV_TRACE") != nullptr;
+    if (want_trace) {
+      MLFF_TRY(scratch_alloc(ctx, &pa.trace, (size_t)k * Gp * 4));
+      MLFF_HIP(ctx, hipMemsetAsync(pa.trace, 0, sizeof(unsigned long long) * k * Gp * 4, s));
+    }
+    if (const char *e = std::getenv("MLFF_PIV_MUTE")) pa.mute = std::atoi(e);
+    const size_t shm = sizeof(double) * (size_t)std::max<int64_t>(k, 8);
+    hipLaunchKernelGGL(k_piv_argmax, dim3(np), dim3(256), 0, s, ctx->dwork, ctx->perm, N, (int64_t)0,
+                       ctx->row0, nrows, pv, pp);
+    const double *pin = pv;
+    const long long *ppin = pp, *prin = nullptr;
+    int npc = np;
+    bool flip = false;
+    stamp_at(0);
+    for (int64_t m = 0; m < k;) {
+      int64_t m_end = k;
+      pa.spec_m0 = -1;
+      if (spec) {
+        if (m < kSpecMin) {
+          m_end = std::min<int64_t>(k, kSpecMin);
+        } else {
+          hipLaunchKernelGGL(k_spec_top_part, dim3(kSpecGroups), dim3(256), 0, s, ctx->dwork,
+                             ctx->pivflag, nrows, cv, ci);
+          hipLaunchKernelGGL(k_spec_top_merge, dim3(1), dim3(256), 0, s, (const double *)cv,
+                             (const long long *)ci, Cspec);
+          hipLaunchKernelGGL(k_spec_gather, dim3((unsigned)std::min<int64_t>((m * kSpecC + 255) / 256, 4096)),
+                             dim3(256), 0, s, ctx->T, blk, m, Cspec, Aspec);
+          MLFF_TRY(gemm_splitk(ctx, true, false, kSpecC, blk, m, Aspec, kSpecC, ctx->T, blk, Gspec, blk));
+          pa.spec_m0 = m;
+          m_end = std::min<int64_t>(k, m + kSpecB);
+        }
+      }
+      pa.pv_in = pin;
+      pa.pp_in = ppin;
+      pa.pr_in = prin;
+      pa.npc = npc;
+      pa.pv_out = flip ? pv : pv2;
+      pa.pp_out = flip ? pp : pp2;
+      pa.pr_out = flip ? pr : pr2;
+      pa.slots = slots;
+      pa.flags = flags;
+      pa.m_begin = m;
+      pa.m_end = m_end;
+      if (sg)
+        hipLaunchKernelGGL(k_piv_persist<true>, dim3((unsigned)Gp), dim3(256), shm, s, pa);
+      else
+        hipLaunchKernelGGL(k_piv_persist<false>, dim3((unsigned)Gp), dim3(256), shm, s, pa);
+      MLFF_HIP(ctx, hipGetLastError());
+      pin = pa.pv_out;
+      ppin = pa.pp_out;
+      prin = pa.pr_out;
+      npc = Gp;
+      flip = !flip;
+      m = m_end;
+      stamp_at(m);
+    }
+    if (want_trace) {  // per step: the medians over workgroups of each phase, and the step time
+      std::vector<unsigned long long> tr((size_t)k * Gp * 4);
+      MLFF_HIP(ctx, hipMemcpyAsync(tr.data(), pa.trace, sizeof(unsigned long long) * tr.size(),
+                                   hipMemcpyDeviceToHost, s));
+      MLFF_HIP(ctx, hipStreamSynchronize(s));
+      double acc[4] = {0, 0, 0, 0};
+      int64_t cnt = 0;
+      for (int64_t m = 1; m + 1 < k; ++m) {
+        const unsigned long long *a0 = &tr[(size_t)m * Gp * 4], *a1 = &tr[(size_t)(m + 1) * Gp * 4];
+        if (a0[0] == 0 || a1[0] == 0 || a0[3] == 0) continue;  // launch boundaries
+        std::vector<double> ph[4];
+        for (int g = 0; g < Gp; ++g) {
+          const unsigned long long *e = a0 + 4 * g, *f = a1 + 4 * g;
+          ph[0].push_back(10.0 * (double)(e[1] - e[0]));
+          ph[1].push_back(e[2] > e[1] ? 10.0 * (double)(e[2] - e[1]) : 0.0);
+          ph[2].push_back(10.0 * (double)(e[3] - (e[2] > e[1] ? e[2] : e[1])));
+          ph[3].push_back(10.0 * (double)(f[0] - e[0]));
+        }
+        for (int q = 0; q < 4; ++q) {
+          std::nth_element(ph[q].begin(), ph[q].begin() + Gp / 2, ph[q].end());
+          acc[q] += ph[q][Gp / 2];
+        }
+        ++cnt;
+      }
+      if (cnt > 0)
+        std::fprintf(stderr, "[piv trace] G=%d steps=%lld median ns: winner+stage+miss %.0f, rows %.0f, "
+                     "publish %.0f, step %.0f\n", Gp, (long long)cnt, acc[0] / cnt, acc[1] / cnt,
+                     acc[2] / cnt, acc[3] / cnt);
+    }
+  } else {
+  stamp_at(0);
   for (int64_t m = 0; m < k; ++m) {
-    if (m > 0 && m % kStampEvery == 0) stamp();
+    if (m > 0 && m % kStampEvery == 0) stamp_at(m);
     // candidates of step m: a scan of the positions [m, N) at m = 0 (and on a rank without
     // rows), afterwards the per-workgroup winners k_piv_fin left from step m - 1
     int npc = (int)gcol;
@@ -562,7 +1099,8 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                          ctx->st, 0.0);
     if ((m & 255) == 255) MLFF_HIP(ctx, hipGetLastError());
   }
-  stamp();
+  stamp_at(k);
+  }
   MLFF_HIP(ctx, hipGetLastError());
   int perr = 0;
   MLFF_HIP(ctx, hipMemcpyAsync(&perr, &ctx->st->pivot_err, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -571,15 +1109,21 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                                  hipMemcpyDeviceToHost, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   ctx->piv_col_s.assign((size_t)k, 0.0);
-  if (stamps.size() == (size_t)((k + kStampEvery - 1) / kStampEvery + 1)) {
+  if (stamp_col.size() == stamps.size()) {  // each segment's time split evenly over its columns
     for (size_t g = 0; g + 1 < stamps.size(); ++g) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, stamps[g], stamps[g + 1]);
-      const int64_t c0 = (int64_t)g * kStampEvery, c1 = std::min<int64_t>(c0 + kStampEvery, k);
+      const int64_t c0 = stamp_col[g], c1 = std::min<int64_t>(stamp_col[g + 1], k);
       for (int64_t c = c0; c < c1; ++c) ctx->piv_col_s[c] = 1e-3 * ms / (double)(c1 - c0);
     }
   }
   for (hipEvent_t e : stamps) (void)hipEventDestroy(e);
+  if (perr == 2 && persist) {
+    // a workgroup of the persistent grid waited > 1 s for the others (not co-resident: another
+    // process's kernels hold CUs): this context builds with the launch sequence from now on
+    ctx->piv_persist_off = true;
+    return pivoted_cholesky(ctx, k, index_columns_out);
+  }
   if (perr)
     return set_error(ctx, MLFF_ERR_NOT_PSD,
                      "given matrix is not PSD (pivot <= 0 in pivoted Cholesky)");

@@ -755,7 +755,7 @@ void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double si
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
                              const double *p_full, double *pq_part, double *pp_part,
                              double sigma, double lam, const int *status, hipStream_t s,
-                             PGather pg) {
+                             PGather pg, bool separate_publish) {
   const int64_t ld = (int64_t)world * blk;
   const dim3 grid(kVecGrid);
   double *pw = const_cast<double *>(p_full);  // written only when the p update is fused
@@ -766,11 +766,7 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
                        sp.ticket, status, PGather{}, PqPublish{});
     return;
   }
-  static const bool separate = [] {  // MLFF_PQ_PUBLISH=1: the separate launch (A/B)
-    const char *e = std::getenv("MLFF_PQ_PUBLISH");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  if (!separate) {
+  if (!separate_publish) {  // MLFF_PQ_PUBLISH=1 (ctx->pq_publish): the separate launch (A/B)
     hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (1 << sp.lsub) - 1, (int)sp.nb, rank,
                        sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,

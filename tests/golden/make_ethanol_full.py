@@ -132,13 +132,15 @@ def _solve(job):
             T = woodbury_panel(Lk, LAM)[0]
         elif po in ("qr", "refined"):
             T = accurate_panel(Lk, LAM, po)
+        elif po == "subst":
+            T = subst_panel(Lk, LAM)
         else:
             T = woodbury_gram_order(Lk, LAM, po)
-        mvK = kop_variant(Rd, Rdd, perms, SIG, order)
-        if order == "mf_rows":  # the device's one-pass apply order (rows_apply)
+        if order in ("mf_rows", "mf_rows7"):  # the device's one-pass apply order (rows_apply)
             mvK = kop_variant(Rd, Rdd, perms, SIG, "mf")
-            psolve = rows_apply(T, ROWS_PER_GROUP[k])
+            psolve = rows_apply(T, ROWS_PER_GROUP[k] if order == "mf_rows" else 7)
         else:
+            mvK = kop_variant(Rd, Rdd, perms, SIG, order)
             panel_order = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}[order]
             mvT = make_gemv(T, panel_order)
             mvTt = make_gemv(np.ascontiguousarray(T.T), panel_order)
@@ -146,9 +148,33 @@ def _solve(job):
         x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=tol, maxiter=MAXITER,
                                     psolve=psolve)
     name = order if not po else f"panel_{po}" if po not in ("qr", "refined") else f"{po}_{order}"
+    if po and po not in ("qr", "refined") and order != "mf":
+        name += "_" + order
     print(f"k={k} tol={tol:g} {name:10s} iters {it} info {info} ({time.time() - t0:.0f} s)",
           flush=True)
     return job, x, info, tr, it
+
+
+def subst_panel(L, lam):
+    """The one-step Woodbury panel T = chol(lam I + L^T L)^-1 L^T (iterative_cholesky.py:141-143)
+    in another evaluation order: the Gram matrix in 64-row chunks added exactly, the Cholesky
+    factor column by column (left-looking dot products), T row by row by forward substitution
+    (each row one dot product over the rows before it) -- the same formula with the factorisation's
+    and the triangular solve's sums ordered unlike LAPACK's blocked dpotrf / dtrsm."""
+    from make_nanotube_full import gram_in_order
+
+    k = L.shape[1]
+    A = gram_in_order(L, "chunk64dd") + lam * np.eye(k)
+    L2 = np.zeros((k, k))
+    for j in range(k):
+        v = A[j:, j] - L2[j:, :j] @ L2[j, :j]
+        L2[j, j] = np.sqrt(v[0])
+        L2[j + 1:, j] = v[1:] / L2[j, j]
+    Lt = np.ascontiguousarray(L.T)
+    T = np.empty_like(Lt)
+    for j in range(k):
+        T[j] = (Lt[j] - L2[j, :j] @ T[:j]) / L2[j, j]
+    return T
 
 
 def band_of(runs, ref_name, tol):
@@ -202,6 +228,77 @@ def merge_rows(cache, procs):
         print(key, "accurate", json.dumps({q: b[q] for q in ("ref_iters", "band_iters",
                                                             "band_crossing", "band_rel_dalpha")}),
               flush=True)
+    (GOLDEN / "ethanol_n15741_band.json").write_text(json.dumps(out, indent=1, sort_keys=True))
+
+
+def _factor(cache):
+    """L of the rank-1264 pivoted Cholesky (from --cache when present), pivots checked against
+    the committed fixture's."""
+    R, Rd, Rdd, perms, y = problem()
+    if cache is not None and Path(cache).exists():
+        L = np.load(cache, allow_pickle=False)["L"]
+    else:
+        mv0 = kop_variant(Rd, Rdd, perms, SIG, "mf")
+
+        def get_col(i):  # (-K_op) e_i (iterative_cholesky.py:152-156)
+            e = np.zeros(y.size)
+            e[i] = 1.0
+            return -mv0(e) + LAM * e
+
+        L, piv, piv_val, gap = pivoted_cholesky_logged(get_col, -kernel_diag(Rd, Rdd, perms, SIG),
+                                                       max(K_RANKS))
+        with np.load(GOLDEN / "ethanol_n15741.npz", allow_pickle=False) as f:
+            assert np.array_equal(piv[:max(K_RANKS)], f["index_columns"])
+        if cache is not None:
+            np.savez(cache, L=L, piv=piv, piv_val=piv_val, gap=gap)
+    return Rd, Rdd, perms, y, L
+
+
+GRAM_JOBS_1 = [("mf", "chunk64dd"), ("mf", "pair"), ("mf", "ld")]
+# the round's second pass: the one-step panel with the device's apply order (7 rows per group,
+# lr_rows_per_wg) for three Gram orders, and the substitution-ordered factorisation / solve
+GRAM_JOBS_2 = [("mf_rows7", "blas"), ("mf_rows7", "chunk64dd"), ("mf_rows7", "ld"),
+               ("mf", "subst")]
+
+
+def merge_gram(cache, procs, gram_jobs=GRAM_JOBS_1):
+    """--gram (round 6): the reference's one-step panel (iterative_cholesky.py:141-143) with its
+    Gram matrix L^T L in three more summation orders (make_nanotube_full.GRAM_ORDERS: 64-row
+    chunks added exactly, pairwise, extended precision) merged into the one-step LAPACK bands at
+    both ranks and both tolerances.  DESIGN.md 2 showed that this rounding, not the operator's,
+    sets the one-step count at cond([L; sqrt(lam) I]) ~ 6e3; the band of rounds 5 sampled only
+    BLAS / reversed / 8 slabs."""
+    Rd, Rdd, perms, y, L = _factor(cache)
+    _G.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, L=L)
+    out = json.loads((GOLDEN / "ethanol_n15741_band.json").read_text())
+    with np.load(GOLDEN / "ethanol_n15741.npz", allow_pickle=False) as f:
+        arrays = {name: f[name] for name in f.files}
+    jobs = [(k, order, po, tol) for k in K_RANKS for tol in TOLS for order, po in gram_jobs]
+    jobs.sort(key=lambda j: (j[3] > 1e-5, -j[0]))
+    with mp.get_context("fork").Pool(procs) as pool:
+        results = pool.map(_solve, jobs, chunksize=1)
+    for (k, order, po, tol), x, info, tr, it in results:
+        key = f"k{k}_tol{tol:g}"
+        b = out["bands"][key]
+        x0 = -arrays[f"{key}_alphas"]
+        tr0, it0 = arrays[f"{key}_trace"], int(arrays[f"{key}_iters"])
+        top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+        cr0, cr = half_decade_crossings(tr0[1:], top), half_decade_crossings(tr[1:], top)
+        dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+        vname = f"panel_{po}" if order == "mf" else f"panel_{po}_rows7"
+        b["variants"][vname] = {
+            "iters": int(it), "info": int(info), "d_iters": int(it - it0),
+            "max_d_crossing": int(max(dc) if dc else 0),
+            "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+        v = [e for name, e in b["variants"].items()]
+        b["band_iters"] = int(max(abs(e["d_iters"]) for e in v))
+        b["band_crossing"] = int(max(e["max_d_crossing"] for e in v))
+        b["band_rel_dalpha"] = float(max(e["rel_dalpha"] for e in v))
+        xa = -arrays[f"{key}_accurate_alphas"]
+        b["variants"][vname]["accurate_rel_dalpha"] = float(
+            np.linalg.norm(x - xa) / np.linalg.norm(xa))
+        print(key, "one-step", vname, it, json.dumps({q: b[q] for q in (
+            "ref_iters", "band_iters", "band_crossing", "band_rel_dalpha")}), flush=True)
     (GOLDEN / "ethanol_n15741_band.json").write_text(json.dumps(out, indent=1, sort_keys=True))
 
 
@@ -288,8 +385,16 @@ if __name__ == "__main__":
     ap.add_argument("--procs", type=int, default=int(os.environ.get("PROCS", "8")))
     ap.add_argument("--rows", action="store_true",
                     help="merge the device-apply-order accurate solves into the committed fixture")
+    ap.add_argument("--gram2", action="store_true",
+                    help="merge the one-step apply-order / substitution variants into the fixture")
+    ap.add_argument("--gram", action="store_true",
+                    help="merge one-step solves with more Gram summation orders into the fixture")
     a = ap.parse_args()
-    if a.rows:
+    if a.gram2:
+        merge_gram(a.cache, a.procs, GRAM_JOBS_2)
+    elif a.gram:
+        merge_gram(a.cache, a.procs)
+    elif a.rows:
         merge_rows(a.cache, a.procs)
     else:
         main(a.cache, a.procs)

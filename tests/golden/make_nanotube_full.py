@@ -99,27 +99,62 @@ def pivoted_cholesky_logged(get_col, diagonal, max_rank):
     return L, index_columns, piv_val, gap
 
 
-PANEL_ORDERS = ["rev", "blk8", "inverse", "noise", "rownoise"]
+PANEL_ORDERS = ["rev", "blk8", "chunk64dd", "pair", "ld", "inverse", "noise", "rownoise"]
+# the Gram-matrix summation orders of the reference's one-step formula (round 6): the count of
+# the one-step panel at an ill-conditioned [L; sqrt(lam) I] is set by how L^T L is rounded
+# (DESIGN.md 2), so its band samples that rounding -- BLAS, reversed, 8 row slabs, 64-row
+# chunks added exactly, pairwise, extended-precision products and sums
+GRAM_ORDERS = ("rev", "blk8", "chunk64dd", "pair", "ld")
+
+
+def _dd_accumulate(parts):
+    """fl(sum of fp64 matrices) with every addition exact (TwoSum into a double-double
+    accumulator, rounded once): the outer sum of a blocked Gram as k_gram_mfma_dd forms it."""
+    hi = np.zeros_like(parts[0])
+    lo = np.zeros_like(parts[0])
+    for p in parts:
+        s = hi + p
+        bp = s - hi
+        lo += (hi - (s - bp)) + (p - bp)
+        hi = s
+    return hi + lo
+
+
+def gram_in_order(L, order):
+    """L^T L (the Woodbury Gram matrix, iterative_cholesky.py:141) in a given summation order
+    over the rows of L."""
+    if order == "rev":
+        Lr = np.ascontiguousarray(L[::-1])
+        return Lr.T @ Lr
+    if order == "blk8":
+        return sum(L[b].T @ L[b] for b in np.array_split(np.arange(L.shape[0]), 8))
+    if order == "chunk64dd":  # 64-row chunks in fp64, the chunk partials added exactly
+        return _dd_accumulate([L[a:a + 64].T @ L[a:a + 64] for a in range(0, L.shape[0], 64)])
+    if order == "pair":  # pairwise over row halves down to 128-row leaves
+        def pw(A):
+            if A.shape[0] <= 128:
+                return A.T @ A
+            h = A.shape[0] // 2
+            return pw(A[:h]) + pw(A[h:])
+        return pw(L)
+    if order == "ld":  # products and sums with a 64-bit significand, rounded once
+        Ll = L.astype(np.longdouble)
+        return (Ll.T @ Ll).astype(np.float64)
+    return L.T @ L
 
 
 def woodbury_gram_order(L, lam, order):
     """oracle.precon.woodbury_panel (iterative_cholesky.py:141-143) rounded another way:
-    'rev' / 'blk8': the Gram matrix L^T L summed with the rows of L reversed / in 8 row blocks;
-    'inverse': T = inv(L2) L^T (the triangular inverse, then one GEMM) instead of the
-    triangular solve; 'noise' / 'rownoise': the LAPACK panel with independent relative
-    perturbations of 2e-15 per entry / with 2e-15 (E T), E a k x k Gaussian (a perturbed L2).
-    The PCG at lam = 1e-10 is sensitive to how the panel is rounded (scripts/dev/
+    'rev' / 'blk8' / 'chunk64dd' / 'pair' / 'ld': the Gram matrix L^T L in another summation
+    order (gram_in_order); 'inverse': T = inv(L2) L^T (the triangular inverse, then one GEMM)
+    instead of the triangular solve; 'noise' / 'rownoise': the LAPACK panel with independent
+    relative perturbations of 2e-15 per entry / with 2e-15 (E T), E a k x k Gaussian (a perturbed
+    L2).  The PCG at lam = 1e-10 is sensitive to how the panel is rounded (scripts/dev/
     diag_config1[b,c].py): LAPACK-built panels take 364-366 iterations, the others 552-577."""
     import scipy.linalg
 
     k = L.shape[1]
-    if order == "rev":
-        Lr = np.ascontiguousarray(L[::-1])
-        G = Lr.T @ Lr
-    elif order == "blk8":
-        G = sum(L[b].T @ L[b] for b in np.array_split(np.arange(L.shape[0]), 8))
-    else:
-        G = L.T @ L
+    G = gram_in_order(L, order if order in GRAM_ORDERS else "blas")
     L2 = scipy.linalg.cholesky(lam * np.eye(k) + G, lower=True)
     if order == "inverse":
         return np.tril(scipy.linalg.solve_triangular(L2, np.eye(k), lower=True)) @ L.T
@@ -222,6 +257,87 @@ def accurate(cache, procs=5):
                                                       "band_rel_dalpha")}), flush=True)
 
 
+K4_RANK = 1024   # BASELINE configs[4]: the same nanotube, rank-1024 pivoted Cholesky
+K4_TOLS = (1e-4, 1e-6)
+
+
+def _k4_solve(job):
+    """(operator order, Gram order, tol) -> the rank-1024 Woodbury PCG solve (iterative_cholesky.py:
+    135-150, iterative_solver.py:995-1009) on the oracle's matrix-free operator."""
+    import threadpoolctl
+
+    order, po, tol = job
+    Rd, Rdd, perms, y, L = _A["Rd"], _A["Rdd"], _A["perms"], _A["y"], _A["L"]
+    t0 = time.time()
+    with threadpoolctl.threadpool_limits(limits=1, user_api="blas"):
+        T = woodbury_gram_order(L, LAM, po) if po else woodbury_panel(L, LAM)[0]
+        mvK = kop_variant(Rd, Rdd, perms, SIG, order)
+        pord = {"mf": "blas", "mf_rev": "rev", "mf_split": "blk7"}[order]
+        mvT, mvTt = make_gemv(T, pord), make_gemv(np.ascontiguousarray(T.T), pord)
+        x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=tol, maxiter=5 * y.size,
+                                    psolve=lambda r: (r - mvTt(mvT(r))) / LAM)
+    name = order if not po else f"panel_{po}"
+    print(f"k={K4_RANK} tol={tol:g} {name:16s} iters {it} info {info} ({time.time() - t0:.0f} s)",
+          flush=True)
+    return job, x, info, tr, it
+
+
+def configs4(cache, procs=8):
+    """--configs4 (needs --cache of a full run; round 6): BASELINE configs[4]'s solve pinned.  The
+    rank-1024 factor is the first 1024 columns of the rank-2701 one (the greedy pivot sequence
+    does not depend on max_rank; its pivots are the committed index_columns[:1024]).  Woodbury
+    panel and PCG to 1e-4 and 1e-6 in three operator / apply orders and five Gram orders
+    (GRAM_ORDERS): nanotube_n15540_k1024.npz (reference 'mf' trace, alpha, iters per tol) and
+    nanotube_n15540_k1024_band.json (the band per tol)."""
+    import multiprocessing as mp
+
+    R, Rd, Rdd, perms, y = problem()
+    c = np.load(cache, allow_pickle=False)
+    with np.load(GOLDEN / "nanotube_n15540.npz", allow_pickle=False) as f:
+        assert np.array_equal(c["piv"][:K4_RANK], f["index_columns"][:K4_RANK])
+    _A.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, L=np.ascontiguousarray(c["L"][:, :K4_RANK]))
+    del c
+    jobs = [(o, "", tol) for tol in K4_TOLS for o in ("mf", "mf_rev", "mf_split")]
+    jobs += [("mf", po, tol) for tol in K4_TOLS for po in GRAM_ORDERS]
+    jobs.sort(key=lambda j: j[2] > 1e-5)  # the long solves first
+    with mp.get_context("fork").Pool(procs) as pool:
+        results = pool.map(_k4_solve, jobs, chunksize=1)
+    arrays = {"R": R, "y": y, "index_columns": _A_piv(cache)}
+    bands = {"n": int(y.size), "k": K4_RANK, "ref_order": "mf", "bands": {}}
+    for tol in K4_TOLS:
+        runs = {(o if not po else f"panel_{po}"): (x, info, tr, it)
+                for (o, po, t), x, info, tr, it in results if t == tol}
+        x0, info0, tr0, it0 = runs["mf"]
+        top = float(np.log10(np.minimum.accumulate(tr0[1:])[0]))
+        cr0 = half_decade_crossings(tr0[1:], top)
+        variants = {}
+        for name, (x, info, tr, it) in runs.items():
+            cr = half_decade_crossings(tr[1:], top)
+            dc = [abs(cr[q] - cr0[q]) for q in cr0 if q in cr]
+            variants[name] = {"iters": int(it), "info": int(info), "d_iters": int(it - it0),
+                              "max_d_crossing": int(max(dc) if dc else 0),
+                              "rel_dalpha": float(np.linalg.norm(x - x0) / np.linalg.norm(x0))}
+        v = variants.values()
+        key = f"tol{tol:g}"
+        bands["bands"][key] = {"tol": tol, "ref_order": "mf", "ref_iters": int(it0),
+                               "variants": variants,
+                               "band_iters": int(max(abs(e["d_iters"]) for e in v)),
+                               "band_crossing": int(max(e["max_d_crossing"] for e in v)),
+                               "band_rel_dalpha": float(max(e["rel_dalpha"] for e in v))}
+        arrays.update({f"{key}_trace": tr0, f"{key}_alphas": -x0, f"{key}_iters": np.int64(it0),
+                       f"{key}_info": np.int64(info0)})
+        print(key, json.dumps({q: bands["bands"][key][q] for q in (
+            "ref_iters", "band_iters", "band_crossing", "band_rel_dalpha")}),
+              json.dumps({o: e["iters"] for o, e in variants.items()}), flush=True)
+    np.savez_compressed(GOLDEN / "nanotube_n15540_k1024.npz", **arrays)
+    (GOLDEN / "nanotube_n15540_k1024_band.json").write_text(json.dumps(bands, indent=1,
+                                                                       sort_keys=True))
+
+
+def _A_piv(cache):
+    return np.load(cache, allow_pickle=False)["piv"][:K4_RANK]
+
+
 def main(cache=None, panel_orders=()):
     """cache: .npz path (outside the repository: 336 MB) holding L and the pivot log, written
     on the first run and read by later ones; panel_orders: Gram-matrix orders of the Woodbury
@@ -297,8 +413,13 @@ if __name__ == "__main__":
                     help="the accurate-panel band only (needs --cache from a full run)")
     ap.add_argument("--compute-cache", action="store_true",
                     help="compute the factor into --cache (no solves)")
+    ap.add_argument("--configs4", action="store_true",
+                    help="the rank-1024 (configs[4]) solve band (needs --cache from a full run)")
+    ap.add_argument("--procs", type=int, default=8)
     a = ap.parse_args()
-    if a.compute_cache:
+    if a.configs4:
+        configs4(a.cache, a.procs)
+    elif a.compute_cache:
         _, Rd, Rdd, perms, y = problem()
         mv0 = kop_variant(Rd, Rdd, perms, SIG, "mf")
 

@@ -419,3 +419,35 @@ def test_cluster_apply_fault_mid_chunk(sg, monkeypatch):
                       mode="chaotic", x_tol=1e-6)
     assert_pcg_parity(res.iters, res.trace[1:], res.x, two.iters, two.trace[1:], two.x,
                       mode="chaotic", x_tol=1e-6)
+
+
+@pytest.mark.parametrize("steps", ["1", "2", "3"])
+def test_woodbury_refine_steps(sg, monkeypatch, steps):
+    """MLFF_WB_REFINE=<steps> (CholeskyQR2 and beyond): every refined panel T
+    represents the same preconditioner as the exact formula -- T^T T = L (lam I + L^T L)^-1 L^T,
+    evaluated on the host as Q1 Q1^T from a Householder QR of [L; sqrt(lam) I]
+    (iterative_cholesky.py:141-148) -- to rounding, and steps >= 2 (the accumulated-inverse
+    branch, Li <- C^-1 Li) agrees with the one-refinement panel to rounding."""
+    n, k, lam = 1500, 96, 1e-6
+    rng = np.random.default_rng(7)
+    L = rng.standard_normal((n, k)) * np.logspace(0, -3, k)   # cond([L; sqrt(lam) I]) ~ 1e3
+    A = np.vstack([L, np.sqrt(lam) * np.eye(k)])
+    Q1 = np.linalg.qr(A, mode="reduced")[0][:n]
+    P_ref = Q1 @ Q1.T
+    panels = {}
+    for st in ("1", steps):
+        monkeypatch.setenv("MLFF_WB_REFINE", st)
+        with sg.KernelSolver(n) as s:
+            X, _ = _rbf(n)
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, lam)
+            s.precon_lowrank(np.ascontiguousarray(L.T))
+            panels[st] = s.precon_panel()
+    for st, T in panels.items():
+        err = np.abs(T.T @ T - P_ref).max()
+        assert err <= 1e-12, (st, err)
+        # the orthogonality the refinement restores: T T^T + lam L2^-1 L2^-T = I implies
+        # T T^T <= I with the rest lam-sized
+        assert np.linalg.eigvalsh(T @ T.T).max() <= 1.0 + 1e-12, st
+    d = np.abs(panels[steps].T @ panels[steps] - panels["1"].T @ panels["1"]).max()
+    assert d <= 1e-12, d

@@ -152,6 +152,24 @@ def test_sharded_fused_p_update_bitwise(world, precon, monkeypatch):
         np.testing.assert_array_equal(a["x"], b["x"])
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,precon", [(2, "nystrom"), (3, "pivchol"), (8, "nystrom")])
+def test_sharded_pq_publish_folded_bitwise(world, precon, monkeypatch):
+    """The p.q share publish folded into k_sym_reduce_w's last-arriving workgroup (default)
+    against the separate k_pq_publish launch (MLFF_PQ_PUBLISH=1, read at context creation): the
+    same sums in the same order, so the shares, iterates, residual curve and stop decisions are
+    bit-identical."""
+    n = 1003
+    out = {}
+    for sep in ("1", "0"):
+        monkeypatch.setenv("MLFF_PQ_PUBLISH", sep)
+        out[sep] = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    for a, b in zip(out["1"], out["0"]):
+        assert a["iters"] == b["iters"] and a["info"] == b["info"] == 0
+        np.testing.assert_array_equal(a["trace"], b["trace"])
+        np.testing.assert_array_equal(a["x"], b["x"])
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world,precon,n", [(2, "nystrom", 1003), (3, "pivchol", 1003),
                                             (8, "nystrom", 1003), (2, "nystrom", 9000),
