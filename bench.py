@@ -507,9 +507,9 @@ def sgdml_parity(workload, n, k, res):
     fx = json.loads((g / f"{name}_band.json").read_text())
     out = {"source": f"tests/golden/{name}_band.json"}
     if "bands" in fx:
-        # the default (re-orthogonalised) Woodbury panel against the oracle's accurate evaluations
-        # of the formula, the one-step panel (MLFF_WB_REFINE=0) against its one-step LAPACK solves
-        refined = os.environ.get("MLFF_WB_REFINE", "1") != "0"
+        # the default (one-step, the reference's formula) Woodbury panel against the oracle's
+        # one-step solves; the re-orthogonalised panel (MLFF_WB_REFINE=1) against its accurate ones
+        refined = os.environ.get("MLFF_WB_REFINE", "0") != "0"
         out["panel"] = "refined (accurate band)" if refined else "one-step (LAPACK band)"
         cases = {}
         for t in (1e-4, 1e-6):

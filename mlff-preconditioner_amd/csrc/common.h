@@ -354,7 +354,7 @@ struct mlff_ctx {
   // Woodbury panel re-orthogonalised by a second CholeskyQR step (MLFF_WB_REFINE, woodbury_inplace;
   // configs[1] at full size: 571 -> 366 iterations, the oracle's 367) and the same for the
   // Nystrom panel (MLFF_NYS_REFINE)
-  int wb_refine = 1;  // re-orthogonalisation steps (MLFF_WB_REFINE=0 / 1 / 2 ...)
+  int wb_refine = 0;  // re-orthogonalisation steps (MLFF_WB_REFINE=1 / 2 ...; 0: the reference's one-step panel)
   // the Woodbury Gram matrices L^T L (and the refinement's T T^T): 0 the fp64 matrix-core GEMM,
   // 1 chunked double-double on the matrix cores, 2 exact products in double-double
   // (MLFF_WB_GRAM; kernels_dd.hip gram_wide_dd)

@@ -562,7 +562,9 @@ __device__ __forceinline__ bool persist_wait(unsigned long long *g, int count, i
       for (int q = 0; q < per; ++q) {
         vals[q] = __hip_atomic_load(g + (int64_t)t * per + q, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
-        ok = ok && (unsigned)(vals[q] >> 32) == tag;
+        // tags only grow within a build: a workgroup already past this point may have
+        // published a later one
+        ok = ok && (unsigned)(vals[q] >> 32) >= tag;
       }
       if (ok) break;
       if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
@@ -585,26 +587,97 @@ __device__ __forceinline__ void persist_publish(unsigned long long *g, int per, 
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// argmax over the workgroup of (value, position, row, source) under better()'s strict total order
+// (so every workgroup reducing the same candidates picks the same one); result in every thread
+__device__ __forceinline__ void wg_argmax(double &v, long long &p, long long &r, int &src,
+                                          double *sv, long long *sp, long long *sr, int *ss) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(v, o, 64);
+    const long long p2 = __shfl_xor(p, o, 64), r2 = __shfl_xor(r, o, 64);
+    const int s2 = __shfl_xor(src, o, 64);
+    if (better(v2, p2, v, p)) {
+      v = v2;
+      p = p2;
+      r = r2;
+      src = s2;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sv[w] = v;
+    sp[w] = p;
+    sr[w] = r;
+    ss[w] = src;
+  }
+  __syncthreads();
+  v = sv[0];
+  p = sp[0];
+  r = sr[0];
+  src = ss[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (better(sv[q], sp[q], v, p)) {
+      v = sv[q];
+      p = sp[q];
+      r = sr[q];
+      src = ss[q];
+    }
+}
+
+constexpr int kSlot = 4 + 2 * kSpecB;  // granules per workgroup slot: header + L segment
+
 template <bool SG>
 __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
-  extern __shared__ double t_sh[];  // the pivot row L[c, m_pi] of the step's Schur range
-  __shared__ double sv[256];
-  __shared__ long long sp[256], sr[256];
+  extern __shared__ double t_sh[];  // the pivot row L[c, m_pi] over the step's Schur range
+  __shared__ double sv[4];
+  __shared__ long long sp[4], sr[4];
+  __shared__ int ss[4];
   __shared__ long long s_C[kSpecC];
   __shared__ int s_bail;
   const int G = (int)gridDim.x, wg = (int)blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   if (tid == 0) s_bail = 0;
-  if (a.spec_m0 >= 0 && tid < kSpecC) s_C[tid] = a.Cspec[tid];
-  __syncthreads();
+  if (a.st->pivot_err == 2) return;  // an earlier launch of this build timed out: host falls back
+  const bool spec = a.spec_m0 >= 0;
+  if (spec && tid < kSpecC) s_C[tid] = a.Cspec[tid];
   const int64_t ldl = a.blk;
+  // ---- this thread's row (one row wave per wave: nrw <= 4 G) and its state in registers
+  const int r = wg + G * w;
+  int64_t i = -1;
+  bool act = false;
+  if (r < a.nrw) {
+    if (SG) {
+      const int n3 = 3 * a.n, t = (r % a.chunks) * kColRows + lane;
+      i = (int64_t)(r / a.chunks) * n3 + t;
+      act = t < n3 && i < a.nrows;
+    } else {
+      i = (int64_t)r * 64 + lane;
+      act = i < a.nrows;
+    }
+  }
+  bool piv = true;
+  double dw = 0.0;
+  long long ip = 0;
+  if (act) {
+    piv = a.pivflag[i] != 0;
+    dw = a.dwork[i];
+    ip = a.iperm[i];
+  }
+  double seg[kSpecB];  // L[spec_m0 + u, i] of this block's steps
+#pragma unroll
+  for (int u = 0; u < kSpecB; ++u) seg[u] = 0.0;
+  __syncthreads();
   long long mpi = -1;
   double sq = 0.0;
   for (int64_t m = a.m_begin; m < a.m_end; ++m) {
-    // ---- the winner of step m from the partials of step m - 1 (the same in every workgroup:
-    // a strict total order, value descending then position ascending)
+    const int S = spec ? (int)(m - a.spec_m0) : 0;  // segment length of the step-(m - 1) slots
+    // ---- the winner of step m from the partials of step m - 1
     double bv = -INFINITY;
     long long bp = LLONG_MAX, br = -1;
+    int src = -1;
+    unsigned long long g[4];
     if (m == a.m_begin) {
       for (int t = tid; t < a.npc; t += 256)
         if (better(a.pv_in[t], a.pp_in[t], bv, bp)) {
@@ -613,38 +686,41 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
           br = a.pr_in != nullptr ? a.pr_in[t] : bp;
         }
     } else {
-      unsigned long long g[4];
-      if (!persist_wait(a.slots, G, 4, (unsigned)m, g, &s_bail)) goto fault;  // tag of step m - 1
+      // thread t < G: slot t's header (the winner's L segment is read after the reduction)
       if (tid < G) {
+        const unsigned tag = (unsigned)m;  // published at step m - 1
+        // two slot buffers by step parity: a workgroup one step ahead overwrites the other one
+        unsigned long long *gs = a.slots + ((int64_t)(m & 1) * G + tid) * kSlot;
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            g[q] = __hip_atomic_load(gs + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          bool ok = true;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ok = ok && (unsigned)(g[q] >> 32) == tag;
+          if (ok) break;
+          if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
+            s_bail = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
         bv = __builtin_bit_cast(double, (g[1] << 32) | (g[0] & 0xffffffffull));
         bp = (long long)(unsigned)(g[2] & 0xffffffffull);
         br = (long long)(int)(unsigned)(g[3] & 0xffffffffull);
         if (br < 0) bp = LLONG_MAX;  // an empty partial
+        src = tid;
       }
     }
-    if (a.trace != nullptr && tid == 0) a.trace[(m * G + wg) * 4 + 0] = wall_clock64();
-    sv[tid] = bv;
-    sp[tid] = bp;
-    sr[tid] = br;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o && better(sv[tid + o], sp[tid + o], sv[tid], sp[tid])) {
-        sv[tid] = sv[tid + o];
-        sp[tid] = sp[tid + o];
-        sr[tid] = sr[tid + o];
-      }
-      __syncthreads();
-    }
-    bv = sv[0];
-    bp = sp[0];
-    br = sr[0];
-    __syncthreads();
+    wg_argmax(bv, bp, br, src, sv, sp, sr, ss);
+    if (s_bail) goto fault;
     const bool valid = bp >= m && bp < (long long)a.N && bv == bv && bv > -INFINITY && br >= 0;
     mpi = valid ? br : -1;
     sq = valid ? sqrt(bv) : 0.0;
     if (wg == 0 && tid == 0 && (!valid || !(bv > 0.0))) a.st->pivot_err = 1;
     int hit = -1;
-    if (a.spec_m0 >= 0 && mpi >= 0)
+    if (spec && mpi >= 0)
       for (int j = 0; j < kSpecC; ++j)
         if (s_C[j] == mpi) {
           hit = j;
@@ -652,136 +728,174 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
         }
     const int ks = m > 0 ? min(a.kmax_split, ksplit_of(m, a.blk)) : 0;
     const int64_t kslice = ks > 0 ? (m + ks - 1) / ks : 1;
-    const int64_t c_lo = hit >= 0 ? a.spec_m0 : 0;
-    if (mpi >= 0)
-      for (int64_t c = c_lo + tid; c < m; c += 256) t_sh[c - c_lo] = a.Lt[c * ldl + mpi];
-    __syncthreads();
-    // ---- a miss: k_colgemv_part's split-K slices over [0, m) by the whole grid
-    if (mpi >= 0 && hit < 0 && ks > 0) {
+    if (hit >= 0) {
+      // the pivot row over [spec_m0, m): the segment the winner's workgroup published beside its
+      // header (tagged granules: polled, normally already there)
+      if (tid < S && src >= 0) {
+        unsigned long long *gq = a.slots + ((int64_t)(m & 1) * G + src) * kSlot + 4 + 2 * tid;
+        const unsigned long long t0 = wall_clock64();
+        unsigned long long lo, hi;
+        for (;;) {
+          lo = __hip_atomic_load(gq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi = __hip_atomic_load(gq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((unsigned)(lo >> 32) == (unsigned)m && (unsigned)(hi >> 32) == (unsigned)m) break;
+          if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
+            s_bail = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        t_sh[tid] = __builtin_bit_cast(double, (hi << 32) | (lo & 0xffffffffull));
+      }
+      __syncthreads();
+      if (s_bail) goto fault;
+    } else if (mpi >= 0 && ks > 0) {
+      // a miss: every L row so far is written back and visible (fenced arrival), the whole
+      // pivot row is staged, and the grid runs k_colgemv_part's split-K slices over [0, m)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned zero = 0;
+        persist_publish(a.flags + wg, 1, (unsigned)(2 * m + 1), &zero);
+      }
+      unsigned long long g1[1];
+      if (!persist_wait(a.flags, G, 1, (unsigned)(2 * m + 1), g1, &s_bail)) goto fault;
+      for (int64_t c = tid; c < m; c += 256) t_sh[c] = a.Lt[c * ldl + mpi];
+      __syncthreads();
       const int64_t nbx = (a.blk / 2 + 255) / 256, nvb = nbx * ks, ld2 = a.blk / 2;
       for (int64_t vb = wg; vb < nvb; vb += G) {
         const int64_t bx = vb % nbx, by = vb / nbx;
         const int64_t j0 = by * kslice, j1 = j0 + kslice < m ? j0 + kslice : m;
         const int64_t c2 = bx * 256 + tid;
-        if (2 * c2 < a.blk && j0 < j1) {
-          const pd2 acc = persist_slice(reinterpret_cast<const pd2 *>(a.Lt) + c2, ld2, j0, j1,
-                                        t_sh + j0);
+        if (2 * c2 < a.blk) {
+          pd2 acc = {0.0, 0.0};
+          if (j0 < j1)
+            acc = persist_slice(reinterpret_cast<const pd2 *>(a.Lt) + c2, ld2, j0, j1, t_sh + j0);
           reinterpret_cast<pd2 *>(a.part + by * a.blk)[c2] = acc;
-        } else if (2 * c2 < a.blk) {
-          reinterpret_cast<pd2 *>(a.part + by * a.blk)[c2] = pd2{0.0, 0.0};
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       __syncthreads();
       if (tid == 0) {
         const unsigned zero = 0;
-        persist_publish(a.flags + wg, 1, (unsigned)m + 1, &zero);
+        persist_publish(a.flags + wg, 1, (unsigned)(2 * m + 2), &zero);
       }
-      unsigned long long g1[1];
-      if (!persist_wait(a.flags, G, 1, (unsigned)m + 1, g1, &s_bail)) goto fault;
+      if (!persist_wait(a.flags, G, 1, (unsigned)(2 * m + 2), g1, &s_bail)) goto fault;
     }
-    // ---- rows: column entry, Schur sum, L[m, i], residual diagonal, partial argmax
     if (a.trace != nullptr && tid == 0) a.trace[(m * G + wg) * 4 + 1] = wall_clock64();
+    // ---- rows: column entry, Schur sum, L[m, i], residual diagonal, partial argmax
     {
+      double col = 0.0;
+      if (SG) {
+        if (r < a.nrw && mpi >= 0) {  // wave-uniform: the column code is a wave sum
+          bool a2;
+          int64_t i2;
+          col = a.sigma * sgdml_col_acc(a.Rdd, a.M, a.n, a.D, a.i0, a.pi, a.piinv, a.n_perms,
+                                        a.uvk, 0, a.nrows, mpi, r / a.chunks,
+                                        (r % a.chunks) * kColRows, lane, a2, i2);
+        }
+      } else if (act && mpi >= 0) {
+        const int64_t pos = (mpi / a.rows_per) * a.blk + (mpi % a.rows_per);
+        col = a.sigma * a.K[i * a.ld + pos];
+      }
       double cbv = -INFINITY;
       long long cbp = (long long)a.N, cbr = -1;
-      const int64_t pos = mpi >= 0 ? (mpi / a.rows_per) * a.blk + (mpi % a.rows_per) : 0;
-      for (int r = wg + G * w; r < a.nrw; r += 4 * G) {
-        bool act;
-        int64_t i;
-        double col = 0.0;
-        if (SG) {
-          double acc = 0.0;
-          if (mpi >= 0)
-            acc = sgdml_col_acc(a.Rdd, a.M, a.n, a.D, a.i0, a.pi, a.piinv, a.n_perms, a.uvk, 0,
-                                a.nrows, mpi, r / a.chunks, (r % a.chunks) * kColRows, lane, act, i);
-          else {
-            act = false;
-            i = 0;
-          }
-          col = a.sigma * acc;
-        } else {
-          i = (int64_t)r * 64 + lane;
-          act = i < a.nrows;
-          if (act && mpi >= 0) col = a.sigma * a.K[i * a.ld + pos];
-        }
-        if (!act || mpi < 0) continue;
+      if (act && mpi >= 0) {
+        const int u_m = S;  // this step's index in the segment
+        // (perm, the inverse of iperm, is written once after the build: two rows' owners on
+        // different XCDs would write the same perm entry at different steps, and without a
+        // fence on a hit step nothing orders the two write-backs)
         if (i == mpi) {  // k_piv_finalize's writes for the pivot row
           a.Lt[m * ldl + i] = sq;
-          a.pivflag[i] = 1;
-          a.iperm[i] = m;
-          a.perm[m] = i;
-          continue;
-        }
-        if (a.pivflag[i]) continue;
-        long long pos_i = a.iperm[i];
-        if (pos_i == m) {  // the row the swap moves from position m to bp
-          pos_i = bp;
-          a.iperm[i] = bp;
-          a.perm[bp] = i;
-        }
-        double s0 = 0.0;
-        if (hit >= 0) {  // the slices' parts from spec_m0 on, in slice order, then the G row
-          for (int64_t z = c_lo / kslice; z < ks; ++z) {
-            int64_t j0 = z * kslice;
-            const int64_t j1 = j0 + kslice < m ? j0 + kslice : m;
-            if (j0 < a.spec_m0) j0 = a.spec_m0 < j1 ? a.spec_m0 : j1;
-            if (j0 >= j1) continue;
-            s0 += persist_slice1(a.Lt, ldl, i, j0, j1, t_sh + (j0 - c_lo));
-          }
-          s0 += a.Gspec[(int64_t)hit * ldl + i];
-        } else {
-          int z = 0;
-          for (; z + 7 < ks; z += 8) {
-            double t[8];
+          piv = true;
+          ip = m;
+        } else if (!piv) {
+          if (ip == m) ip = bp;  // the row the swap moves from position m to bp
+          double s0 = 0.0;
+          if (hit >= 0) {  // the slices' sums from spec_m0 on (registers), in slice order
+            const int64_t z0 = a.spec_m0 / kslice, z1 = (m - 1) / kslice;
+            for (int64_t z = z0; z <= z1 && m > a.spec_m0; ++z) {
+              const int64_t j0 = z * kslice > a.spec_m0 ? z * kslice : a.spec_m0;
+              const int64_t j1 = (z + 1) * kslice < m ? (z + 1) * kslice : m;
+              if (j0 >= j1) continue;
+              const int64_t full = ((j1 - j0) / 8) * 8;
+              double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) t[u] = a.part[(int64_t)(z + u) * a.blk + i];
+              for (int u = 0; u < kSpecB; ++u) {
+                const int64_t j = a.spec_m0 + u;
+                if (j >= j0 && j < j1) {
+                  const int64_t o = j - j0;
+                  if (o < full && (o & 1))
+                    acc1 = fma(seg[u], t_sh[u], acc1);
+                  else
+                    acc0 = fma(seg[u], t_sh[u], acc0);
+                }
+              }
+              s0 += acc0 + acc1;
+            }
+            s0 += a.Gspec[(int64_t)hit * ldl + i];
+          } else {
+            int z = 0;
+            for (; z + 7 < ks; z += 8) {
+              double t[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s0 += t[u];
+              for (int u = 0; u < 8; ++u) t[u] = a.part[(int64_t)(z + u) * a.blk + i];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) s0 += t[u];
+            }
+            for (; z < ks; ++z) s0 += a.part[(int64_t)z * a.blk + i];
           }
-          for (; z < ks; ++z) s0 += a.part[(int64_t)z * a.blk + i];
-        }
-        const double v = (col - s0) / sq;
-        a.Lt[m * ldl + i] = v;
-        const double dn = a.dwork[i] - v * v;
-        a.dwork[i] = dn;
-        if (better(dn, pos_i, cbv, cbp)) {
-          cbv = dn;
-          cbp = pos_i;
-          cbr = i;
+          const double v = (col - s0) / sq;
+          a.Lt[m * ldl + i] = v;
+          dw = dw - v * v;
+#pragma unroll
+          for (int u = 0; u < kSpecB; ++u)
+            if (u == u_m) seg[u] = v;
+          if (better(dw, ip, cbv, cbp)) {
+            cbv = dw;
+            cbp = ip;
+            cbr = i;
+          }
         }
       }
-      if (a.trace != nullptr && lane == 0)  // the slowest wave's row phase
+      if (a.trace != nullptr && lane == 0)
         atomicMax(&a.trace[(m * G + wg) * 4 + 2], (unsigned long long)wall_clock64());
-      sv[tid] = cbv;
-      sp[tid] = cbp;
-      sr[tid] = cbr;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __syncthreads();
-      for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o && better(sv[tid + o], sp[tid + o], sv[tid], sp[tid])) {
-          sv[tid] = sv[tid + o];
-          sp[tid] = sp[tid + o];
-          sr[tid] = sr[tid + o];
-        }
-        __syncthreads();
-      }
-      if (tid == 0) {
-        if (m + 1 < a.m_end) {
-          const unsigned long long vb = __builtin_bit_cast(unsigned long long, sv[0]);
+      int csrc = tid;
+      wg_argmax(cbv, cbp, cbr, csrc, sv, sp, sr, ss);
+      // the workgroup's partial of step m: header, and the winning row's segment [spec_m0, m]
+      if (m + 1 < a.m_end) {
+        const bool mine = cbr >= 0 ? tid == csrc : tid == 0;
+        if (mine && !(wg == a.mute && m > a.m_begin)) {
+          const unsigned tag = (unsigned)m + 1;
+          unsigned long long *gs = a.slots + ((int64_t)((m + 1) & 1) * G + wg) * kSlot;
+          if (cbr >= 0 && spec) {
+#pragma unroll
+            for (int u = 0; u < kSpecB; ++u)
+              if (u <= S) {
+                const unsigned long long b = __builtin_bit_cast(unsigned long long, seg[u]);
+                const unsigned pl[2] = {(unsigned)(b & 0xffffffffull), (unsigned)(b >> 32)};
+                persist_publish(gs + 4 + 2 * u, 2, tag, pl);
+              }
+          }
+          const unsigned long long vb = __builtin_bit_cast(unsigned long long, cbv);
           const unsigned pl[4] = {(unsigned)(vb & 0xffffffffull), (unsigned)(vb >> 32),
-                                  (unsigned)(sr[0] >= 0 ? sp[0] : 0), (unsigned)(int)sr[0]};
-          if (wg != a.mute || m == a.m_begin)  // a muted workgroup: every wait times out
-            persist_publish(a.slots + (int64_t)wg * 4, 4, (unsigned)m + 1, pl);
+                                  (unsigned)(cbr >= 0 ? cbp : 0), (unsigned)(int)cbr};
+          persist_publish(gs, 4, tag, pl);
           if (a.trace != nullptr) a.trace[(m * G + wg) * 4 + 3] = wall_clock64();
-        } else {
-          a.pv_out[wg] = sv[0];
-          a.pp_out[wg] = sr[0] >= 0 ? sp[0] : (long long)a.N;
-          a.pr_out[wg] = sr[0];
         }
+      } else if (tid == 0) {
+        a.pv_out[wg] = cbv;
+        a.pp_out[wg] = cbr >= 0 ? cbp : (long long)a.N;
+        a.pr_out[wg] = cbr;
       }
-      __syncthreads();
     }
+    if (a.trace != nullptr && tid == 0 && m + 1 < a.m_end)
+      a.trace[((m + 1) * G + wg) * 4 + 0] = wall_clock64();
+  }
+  if (act) {  // the row state back for the next launch / the speculation kernels
+    a.pivflag[i] = piv ? 1 : 0;
+    a.dwork[i] = dw;
+    a.iperm[i] = ip;
   }
   if (wg == 0 && tid == 0) {
     a.st->m_pi = mpi;
@@ -792,9 +906,16 @@ fault:
   if (tid == 0) a.st->pivot_err = 2;
 }
 
+// perm[iperm[i]] = i (the persistent form keeps only the row -> position map)
+__global__ __launch_bounds__(256) void k_perm_from_iperm(const int64_t *__restrict__ iperm, int64_t n,
+                                                         int64_t *__restrict__ perm) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    perm[iperm[i]] = i;
+}
+
 // the persistent form applies: one rank, the dense rows or the sGDML single-column path, a panel
 // short enough for its pivot row to sit in LDS, and MLFF_PIVCHOL_PERSIST not 0
-static bool persist_grid(int64_t k, int *G_out) {
+static bool persist_grid(int64_t k, int64_t nrw, int *G_out) {
   const char *e0 = std::getenv("MLFF_PIVCHOL_PERSIST");  // read per build: 0 = launch sequence
   if ((e0 != nullptr && std::atoi(e0) == 0) || k > 12288) return false;
   int dev = 0, cus = 0;
@@ -807,10 +928,14 @@ static bool persist_grid(int64_t k, int *G_out) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void *>(k_piv_persist<true>),
                                                    256, shm) != hipSuccess || per < 1)
     return false;
-  int G = std::min(64, cus);  // 64 / 128 / 256: 24.1 / 28.3 / 37.7 us per step (configs[1])
-  if (const char *e = std::getenv("MLFF_PIV_G")) G = std::max(1, std::min(cus * per, std::atoi(e)));
-  *G_out = G;
-  return G >= 1;
+  // every row wave is one wave of the grid (its rows' state lives in registers): G >= nrw / 4;
+  // all of the grid resident at once (one workgroup per CU)
+  const int64_t need = (nrw + 3) / 4, cap = std::min<int64_t>(256, cus);
+  if (need > cap) return false;
+  int64_t G = std::max<int64_t>(need, std::min<int64_t>(cap, 256));
+  if (const char *e = std::getenv("MLFF_PIV_G")) G = std::max<int64_t>(need, std::min<int64_t>(cap, std::atoi(e)));
+  *G_out = (int)G;
+  return true;
 }
 
 int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
@@ -892,9 +1017,14 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
   };
   // the persistent form (k_piv_persist): one launch per speculative block
   int Gp = 0;
+  int64_t nrw = (nrows + 63) / 64;  // row waves: 64 dense rows, or 64 rows of a query point
+  if (!ctx->has_matrix && mfcols && ctx->mf.uvk != nullptr) {
+    const int64_t n3 = 3 * (int64_t)ctx->mf.n;
+    nrw = ((nrows + n3 - 1) / n3) * ((n3 + kColRows - 1) / kColRows);  // one rank: row0 = 0
+  }
   const bool persist = ctx->world == 1 && nrows > 0 && !rbfcols && !ctx->piv_persist_off &&
                        (ctx->has_matrix || (mfcols && ctx->mf.uvk != nullptr)) &&
-                       persist_grid(k, &Gp);
+                       persist_grid(k, nrw, &Gp);
   if (persist) {
     const bool sg = !ctx->has_matrix;
     const MfData &mf = ctx->mf;
@@ -906,9 +1036,9 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     MLFF_TRY(scratch_alloc(ctx, &pv2, std::max(npart, Gp)));
     MLFF_TRY(scratch_alloc(ctx, &pp2, std::max(npart, Gp)));
     MLFF_TRY(scratch_alloc(ctx, &pr2, std::max(npart, Gp)));
-    MLFF_TRY(scratch_alloc(ctx, &slots, (size_t)Gp * 4));
+    MLFF_TRY(scratch_alloc(ctx, &slots, (size_t)2 * Gp * kSlot));
     MLFF_TRY(scratch_alloc(ctx, &flags, (size_t)Gp));
-    MLFF_HIP(ctx, hipMemsetAsync(slots, 0, sizeof(unsigned long long) * Gp * 4, s));
+    MLFF_HIP(ctx, hipMemsetAsync(slots, 0, sizeof(unsigned long long) * 2 * Gp * kSlot, s));
     MLFF_HIP(ctx, hipMemsetAsync(flags, 0, sizeof(unsigned long long) * Gp, s));
     if (npart < Gp) {  // the partial buffers hold G entries
       MLFF_TRY(scratch_alloc(ctx, &pv, Gp));
@@ -940,11 +1070,8 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       pa.n_perms = mf.n_perms;
       pa.uvk = mf.uvk;
       pa.chunks = (3 * mf.n + kColRows - 1) / kColRows;
-      const int64_t n3 = 3 * (int64_t)mf.n;
-      pa.nrw = (int)(((nrows + n3 - 1) / n3) * pa.chunks);  // one rank: row0 = 0, i0 = 0
-    } else {
-      pa.nrw = (int)((nrows + 63) / 64);
     }
+    pa.nrw = (int)nrw;
     pa.part = part;
     pa.kmax_split = kmax_split;
     pa.Cspec = Cspec;
@@ -1007,13 +1134,16 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       m = m_end;
       stamp_at(m);
     }
+    hipLaunchKernelGGL(k_perm_from_iperm, dim3((unsigned)std::min<int64_t>((N + 255) / 256, 1024)),
+                       dim3(256), 0, s, (const int64_t *)iperm, N, ctx->perm);
     if (want_trace) {  // per step: the medians over workgroups of each phase, and the step time
       std::vector<unsigned long long> tr((size_t)k * Gp * 4);
       MLFF_HIP(ctx, hipMemcpyAsync(tr.data(), pa.trace, sizeof(unsigned long long) * tr.size(),
                                    hipMemcpyDeviceToHost, s));
       MLFF_HIP(ctx, hipStreamSynchronize(s));
       double acc[4] = {0, 0, 0, 0};
-      int64_t cnt = 0;
+      double slow_sum = 0.0, fast_sum = 0.0;  // steps with / without a grid-wide Schur GEMV
+      int64_t cnt = 0, slow = 0;
       for (int64_t m = 1; m + 1 < k; ++m) {
         const unsigned long long *a0 = &tr[(size_t)m * Gp * 4], *a1 = &tr[(size_t)(m + 1) * Gp * 4];
         if (a0[0] == 0 || a1[0] == 0 || a0[3] == 0) continue;  // launch boundaries
@@ -1029,12 +1159,22 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
           std::nth_element(ph[q].begin(), ph[q].begin() + Gp / 2, ph[q].end());
           acc[q] += ph[q][Gp / 2];
         }
+        if (ph[0][Gp / 2] > 20000.0) {
+          ++slow;
+          slow_sum += ph[3][Gp / 2];
+        } else {
+          fast_sum += ph[3][Gp / 2];
+        }
         ++cnt;
       }
       if (cnt > 0)
         std::fprintf(stderr, "[piv trace] G=%d steps=%lld median ns: winner+stage+miss %.0f, rows %.0f, "
                      "publish %.0f, step %.0f\n", Gp, (long long)cnt, acc[0] / cnt, acc[1] / cnt,
                      acc[2] / cnt, acc[3] / cnt);
+      if (cnt > 0)
+        std::fprintf(stderr, "[piv trace] %lld steps > 20 us before the rows (misses): %.2f ms; "
+                     "the other %lld: %.2f ms\n", (long long)slow, 1e-6 * slow_sum,
+                     (long long)(cnt - slow), 1e-6 * fast_sum);
     }
   } else {
   stamp_at(0);

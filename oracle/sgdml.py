@@ -146,6 +146,44 @@ def kernel_matvec_matrix_free(R_desc, R_d_desc, perms, sig, x, use_E_cstr=False)
     return np.concatenate([y.reshape(-1), outE]) if use_E_cstr else y.reshape(-1)
 
 
+def kernel_column_matrix_free(R_desc, R_d_desc, perms, sig, g):
+    """K e_g of kernel_matvec_matrix_free (the reference's get_col through K_op,
+    iterative_cholesky.py:152-156 with predict.py:72-234) from the one training point it touches:
+    e_g (g = j 3n + 3a + c) makes z_j = J_j e_(a,c) the only non-zero z, so
+        F_i = sum_p 5 m_ijp (diff_ijp . z_j[P_p]) diff_ijp - w_ijp z_j[P_p],   y_i = J_i^T F_i
+    -- O(M n_perms D) instead of a full operator application (O(M^2 n_perms D)); the same products,
+    the zero terms of the other training points left out, so the column equals K_op e_g to the
+    rounding of its sums (<= 3e-16 of its largest entry,
+    tests/test_oracle_golden.py::test_column_restatement_matches_operator)."""
+    R_desc = np.asarray(R_desc, dtype=np.float64)
+    M, D = R_desc.shape
+    n = int((1 + np.sqrt(8 * D + 1)) / 2)
+    perms = np.atleast_2d(perms)
+    P = np.array([desc_perm(p) for p in perms])
+    s_at, t_at = np.tril_indices(n, k=-1)
+    j, a, c = g // (3 * n), (g % (3 * n)) // 3, g % 3
+    X = np.zeros((n, 3))
+    X[a, c] = 1.0
+    z = np.einsum("dc,dc->d", R_d_desc[j], X[t_at, :] - X[s_at, :])   # J_j e_(a,c)
+    Rt = R_desc[j][P][None]                         # 1 x n_perms x D
+    Zt = z[P][None]
+    sqrt5 = np.sqrt(5.0)
+    y = np.empty((M, n, 3))
+    for i in range(M):
+        diff = R_desc[i][None, None, :] - Rt
+        norm = sqrt5 * np.linalg.norm(diff, axis=2)
+        m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
+        w = (sig ** 2 + sig * norm) * m
+        aa = np.einsum("jpd,jpd->jp", diff, Zt)
+        F = np.einsum("jp,jpd->d", 5.0 * m * aa, diff) - np.einsum("jp,jpd->d", w, Zt)
+        contrib = R_d_desc[i] * F[:, None]
+        yi = np.zeros((n, 3))
+        np.add.at(yi, t_at, contrib)
+        np.add.at(yi, s_at, -contrib)
+        y[i] = yi
+    return y.reshape(-1)
+
+
 def pair_records(R_desc, R_d_desc, perms, sig):
     """The x-independent per-(i, j, p) quantities of the operator above, as the GPU keeps
     them (kernels_gen.hip k_sgdml_uv, mirror = 0): u = J_i^T diff (query point side),

@@ -13,13 +13,16 @@ import sgdml_amd  # noqa: E402
 from sgdml_amd import synthetic  # noqa: E402
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 2701
+only = sys.argv[2] if len(sys.argv) > 2 else None  # e.g. "G=64": that configuration only
 ds = synthetic.nanotube_like(14, seed=0)
 Rd, Rdd = sgdml_amd.sgdml_descriptors(ds["R"])
 y, _ = synthetic.labels(ds["F"])
 n = y.size
 ref = None
 configs = [("legacy", {"MLFF_PIVCHOL_PERSIST": "0"})] + [
-    (f"G={g}", {"MLFF_PIVCHOL_PERSIST": "1", "MLFF_PIV_G": str(g)}) for g in (256, 128, 64, 32)]
+    (f"G={g}", {"MLFF_PIVCHOL_PERSIST": "1", "MLFF_PIV_G": str(g)}) for g in (256, 128, 64)]
+if only is not None:
+    configs = [c for c in configs if c[0] == only]
 for rep in range(2):
     for name, env in configs:
         for key in ("MLFF_PIV_G", "MLFF_PIV_TRACE"):
