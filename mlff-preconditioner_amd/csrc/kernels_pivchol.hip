@@ -485,6 +485,12 @@ struct PersistArgs {
   int64_t m_begin, m_end;
   int mute;  // test hook (MLFF_PIV_MUTE): this workgroup stops publishing after step m_begin
   unsigned long long *trace;  // MLFF_PIV_TRACE: 4 wall-clock stamps per (step, workgroup)
+  unsigned long long *step_clock;  // 2 k: workgroup 0's wall clock at each step's start and end
+  // the speculative block's candidates: each one's L value of every step (2 x kSpecC x 2
+  // granules, by step parity), published by its row's owner; and their columns S e_c
+  // (kSpecC x blk, k_sgdml_col before the launch; nullptr: evaluated in the step)
+  unsigned long long *cands;
+  const double *colbuf;
 };
 
 __host__ __device__ inline int ksplit_of(int64_t k, int64_t ncols) {  // choose_ksplit
@@ -626,7 +632,7 @@ __device__ __forceinline__ void wg_argmax(double &v, long long &p, long long &r,
     }
 }
 
-constexpr int kSlot = 4 + 2 * kSpecB;  // granules per workgroup slot: header + L segment
+constexpr int kSlot = 4;  // granules per workgroup slot: value lo / hi, position, row
 
 template <bool SG>
 __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
@@ -635,6 +641,8 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
   __shared__ long long sp[4], sr[4];
   __shared__ int ss[4];
   __shared__ long long s_C[kSpecC];
+  __shared__ double s_ch[kSpecC][kSpecB];  // the candidates' L values over the block's steps
+  __shared__ unsigned long long s_pg[4 * 256 + 2 * kSpecC];  // one poll round's granules
   __shared__ int s_bail;
   const int G = (int)gridDim.x, wg = (int)blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
@@ -669,15 +677,19 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
 #pragma unroll
   for (int u = 0; u < kSpecB; ++u) seg[u] = 0.0;
   __syncthreads();
+  int cidx = -1;  // this row's index among the block's candidates
+  if (spec && act)
+    for (int c = 0; c < kSpecC; ++c)
+      if (s_C[c] == i) cidx = c;
   long long mpi = -1;
   double sq = 0.0;
   for (int64_t m = a.m_begin; m < a.m_end; ++m) {
     const int S = spec ? (int)(m - a.spec_m0) : 0;  // segment length of the step-(m - 1) slots
+    if (wg == 0 && tid == 0) a.step_clock[2 * m] = wall_clock64();
     // ---- the winner of step m from the partials of step m - 1
     double bv = -INFINITY;
     long long bp = LLONG_MAX, br = -1;
     int src = -1;
-    unsigned long long g[4];
     if (m == a.m_begin) {
       for (int t = tid; t < a.npc; t += 256)
         if (better(a.pv_in[t], a.pp_in[t], bv, bp)) {
@@ -686,32 +698,43 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
           br = a.pr_in != nullptr ? a.pr_in[t] : bp;
         }
     } else {
-      // thread t < G: slot t's header (the winner's L segment is read after the reduction)
-      if (tid < G) {
-        const unsigned tag = (unsigned)m;  // published at step m - 1
-        // two slot buffers by step parity: a workgroup one step ahead overwrites the other one
-        unsigned long long *gs = a.slots + ((int64_t)(m & 1) * G + tid) * kSlot;
-        const unsigned long long t0 = wall_clock64();
-        for (;;) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            g[q] = __hip_atomic_load(gs + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          bool ok = true;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ok = ok && (unsigned)(g[q] >> 32) == tag;
-          if (ok) break;
-          if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
-            s_bail = 1;
-            break;
+      // one round trip: the G slot headers of step m - 1 and the candidates' L values of that
+      // step; thread t polls granules t, t + 256, ... (a workgroup one step ahead writes the
+      // other buffer of each pair)
+      const unsigned tag = (unsigned)m;
+      const int nh = 4 * G, ne = nh + (spec ? 2 * kSpecC : 0);
+      unsigned long long *gh = a.slots + (int64_t)(m & 1) * G * kSlot;
+      unsigned long long *gc = a.cands + (int64_t)(m & 1) * 2 * kSpecC;
+      const unsigned long long t0 = wall_clock64();
+      for (int e = tid; e < ne; e += 256) {
+        unsigned long long *ge = e < nh ? gh + e : gc + (e - nh);
+        unsigned long long v = 0;
+        if (e < nh || s_C[(e - nh) >> 1] >= 0)  // (an empty candidate publishes nothing)
+          for (;;) {
+            v = __hip_atomic_load(ge, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(v >> 32) == tag) break;
+            if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
+              s_bail = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
           }
-          __builtin_amdgcn_s_sleep(2);
-        }
+        s_pg[e] = v;
+      }
+      __syncthreads();
+      if (tid < G) {
+        unsigned long long g[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[q] = s_pg[4 * tid + q];
         bv = __builtin_bit_cast(double, (g[1] << 32) | (g[0] & 0xffffffffull));
         bp = (long long)(unsigned)(g[2] & 0xffffffffull);
         br = (long long)(int)(unsigned)(g[3] & 0xffffffffull);
         if (br < 0) bp = LLONG_MAX;  // an empty partial
         src = tid;
       }
+      if (spec && tid < kSpecC && S > 0)
+        s_ch[tid][S - 1] = __builtin_bit_cast(double, (s_pg[nh + 2 * tid + 1] << 32) |
+                                                          (s_pg[nh + 2 * tid] & 0xffffffffull));
     }
     wg_argmax(bv, bp, br, src, sv, sp, sr, ss);
     if (s_bail) goto fault;
@@ -729,26 +752,7 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
     const int ks = m > 0 ? min(a.kmax_split, ksplit_of(m, a.blk)) : 0;
     const int64_t kslice = ks > 0 ? (m + ks - 1) / ks : 1;
     if (hit >= 0) {
-      // the pivot row over [spec_m0, m): the segment the winner's workgroup published beside its
-      // header (tagged granules: polled, normally already there)
-      if (tid < S && src >= 0) {
-        unsigned long long *gq = a.slots + ((int64_t)(m & 1) * G + src) * kSlot + 4 + 2 * tid;
-        const unsigned long long t0 = wall_clock64();
-        unsigned long long lo, hi;
-        for (;;) {
-          lo = __hip_atomic_load(gq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          hi = __hip_atomic_load(gq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(lo >> 32) == (unsigned)m && (unsigned)(hi >> 32) == (unsigned)m) break;
-          if ((unsigned long long)(wall_clock64() - t0) > kPersistTimeout) {
-            s_bail = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        t_sh[tid] = __builtin_bit_cast(double, (hi << 32) | (lo & 0xffffffffull));
-      }
-      __syncthreads();
-      if (s_bail) goto fault;
+      // the pivot row over [spec_m0, m) is the winning candidate's history (s_ch)
     } else if (mpi >= 0 && ks > 0) {
       // a miss: every L row so far is written back and visible (fenced arrival), the whole
       // pivot row is staged, and the grid runs k_colgemv_part's split-K slices over [0, m)
@@ -786,7 +790,9 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
     // ---- rows: column entry, Schur sum, L[m, i], residual diagonal, partial argmax
     {
       double col = 0.0;
-      if (SG) {
+      if (SG && hit >= 0 && a.colbuf != nullptr) {  // the candidate's column, evaluated before
+        if (act) col = a.colbuf[(int64_t)hit * ldl + i];
+      } else if (SG) {
         if (r < a.nrw && mpi >= 0) {  // wave-uniform: the column code is a wave sum
           bool a2;
           int64_t i2;
@@ -800,6 +806,7 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
       }
       double cbv = -INFINITY;
       long long cbp = (long long)a.N, cbr = -1;
+      double lval = 0.0;  // this row's L[m, i] (0 for a row pivoted before: never written)
       if (act && mpi >= 0) {
         const int u_m = S;  // this step's index in the segment
         // (perm, the inverse of iperm, is written once after the build: two rows' owners on
@@ -807,6 +814,7 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
         // fence on a hit step nothing orders the two write-backs)
         if (i == mpi) {  // k_piv_finalize's writes for the pivot row
           a.Lt[m * ldl + i] = sq;
+          lval = sq;
           piv = true;
           ip = m;
         } else if (!piv) {
@@ -826,9 +834,9 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
                 if (j >= j0 && j < j1) {
                   const int64_t o = j - j0;
                   if (o < full && (o & 1))
-                    acc1 = fma(seg[u], t_sh[u], acc1);
+                    acc1 = fma(seg[u], s_ch[hit][u], acc1);
                   else
-                    acc0 = fma(seg[u], t_sh[u], acc0);
+                    acc0 = fma(seg[u], s_ch[hit][u], acc0);
                 }
               }
               s0 += acc0 + acc1;
@@ -847,6 +855,7 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
           }
           const double v = (col - s0) / sq;
           a.Lt[m * ldl + i] = v;
+          lval = v;
           dw = dw - v * v;
 #pragma unroll
           for (int u = 0; u < kSpecB; ++u)
@@ -862,21 +871,17 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
         atomicMax(&a.trace[(m * G + wg) * 4 + 2], (unsigned long long)wall_clock64());
       int csrc = tid;
       wg_argmax(cbv, cbp, cbr, csrc, sv, sp, sr, ss);
-      // the workgroup's partial of step m: header, and the winning row's segment [spec_m0, m]
+      // the workgroup's partial of step m, and (candidate rows) their L[m, i]
       if (m + 1 < a.m_end) {
+        const unsigned tag = (unsigned)m + 1;
+        if (cidx >= 0) {
+          const unsigned long long b = __builtin_bit_cast(unsigned long long, lval);
+          const unsigned pl[2] = {(unsigned)(b & 0xffffffffull), (unsigned)(b >> 32)};
+          persist_publish(a.cands + ((int64_t)((m + 1) & 1) * kSpecC + cidx) * 2, 2, tag, pl);
+        }
         const bool mine = cbr >= 0 ? tid == csrc : tid == 0;
         if (mine && !(wg == a.mute && m > a.m_begin)) {
-          const unsigned tag = (unsigned)m + 1;
           unsigned long long *gs = a.slots + ((int64_t)((m + 1) & 1) * G + wg) * kSlot;
-          if (cbr >= 0 && spec) {
-#pragma unroll
-            for (int u = 0; u < kSpecB; ++u)
-              if (u <= S) {
-                const unsigned long long b = __builtin_bit_cast(unsigned long long, seg[u]);
-                const unsigned pl[2] = {(unsigned)(b & 0xffffffffull), (unsigned)(b >> 32)};
-                persist_publish(gs + 4 + 2 * u, 2, tag, pl);
-              }
-          }
           const unsigned long long vb = __builtin_bit_cast(unsigned long long, cbv);
           const unsigned pl[4] = {(unsigned)(vb & 0xffffffffull), (unsigned)(vb >> 32),
                                   (unsigned)(cbr >= 0 ? cbp : 0), (unsigned)(int)cbr};
@@ -891,6 +896,7 @@ __global__ __launch_bounds__(256) void k_piv_persist(PersistArgs a) {
     }
     if (a.trace != nullptr && tid == 0 && m + 1 < a.m_end)
       a.trace[((m + 1) * G + wg) * 4 + 0] = wall_clock64();
+    if (wg == 0 && tid == 0) a.step_clock[2 * m + 1] = wall_clock64();
   }
   if (act) {  // the row state back for the next launch / the speculation kernels
     a.pivflag[i] = piv ? 1 : 0;
@@ -1016,6 +1022,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     if (stamp_col.size() < stamps.size()) stamp_col.push_back(m);
   };
   // the persistent form (k_piv_persist): one launch per speculative block
+  unsigned long long *step_clock = nullptr;  // its per-step clocks (split each launch's time)
   int Gp = 0;
   int64_t nrw = (nrows + 63) / 64;  // row waves: 64 dense rows, or 64 rows of a query point
   if (!ctx->has_matrix && mfcols && ctx->mf.uvk != nullptr) {
@@ -1038,6 +1045,11 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     MLFF_TRY(scratch_alloc(ctx, &pr2, std::max(npart, Gp)));
     MLFF_TRY(scratch_alloc(ctx, &slots, (size_t)2 * Gp * kSlot));
     MLFF_TRY(scratch_alloc(ctx, &flags, (size_t)Gp));
+    unsigned long long *cands = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &cands, (size_t)2 * 2 * kSpecC));
+    MLFF_HIP(ctx, hipMemsetAsync(cands, 0, sizeof(unsigned long long) * 2 * 2 * kSpecC, s));
+    double *colbuf = nullptr;  // the candidates' columns (sGDML path, speculative blocks)
+    if (sg && spec) MLFF_TRY(scratch_alloc(ctx, &colbuf, (size_t)kSpecC * blk));
     MLFF_HIP(ctx, hipMemsetAsync(slots, 0, sizeof(unsigned long long) * 2 * Gp * kSlot, s));
     MLFF_HIP(ctx, hipMemsetAsync(flags, 0, sizeof(unsigned long long) * Gp, s));
     if (npart < Gp) {  // the partial buffers hold G entries
@@ -1076,8 +1088,13 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
     pa.kmax_split = kmax_split;
     pa.Cspec = Cspec;
     pa.Gspec = Gspec;
+    pa.cands = cands;
+    pa.colbuf = nullptr;
     pa.mute = -1;
     pa.trace = nullptr;
+    MLFF_TRY(scratch_alloc(ctx, &pa.step_clock, (size_t)2 * k));
+    MLFF_HIP(ctx, hipMemsetAsync(pa.step_clock, 0, sizeof(unsigned long long) * 2 * k, s));
+    step_clock = pa.step_clock;
     const bool want_trace = std::getenv("MLFF_PIV_TRACE") != nullptr;
     if (want_trace) {
       MLFF_TRY(scratch_alloc(ctx, &pa.trace, (size_t)k * Gp * 4));
@@ -1098,6 +1115,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       if (spec) {
         if (m < kSpecMin) {
           m_end = std::min<int64_t>(k, kSpecMin);
+          pa.colbuf = nullptr;
         } else {
           hipLaunchKernelGGL(k_spec_top_part, dim3(kSpecGroups), dim3(256), 0, s, ctx->dwork,
                              ctx->pivflag, nrows, cv, ci);
@@ -1106,6 +1124,12 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
           hipLaunchKernelGGL(k_spec_gather, dim3((unsigned)std::min<int64_t>((m * kSpecC + 255) / 256, 4096)),
                              dim3(256), 0, s, ctx->T, blk, m, Cspec, Aspec);
           MLFF_TRY(gemm_splitk(ctx, true, false, kSpecC, blk, m, Aspec, kSpecC, ctx->T, blk, Gspec, blk));
+          if (colbuf != nullptr) {  // the candidates' columns, the steps' hits read them
+            launch_sgdml_columns(mf.Rdd, mf.M, mf.n, mf.D, mf.i0, mf.pi_d, mf.piinv_d, mf.n_perms,
+                                 mf.uvk, ctx->row0, nrows, Cspec, kSpecC, ctx->st, ctx->sigma_K,
+                                 colbuf, blk, s);
+            pa.colbuf = colbuf;
+          }
           pa.spec_m0 = m;
           m_end = std::min<int64_t>(k, m + kSpecB);
         }
@@ -1249,12 +1273,28 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
                                  hipMemcpyDeviceToHost, s));
   MLFF_HIP(ctx, hipStreamSynchronize(s));
   ctx->piv_col_s.assign((size_t)k, 0.0);
-  if (stamp_col.size() == stamps.size()) {  // each segment's time split evenly over its columns
+  std::vector<unsigned long long> clk;
+  if (step_clock != nullptr && k > 0) {
+    clk.resize((size_t)2 * k);
+    MLFF_HIP(ctx, hipMemcpy(clk.data(), step_clock, sizeof(unsigned long long) * 2 * k,
+                            hipMemcpyDeviceToHost));
+  }
+  if (stamp_col.size() == stamps.size()) {
+    // each segment's event time over its columns: evenly, or (persistent form) in proportion to
+    // the steps' own device clocks
     for (size_t g = 0; g + 1 < stamps.size(); ++g) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, stamps[g], stamps[g + 1]);
       const int64_t c0 = stamp_col[g], c1 = std::min<int64_t>(stamp_col[g + 1], k);
-      for (int64_t c = c0; c < c1; ++c) ctx->piv_col_s[c] = 1e-3 * ms / (double)(c1 - c0);
+      double wsum = 0.0;
+      for (int64_t c = c0; c < c1 && !clk.empty(); ++c)
+        wsum += clk[2 * c + 1] > clk[2 * c] ? (double)(clk[2 * c + 1] - clk[2 * c]) : 0.0;
+      for (int64_t c = c0; c < c1; ++c) {
+        double w = 1.0 / (double)(c1 - c0);
+        if (wsum > 0.0)
+          w = (clk[2 * c + 1] > clk[2 * c] ? (double)(clk[2 * c + 1] - clk[2 * c]) : 0.0) / wsum;
+        ctx->piv_col_s[c] = 1e-3 * ms * w;
+      }
     }
   }
   for (hipEvent_t e : stamps) (void)hipEventDestroy(e);

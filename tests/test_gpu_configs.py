@@ -349,3 +349,4 @@ def test_ethanol_full_size_against_oracle_fixture(sg, golden_dir, monkeypatch, k
             assert r.info == int(f[key + sfx + "_info"]) == 0
             assert_pcg_parity(r.iters, r.trace[1:], -r.x, int(f[key + sfx + "_iters"]),
                               f[key + sfx + "_trace"][1:], f[key + sfx + "_alphas"], band=b)
+

@@ -98,8 +98,12 @@ def test_sharded_solver_gathers(sg):
     np.testing.assert_allclose(y3, y1, rtol=1e-13, atol=1e-13 * np.abs(y1).max())
     np.testing.assert_array_equal(d3, d1)
     np.testing.assert_allclose(z3, z1, rtol=1e-9, atol=1e-9 * np.abs(z1).max())
-    assert r3.info == r1.info == 0 and abs(r3.iters - r1.iters) <= 1
-    assert np.linalg.norm(r3.x - r1.x) <= 1e-7 * np.linalg.norm(r1.x)
+    # 3 ranks vs one: two summation orders of a chaotic solve (the one-step Woodbury panel,
+    # iterative_cholesky.py:141-148): the generic chaotic rule of tests/parity.py
+    from tests.parity import assert_pcg_parity
+
+    assert r3.info == r1.info == 0
+    assert_pcg_parity(r3.iters, r3.trace[1:], r3.x, r1.iters, r1.trace[1:], r1.x, mode="chaotic")
     assert seen and all(s == n for s in seen)
 
 
