@@ -1024,6 +1024,13 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
     fold_op = fold;
     fold = StopFold{};
   }
+  // symmetric tiles + low-rank apply (configs[2]): p = z + beta p formed by the tile workgroups
+  // (k_symv_dyn, PGather with one rank) and written by the slot reduction -- k_update_p's bits,
+  // one launch less; the apply writes z and its rho partials into the gather block for it
+  const bool fuse_p1 = ctx->fuse_p && ctx->use_sym && lowrank && ctx->sym.dyn > 0 &&
+                       ctx->sym.ntiles > 0 && !ctx->exact_sums;
+  double *zout = fuse_p1 ? ctx->gb : ctx->z;
+  double *rhoout = fuse_p1 ? ctx->gb + ctx->blk : rho_part(ctx);
   const double *zsrc;
   if (lowrank) {
     const size_t pm = mark_begin(ctx, marks);
@@ -1033,33 +1040,36 @@ int launch_iteration(mlff_ctx *ctx, long long it, std::vector<GemvMark> *marks, 
                         1.0 / ctx->lam, ctx->tpart, status, s);
       launch_dot_part(ctx->r, ctx->z, ctx->nrows, rho_part(ctx), status, s);
     } else if (ctx->lr_rows) {
-      launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, ctx->z, ctx->nrows, ctx->sigma_p,
-                           1.0 / ctx->lam, rho_part(ctx), status, s, ctx->lr_zpart, fold, xf);
+      launch_lr_apply_rows(ctx->T, ctx->blk, ctx->k, ctx->r, zout, ctx->nrows, ctx->sigma_p,
+                           1.0 / ctx->lam, rhoout, status, s, ctx->lr_zpart, fold, xf);
     } else if (ctx->lr_cluster) {
-      launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, ctx->r, ctx->z, ctx->nrows,
-                              ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s,
+      launch_lr_apply_cluster(ctx->T, ctx->blk, ctx->k, ctx->lr_q, ctx->r, zout, ctx->nrows,
+                              ctx->sigma_p, 1.0 / ctx->lam, rhoout, status, s,
                               ctx->lr_zpart, ctx->lr_slots, next_lr_epoch(ctx), &ctx->st->status,
                               fold);
     } else {
       launch_gemv_split(ctx->T, ctx->blk, ctx->k, ctx->blk, ctx->tsplit, ctx->r, ctx->tpart, status,
                         s, fold);
-      launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, ctx->z, ctx->nrows,
-                      ctx->sigma_p, 1.0 / ctx->lam, rho_part(ctx), status, s, ctx->zpart, ctx->zsplit);
+      launch_precon_z(ctx->T, ctx->blk, ctx->k, ctx->tsplit, ctx->tpart, ctx->r, zout, ctx->nrows,
+                      ctx->sigma_p, 1.0 / ctx->lam, rhoout, status, s, ctx->zpart, ctx->zsplit);
     }
     mark_end(ctx, marks, pm, it, 1);
-    zsrc = ctx->z;
+    zsrc = zout;
   } else {
     launch_dot_part(ctx->r, ctx->r, ctx->nrows, rho_part(ctx), status, s, fold);
     zsrc = ctx->r;
   }
   const PFuse pf{zsrc, rho_part(ctx), ctx->st, it, fold_op};
-  if (!fuse_p) launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
+  if (!fuse_p && !fuse_p1)
+    launch_update_p(zsrc, p_loc, ctx->nrows, rho_part(ctx), ctx->st, it, status, s);
   const size_t e0 = mark_begin(ctx, marks);
   if (ctx->use_sym) {
     // q = sigma K p + lam p and the p.q partials from the slot reduction (no dot launch)
-    launch_symv(ctx->sym, ctx->p_full, ctx->sym.P, status, s);
+    const PGather pg1 = fuse_p1 ? PGather{ctx->gb, ctx->gstride, ctx->blk, 1, ctx->st, it}
+                                : PGather{};
+    launch_symv(ctx->sym, ctx->p_full, ctx->sym.P, status, s, pg1);
     launch_sym_reduce_pq(ctx->sym, ctx->nrows, ctx->q, ctx->sigma_K, ctx->lam, p_loc,
-                         pq_part(ctx), status, s);
+                         pq_part(ctx), status, s, pg1);
     mark_end(ctx, marks, e0, it);
   } else {
     MLFF_TRY(launch_operator(ctx, ctx->p_full, ctx->q, p_loc, status, pq_part(ctx),
@@ -1280,7 +1290,8 @@ int mlff_ctx_create(int device, int rank, int world, const unsigned char *comm_i
       hipMalloc(&ctx->pivflag, sizeof(int) * ctx->blk) != hipSuccess ||
       hipMalloc(&ctx->perm, sizeof(int64_t) * n_global) != hipSuccess)
     return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));
-  if (world > 1) {
+  {
+    // the gather buffer: z | rho partials per rank (one rank: the fused tile iteration's operand)
     ctx->gstride = ctx->blk + kVecGrid;
     if (hipMalloc(&ctx->gb, sizeof(double) * world * ctx->gstride) != hipSuccess)
       return fail(set_error(nullptr, MLFF_ERR_NOMEM, "device allocation failed"));

@@ -675,7 +675,8 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
 // one rank, PCG: q = sigma (slot sums) + lam p over n_out rows, and the p.q partial sums
 // of the kVecGrid workgroups into pq_part
 void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
-                          const double *p, double *pq_part, const int *status, hipStream_t s);
+                          const double *p, double *pq_part, const int *status, hipStream_t s,
+                          PGather pg = PGather{});
 // several ranks: sp.yg = this rank's slot sums of every row (rank blocks of sp.ystride);
 // with p_full: also this rank's share sigma p.y_g + lam ||p_loc||^2 published into the
 // tail slot `rank` of every block (pq_part / pp_part: kVecGrid scratch each)

@@ -388,10 +388,20 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
                                                     const double *__restrict__ vloc,
                                                     double *__restrict__ pq_part,
                                                     unsigned long long *__restrict__ ticket,
-                                                    const int *__restrict__ status) {
+                                                    const int *__restrict__ status,
+                                                    PGather pg = PGather{},
+                                                    double *pw = nullptr) {
   if (status != nullptr && *status != ST_RUNNING) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
   double apq = 0.0;
+  // one rank, fused p update (PGather): rho as k_symv_dyn summed it, p = fma(beta, p_old, z)
+  // written here (every tile has read p_old) and used as the epilogue's v -- k_update_p's bits
+  double beta = 0.0;
+  if (PQ && pg.gb != nullptr) {
+    const double rho = pg.st->rho_new;
+    if (pg.it > 1) beta = rho / pg.st->rho1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) pg.st->rho = rho;
+  }
   const int64_t pl = (int64_t)nb * Np;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_out;
        i += (int64_t)gridDim.x * 256) {
@@ -438,10 +448,17 @@ __global__ __launch_bounds__(256) void k_sym_reduce(const double *__restrict__ P
         if (t + u < nb) s += v[u];
     }
     if (EPI) {
+      double pv = 0.0;
+      if (PQ && pg.gb != nullptr) {  // (vloc is p itself: read through pw only)
+        pv = pg_val(pg, pw, i, beta);
+        pw[i] = pv;
+      } else if (vloc != nullptr) {
+        pv = vloc[i];
+      }
       double yv = sigma * s;
-      if (vloc != nullptr) yv += lam * vloc[i];
+      if (vloc != nullptr) yv += lam * pv;
       y[i] = yv;
-      if (PQ) apq = fma(vloc[i], yv, apq);
+      if (PQ) apq = fma(pv, yv, apq);
     } else {
       y[i] = s;
     }
@@ -745,11 +762,12 @@ void launch_sym_reduce(const SymPack &sp, int64_t n_out, double *y, bool epilogu
 }
 
 void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double sigma, double lam,
-                          const double *p, double *pq_part, const int *status, hipStream_t s) {
+                          const double *p, double *pq_part, const int *status, hipStream_t s,
+                          PGather pg) {
   hipLaunchKernelGGL((k_sym_reduce<true, true>), dim3(kVecGrid), dim3(256), 0, s, sp.P, sp.Pq,
                      sp.split, (int)sp.t_split, sp.Np, (int)sp.nb, (1 << sp.lsub) - 1, n_out, y, sigma,
                      lam, p, pq_part,
-                     sp.ticket, status);
+                     sp.ticket, status, pg, pg.gb != nullptr ? const_cast<double *>(p) : nullptr);
 }
 
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,

@@ -148,3 +148,34 @@ def test_symtile_quarter_tail_matches_dense(sg, n, sched, lsub, monkeypatch):
         ys2 = s.matvec(v)
     np.testing.assert_array_equal(ys, ys2)  # deterministic
     assert np.max(np.abs(ys - yd)) <= 1e-13 * np.abs(yd).max()
+
+
+@pytest.mark.parametrize("n,k,forms", [(9000, 256, "cluster"), (4000, 300, "rows"),
+                                        (20000, 256, "twopass")])
+def test_symtile_fused_p_update_bitwise(sg, n, k, forms, monkeypatch):
+    """One rank, symmetric tiles + low-rank apply (configs[2]'s iteration): p = z + beta p formed
+    by the tile workgroups from the apply's gather block and written by the slot reduction
+    (default, round 6) against the separate k_update_p launch (MLFF_FUSE_P=0): the same sums
+    in the same order, so iterates, residual curve and stop decisions are bit-identical --
+    through the one-pass rows, the cluster and the two-pass applies, with chunk boundaries."""
+    from sgdml_amd import synthetic
+
+    X, b = synthetic.rbf_points(n, 3, 0)
+    idx = np.sort(np.random.default_rng(0).choice(n, k, replace=False))
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MLFF_FUSE_P", fuse)
+        if forms == "twopass":
+            monkeypatch.setenv("MLFF_LR_ROWS", "0")  # neither one-pass form
+        with sg.KernelSolver(n) as s:
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, 1e-6)
+            s.precon_nystrom(idx)
+            assert s.storage_info()[0] == "sym"
+            form, _ = s.precon_apply_traffic()
+            assert form == {"twopass": 0, "rows": 1, "cluster": 2}[forms], form
+            out[fuse] = s.pcg(b, tol=1e-6, maxiter=5 * n, chunk=7)
+    a, c = out["1"], out["0"]
+    assert a.info == c.info == 0 and a.iters == c.iters
+    np.testing.assert_array_equal(a.trace, c.trace)
+    np.testing.assert_array_equal(a.x, c.x)
