@@ -150,7 +150,8 @@ def test_symtile_quarter_tail_matches_dense(sg, n, sched, lsub, monkeypatch):
     assert np.max(np.abs(ys - yd)) <= 1e-13 * np.abs(yd).max()
 
 
-@pytest.mark.parametrize("n,k,forms", [(9000, 256, "cluster"), (4000, 300, "rows"),
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n,k,forms", [(65536, 256, "cluster"), (4000, 300, "rows"),
                                         (20000, 256, "twopass")])
 def test_symtile_fused_p_update_bitwise(sg, n, k, forms, monkeypatch):
     """One rank, symmetric tiles + low-rank apply (configs[2]'s iteration): p = z + beta p formed
@@ -174,8 +175,9 @@ def test_symtile_fused_p_update_bitwise(sg, n, k, forms, monkeypatch):
             assert s.storage_info()[0] == "sym"
             form, _ = s.precon_apply_traffic()
             assert form == {"twopass": 0, "rows": 1, "cluster": 2}[forms], form
-            out[fuse] = s.pcg(b, tol=1e-6, maxiter=5 * n, chunk=7)
+            # configs[2] itself for the cluster form: 300 iterations of it (info = maxiter)
+            out[fuse] = s.pcg(b, tol=1e-6, maxiter=300 if n == 65536 else 5 * n, chunk=7)
     a, c = out["1"], out["0"]
-    assert a.info == c.info == 0 and a.iters == c.iters
+    assert a.info == c.info and a.iters == c.iters
     np.testing.assert_array_equal(a.trace, c.trace)
     np.testing.assert_array_equal(a.x, c.x)
