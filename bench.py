@@ -612,7 +612,12 @@ def sgdml_workload(args, rank, world, local, pg):
     solver.synchronize()
     t_asm = time.perf_counter() - t0
     _, t_chol = solver.precon_pivchol(k)
+    # the first build includes one-time costs (code-object loads of its kernels, the scratch
+    # arena's first chunks); a second, identical build shows the steady-state cost (skipped
+    # where the build itself takes seconds)
+    t_warm = solver.precon_pivchol(k)[1] if t_chol < 1.0 else None
     return solver, n, k, y, {"operator_setup_s": t_asm, "pivchol_build_s": t_chol,
+                             "pivchol_build_warm_s": t_warm,
                              "assembled": args.storage in ("sym", "dense"),
                              "workload": f"sgdml_{name}_n{n}_pivchol{k}", "M": M,
                              "n_atoms": n_atoms, "desc": (Rd, Rdd),
@@ -1001,6 +1006,7 @@ def main():
             "time_to_solution": None if sg_info is None or solve is None else {
                 "precon_build_s": t_pre, "cg_to_1e-6_s": solve["seconds"],
                 "total_s": t_pre + solve["seconds"],
+                "precon_build_warm_s": sg_info.get("pivchol_build_warm_s"),
                 "reference_published": {
                     "pivchol_s_per_column_nanotube_k3885": [0.076, 0.178],
                     "cg_step_s": REF_STEP_S.get(n) if args.workload == "nanotube" else

@@ -188,7 +188,9 @@ __global__ __launch_bounds__(256) void k_gram_mfma_dd(const double *__restrict__
                                                       int64_t k, int64_t ncols, int64_t kchunk,
                                                       double *__restrict__ hi,
                                                       double *__restrict__ lo) {
-  constexpr int BM = 64, BK = 16, LP = 80;
+  // BK = 32 columns per staged step (round 6: half the barriers of 16; the MFMA k-steps and the
+  // 64-column double-double folds are the same, so the same bits)
+  constexpr int BM = 64, BK = 32, LP = 80, PL = BM * BK / 256;
   if ((int64_t)blockIdx.x > (int64_t)blockIdx.y) return;
   __shared__ double As[BK][LP];
   __shared__ double Bs[BK][LP];
@@ -208,16 +210,31 @@ __global__ __launch_bounds__(256) void k_gram_mfma_dd(const double *__restrict__
       for (int r = 0; r < 4; ++r) dacc[i][j][r] = DD{0.0, 0.0};
     }
   int stage = 0;
-  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+  // software pipeline (round 6): the next 16 columns' loads are in flight while the matrix cores
+  // work on the current ones -- the same operands in the same order, so the same bits
+  double va[PL], vb[PL];
+  auto load_stage = [&](int64_t k0) {
 #pragma unroll
-    for (int l = 0; l < 4; ++l) {
+    for (int l = 0; l < PL; ++l) {
       const int e = tid + 256 * l;
-      const int rr = e >> 4, kk = e & 15;
+      const int rr = e / BK, kk = e % BK;
       const int64_t gk = k0 + kk, ga = m0 + rr, gb = n0 + rr;
-      As[kk][rr] = (ga < k && gk < ke) ? W[ga * ldw + gk] : 0.0;
-      Bs[kk][rr] = (gb < k && gk < ke) ? W[gb * ldw + gk] : 0.0;
+      va[l] = (ga < k && gk < ke) ? W[ga * ldw + gk] : 0.0;
+      vb[l] = (gb < k && gk < ke) ? W[gb * ldw + gk] : 0.0;
+    }
+  };
+  if (kb < ke) load_stage(kb);
+  for (int64_t k0 = kb; k0 < ke; k0 += BK) {
+    __syncthreads();  // the previous stage's fragment reads are done
+#pragma unroll
+    for (int l = 0; l < PL; ++l) {
+      const int e = tid + 256 * l;
+      const int rr = e / BK, kk = e % BK;
+      As[kk][rr] = va[l];
+      Bs[kk][rr] = vb[l];
     }
     __syncthreads();
+    if (k0 + BK < ke) load_stage(k0 + BK);
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       const int kr = 4 * ks + (lane >> 4);
@@ -232,7 +249,6 @@ __global__ __launch_bounds__(256) void k_gram_mfma_dd(const double *__restrict__
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
     if (++stage == kDDChunk / BK || k0 + BK >= ke) {  // fold the chunk's fp64 partials
       stage = 0;
 #pragma unroll

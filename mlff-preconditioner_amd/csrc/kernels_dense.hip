@@ -407,6 +407,48 @@ __global__ __launch_bounds__(256) void k_potrf_diag(double *__restrict__ A, int6
   }
 }
 
+// The same diagonal block in ONE wave (round 6): lane i holds row i in registers, the column c
+// entries L[j][c] it needs come from lane j by readlane -- k_potrf_diag's operations in its order
+// (sqrt of the pivot, the column divided by it, then the right-looking fma update of the lower
+// triangle), so the same bits, without its 3 x jb workgroup barriers (83 us per 64 x 64 block at
+// k = 2701, profiles/r06/bench/nanotube_kernel_stats.txt)
+__global__ __launch_bounds__(64) void k_potrf_diag_wave(double *__restrict__ A, int64_t lda,
+                                                        int64_t j0, int jb, int *err) {
+  const int i = threadIdx.x;
+  double r[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) r[j] = (i < jb && j < jb) ? A[(j0 + i) * lda + j0 + j] : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    if (c < jb) {
+      const unsigned long long dbits = __builtin_bit_cast(unsigned long long, r[c]);
+      const double d = __builtin_bit_cast(
+          double, ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(dbits >> 32), c) << 32) |
+                      (unsigned)__builtin_amdgcn_readlane((int)(dbits & 0xffffffffull), c));
+      bad = bad || !(d > 0.0);
+      const double dc = sqrt(d);
+      if (i == c) r[c] = dc;
+      if (i > c) r[c] = r[c] / dc;
+#pragma unroll
+      for (int j = c + 1; j < 64; ++j) {
+        // L[j][c] from lane j: two v_readlane (compile-time lane) into scalar registers
+        const unsigned long long bits = __builtin_bit_cast(unsigned long long, r[c]);
+        const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(bits & 0xffffffffull), j);
+        const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(bits >> 32), j);
+        const double ljc = __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+        if (j < jb && j <= i) r[j] = fma(-r[c], ljc, r[j]);
+      }
+    }
+  }
+  if (bad && i == 0) atomicExch(err, 1);
+  if (i < jb) {
+#pragma unroll
+    for (int j = 0; j < 64; ++j)
+      if (j < jb && j <= i) A[(j0 + i) * lda + j0 + j] = r[j];
+  }
+}
+
 // Panel solve: rows i >= j0 + jb:  A[i, j0:j0+jb] <- A[i, j0:j0+jb] * L_dd^-T
 __global__ __launch_bounds__(64) void k_trsm_panel(double *__restrict__ A, int64_t lda,
                                                    int64_t k, int64_t j0, int jb) {
@@ -464,14 +506,21 @@ int potrf_lower(mlff_ctx *ctx, double *A, int64_t k, bool *ok_out) {
   MLFF_HIP(ctx, hipMemsetAsync(err, 0, sizeof(int), ctx->stream));
   for (int64_t j0 = 0; j0 < k; j0 += 64) {
     const int jb = (int)std::min<int64_t>(64, k - j0);
-    hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, k, j0, jb, err);
+    const char *e_diag = std::getenv("MLFF_POTRF_DIAG");  // 0: the workgroup form (A/B, tests)
+    const bool wave_diag = e_diag == nullptr || std::atoi(e_diag) != 0;
+    if (wave_diag)
+      hipLaunchKernelGGL(k_potrf_diag_wave, dim3(1), dim3(64), 0, ctx->stream, A, k, j0, jb, err);
+    else
+      hipLaunchKernelGGL(k_potrf_diag, dim3(1), dim3(256), 0, ctx->stream, A, k, j0, jb, err);
     const int64_t rest = k - j0 - jb;
     if (rest > 0) {
       hipLaunchKernelGGL(k_trsm_panel, dim3((unsigned)((rest + 63) / 64)), dim3(64), 0,
                          ctx->stream, A, k, k, j0, jb);
       const double *P = A + (j0 + jb) * k + j0;
+      // the lower block triangle only (tri): the upper blocks are never read and are zeroed at
+      // the end; every lower entry gets the same update (round 6: half the trailing GEMM)
       gemm_launch(false, true, rest, rest, jb, -1.0, P, k, P, k, 1.0, A + (j0 + jb) * k + j0 + jb,
-                  k, 1, 0, ctx->stream);
+                  k, 1, 0, ctx->stream, 1);
     }
   }
   launch_zero_upper(A, k, ctx->stream);

@@ -386,35 +386,39 @@ __global__ __launch_bounds__(256) void k_spec_top_part(const double *__restrict_
   }
 }
 
-// the block's candidates C[0..kSpecC): the best of the groups' kSpecGroups x kSpecPer picks, in
-// cand_before order -- each pick's rank is the number of picks before it (a strict total order:
-// ranks are distinct), counted against all 512 with LDS broadcast reads (one workgroup; round 6:
-// replaces a 45-barrier bitonic sort, 14.6 us per block on the nanotube, same C)
+// the block's candidates C[0..kSpecC): the best of the groups' kSpecGroups x kSpecPer picks,
+// by a bitonic sort of the 512 (value, row) pairs in LDS (one workgroup)
 __global__ __launch_bounds__(256) void k_spec_top_merge(const double *__restrict__ cv,
                                                         const long long *__restrict__ ci,
                                                         int64_t *__restrict__ C) {
   constexpr int n = kSpecGroups * kSpecPer;
-  static_assert(n == 512, "two picks per thread");
+  static_assert(n == 512, "two pairs per thread");
   __shared__ double sv[n];
   __shared__ long long si[n];
   for (int t = threadIdx.x; t < n; t += 256) {
     si[t] = ci[t];
     sv[t] = si[t] >= 0 ? cv[t] : -INFINITY;
   }
-  if (threadIdx.x < kSpecC) C[threadIdx.x] = -1;  // fewer than kSpecC picks: empty slots
   __syncthreads();
-  const int t0 = threadIdx.x, t1 = threadIdx.x + 256;
-  const double v0 = sv[t0], v1 = sv[t1];
-  const long long i0 = si[t0], i1 = si[t1];
-  int r0 = 0, r1 = 0;
-  for (int j = 0; j < n; ++j) {
-    const double w = sv[j];
-    const long long q = si[j];
-    r0 += cand_before(w, q, v0, i0) ? 1 : 0;
-    r1 += cand_before(w, q, v1, i1) ? 1 : 0;
-  }
-  if (i0 >= 0 && r0 < kSpecC) C[r0] = i0;
-  if (i1 >= 0 && r1 < kSpecC) C[r1] = i1;
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < n / 2; t += 256) {
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;  // this sub-sequence sorts best-first
+        const bool swap = up ? cand_before(sv[hi], si[hi], sv[lo], si[lo])
+                             : cand_before(sv[lo], si[lo], sv[hi], si[hi]);
+        if (swap) {
+          const double tv = sv[lo];
+          sv[lo] = sv[hi];
+          sv[hi] = tv;
+          const long long ti = si[lo];
+          si[lo] = si[hi];
+          si[hi] = ti;
+        }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x < kSpecC) C[threadIdx.x] = si[threadIdx.x];
 }
 
 // A[c, j] = Lt[c, C_j] for c < m0 (m0 x kSpecC, zero for an empty candidate)

@@ -228,8 +228,12 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
                                                   int nwhole, long long nunits, int nb,
                                                   int lsub,
                                                   unsigned long long *__restrict__ ticket,
-                                                  const int *__restrict__ status, PGather pg) {
+                                                  const int *__restrict__ status, PGather pg,
+                                                  unsigned long long *wgtrace = nullptr) {
   if (status != nullptr && *status != ST_RUNNING) return;
+  // MLFF_SYM_TRACE (diagnostic): per workgroup its start, end and units taken
+  if (wgtrace != nullptr && threadIdx.x == 0) wgtrace[3 * blockIdx.x] = wall_clock64();
+  long long units_done = 0;
   __shared__ double sh[6 * B + 4 * kRB * 64];
   __shared__ long long s_next;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -353,6 +357,7 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
       }
     }
     __syncthreads();  // LDS consumed, s_next read by everyone
+    ++units_done;
     if (un >= nunits) break;
     if (threadIdx.x == 0) s_next = G + (long long)atomicAdd(ticket, 1ull);
     tile = tile2;
@@ -366,6 +371,10 @@ __global__ __launch_bounds__(256) void k_symv_dyn(const double *__restrict__ til
       vrow[gb0 * kRB + i] = pg.gb != nullptr ? pg_val(pg, v, gi, beta) : v[gi];
     }
     __syncthreads();
+  }
+  if (wgtrace != nullptr && threadIdx.x == 0) {
+    wgtrace[3 * blockIdx.x + 1] = wall_clock64();
+    wgtrace[3 * blockIdx.x + 2] = (unsigned long long)units_done;
   }
 }
 
@@ -738,9 +747,58 @@ void launch_symv(const SymPack &sp, const double *v_full, double *P, const int *
   if (sp.ntiles == 0) return;
   const int64_t grid = sp.nwhole + ((sp.ntiles - sp.nwhole) << sp.lsub);
   if (sp.dyn > 0) {
-    hipLaunchKernelGGL(k_symv_dyn, dim3((unsigned)std::min<int64_t>(sp.dyn, grid)), dim3(256), 0, s,
+    const unsigned G = (unsigned)std::min<int64_t>(sp.dyn, grid);
+    // MLFF_SYM_TRACE=<n> (diagnostic): the n-th launch of the process records
+    // each workgroup's start / end / units and prints where the tile stream's time goes (the
+    // ramp until every workgroup runs, the tail after the median one is done); one sync
+    static const long long trace_at = [] {
+      const char *e = std::getenv("MLFF_SYM_TRACE");
+      return e ? std::atoll(e) : 0ll;
+    }();
+    static long long launches = 0;
+    unsigned long long *tr = nullptr;
+    if (trace_at > 0 && ++launches == trace_at &&
+        hipMalloc(&tr, sizeof(unsigned long long) * 3 * G) == hipSuccess)
+      (void)hipMemsetAsync(tr, 0, sizeof(unsigned long long) * 3 * G, s);
+    hipLaunchKernelGGL(k_symv_dyn, dim3(G), dim3(256), 0, s,
                        sp.tiles, sp.list, v_full, P, sp.Pq, sp.Np, (int)sp.nwhole, (long long)grid,
-                       (int)sp.nb, sp.lsub, sp.ticket, status, pg);
+                       (int)sp.nb, sp.lsub, sp.ticket, status, pg, tr);
+    if (tr != nullptr) {
+      std::vector<unsigned long long> h((size_t)3 * G);
+      if (hipStreamSynchronize(s) == hipSuccess &&
+          hipMemcpy(h.data(), tr, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) ==
+              hipSuccess) {
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<double> st, en, un;
+        for (unsigned g = 0; g < G; ++g) {
+          if (h[3 * g] == 0) continue;
+          t0 = std::min(t0, h[3 * g]);
+          t1 = std::max(t1, h[3 * g + 1]);
+        }
+        double idle = 0.0;
+        for (unsigned g = 0; g < G; ++g) {
+          if (h[3 * g] == 0) continue;
+          st.push_back(10.0 * (double)(h[3 * g] - t0));
+          en.push_back(10.0 * (double)(h[3 * g + 1] - t0));
+          un.push_back((double)h[3 * g + 2]);
+          idle += 10.0 * (double)(t1 - h[3 * g + 1]) + 10.0 * (double)(h[3 * g] - t0);
+        }
+        auto q = [](std::vector<double> v, double f) {
+          std::sort(v.begin(), v.end());
+          return v.empty() ? 0.0 : v[(size_t)(f * (double)(v.size() - 1))];
+        };
+        const double span = 10.0 * (double)(t1 - t0);
+        std::fprintf(stderr,
+                     "[sym trace] units %lld on %zu workgroups (units per wg p0/p50/p100 %.0f/%.0f/%.0f); "
+                     "span %.1f us; starts p50/p100 %.1f/%.1f us; ends p0/p10/p50/p90/p100 "
+                     "%.1f/%.1f/%.1f/%.1f/%.1f us; idle (ramp + tail) %.1f %% of wg-time\n",
+                     (long long)grid, st.size(), q(un, 0.0), q(un, 0.5), q(un, 1.0), 1e-3 * span,
+                     1e-3 * q(st, 0.5), 1e-3 * q(st, 1.0), 1e-3 * q(en, 0.0), 1e-3 * q(en, 0.1),
+                     1e-3 * q(en, 0.5), 1e-3 * q(en, 0.9), 1e-3 * q(en, 1.0),
+                     100.0 * idle / (span * (double)st.size()));
+      }
+      (void)hipFree(tr);
+    }
     return;
   }
   hipLaunchKernelGGL(k_symv_tiles, dim3((unsigned)grid), dim3(256), 0, s, sp.tiles, sp.list, v_full,
@@ -840,7 +898,11 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
       cus < 1)
     cus = 256;
   const int64_t C = 2 * (int64_t)cus;
-  const int64_t nwhole = (nt / C) * C;
+  int64_t nwhole = (nt / C) * C;
+  // MLFF_SYM_WHOLE_ROUNDS=<r> (A/B): at most r rounds of whole tiles, the rest split (finer units
+  // for the dynamic schedule where a rank holds only ~2 tiles per resident workgroup, W = 8)
+  if (const char *e = std::getenv("MLFF_SYM_WHOLE_ROUNDS"))
+    nwhole = std::min<int64_t>(nwhole, std::max<int64_t>(0, std::atoll(e)) * C);
   // launch schedule: k_symv_dyn (C resident workgroups taking units from a counter, next
   // unit prefetched across tile boundaries) -- measured on one MI355X: 2.51 ms at 8256
   // tiles where one-workgroup-per-unit launches took 2.51-2.61 ms (bimodal across runs),
@@ -856,7 +918,7 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
   int lsub = 2;
   if (const char *e = std::getenv("MLFF_SYM_LSUB")) {
     const int v = std::atoi(e);
-    if (v >= 2 && v <= 4) lsub = v;
+    if (v >= 1 && v <= 4) lsub = v;
   }
   const int64_t nq = ((int64_t)1 << lsub) - 1;
   int64_t dyn = C;

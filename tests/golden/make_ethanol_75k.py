@@ -14,13 +14,16 @@ this size, energy-consistent labels -- identity permutation, sig = 10, lam = 1e-
    sums).  Per step: the pivot value and the relative gap of the best two candidates.
 2. the reference's Woodbury panel (iterative_cholesky.py:141-148, one CholeskyQR step) and the
    scipy-1.7.3 CG (iterative_solver.py:995-1009) to tol 1e-6 in three operator orders (mf, mf_rev,
-   mf_split: make_noise_band.kop_variant) and with the panel's Gram matrix in 64-row chunks added
-   exactly (chunk64dd, make_nanotube_full.gram_in_order); the count to the reference's training
+   mf_split: make_noise_band.kop_variant), with the panel's Gram matrix in 64-row chunks added
+   exactly (chunk64dd, make_nanotube_full.gram_in_order) and with that Gram matrix factored and
+   substituted in 64-wide blocks (blk64: right-looking blocked Cholesky, blocked forward
+   substitution -- the device's factor orders); the count to the reference's training
    tolerance 1e-4 is each trace's first crossing of 1e-4 ||b||.  The 'mf' solve is the reference
    trajectory, the others its band.
 
 Writes tests/golden/ethanol_n74979.npz and ethanol_n74979_band.json.  CPU only: ~10 min for the
-factor (--cache keeps L: 2.25 GB), then ~2-3 h for the solves on 4 processes.
+factor (--cache keeps L: 2.25 GB), then ~1 h for the solves (each solve's result is kept next
+to the cache as it finishes, so an interrupted run resumes).
 """
 from __future__ import annotations
 
@@ -45,7 +48,7 @@ from oracle.sgdml import descriptors, kernel_column_matrix_free, kernel_diag  # 
 from sgdml_amd import synthetic  # noqa: E402  (input generation only)
 
 M, N_ATOMS, SIG, LAM, K_RANK, TOL = 2777, 9, 10.0, 1e-10, 3752, 1e-6
-JOBS = [("mf", ""), ("mf_rev", ""), ("mf_split", ""), ("mf", "chunk64dd")]
+JOBS = [("mf", ""), ("mf_rev", ""), ("mf_split", ""), ("mf", "chunk64dd"), ("mf", "blk64")]
 _G = {}
 
 
@@ -87,13 +90,49 @@ def pivoted_cholesky_colmajor(get_col, diagonal, max_rank):
     return L, index_columns, piv_val, gap
 
 
-def panel(L, lam, gram):
-    """T = chol(lam I + L^T L)^-1 L^T (iterative_cholesky.py:141-143), Gram in `gram` order."""
+def _chol_blocked(A, nb):
+    """Right-looking blocked Cholesky (lower) in nb-wide panels."""
     import scipy.linalg
 
+    A = np.array(A, copy=True)
+    k = A.shape[0]
+    for j0 in range(0, k, nb):
+        j1 = min(j0 + nb, k)
+        A[j0:j1, j0:j1] = np.linalg.cholesky(A[j0:j1, j0:j1])
+        if j1 < k:
+            A[j1:, j0:j1] = scipy.linalg.solve_triangular(A[j0:j1, j0:j1], A[j1:, j0:j1].T,
+                                                          lower=True).T
+            A[j1:, j1:] -= A[j1:, j0:j1] @ A[j1:, j0:j1].T
+    return np.tril(A)
+
+
+def _trsm_blocked(L2, B, nb):
+    """L2^-1 B by blocked forward substitution in nb-row blocks."""
+    import scipy.linalg
+
+    T = np.empty_like(B)
+    for j0 in range(0, B.shape[0], nb):
+        j1 = min(j0 + nb, B.shape[0])
+        rhs = B[j0:j1] - L2[j0:j1, :j0] @ T[:j0] if j0 else B[j0:j1]
+        T[j0:j1] = scipy.linalg.solve_triangular(L2[j0:j1, j0:j1], rhs, lower=True)
+    return T
+
+
+def panel(L, lam, gram):
+    """T = chol(lam I + L^T L)^-1 L^T (iterative_cholesky.py:141-143), Gram in `gram` order;
+    'blk64' = the chunk64dd Gram factored and substituted in 64-wide blocks."""
+    import scipy.linalg
+
+    if gram == "blk64":
+        G = lam * np.eye(L.shape[1]) + gram_in_order(L, "chunk64dd")
+        return _trsm_blocked(_chol_blocked(G, 64), np.ascontiguousarray(L.T), 64)
     G = gram_in_order(L, gram) if gram else L.T @ L
     L2 = scipy.linalg.cholesky(lam * np.eye(L.shape[1]) + G, lower=True)
     return scipy.linalg.solve_triangular(L2, L.T, lower=True)
+
+
+def _name(job):
+    return job[0] if not job[1] else f"panel_{job[1]}"
 
 
 def _solve(job):
@@ -103,13 +142,14 @@ def _solve(job):
     Rd, Rdd, perms, y = _G["Rd"], _G["Rdd"], _G["perms"], _G["y"]
     t0 = time.time()
     with threadpoolctl.threadpool_limits(limits=2, user_api="blas"):
-        T = _G["T"] if not gram else panel(_G["L"], LAM, gram)
-        mvK = kop_variant(Rd, Rdd, perms, SIG, order)
+        T = _G["T"][gram]
+        mvK = kop_variant(Rd, Rdd, perms, SIG, order, threads=_G["threads"])
         psolve = lambda r: (r - T.T @ (T @ r)) / LAM  # noqa: E731
         x, info, tr, it = cg_legacy(lambda v: -mvK(v) + LAM * v, y, tol=TOL, maxiter=5 * y.size,
                                     psolve=psolve)
-    name = order if not gram else f"panel_{gram}"
-    print(f"solve {name:16s} iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
+    print(f"solve {_name(job):16s} iters {it} info {info} ({time.time() - t0:.0f} s)", flush=True)
+    if _G["keep"] is not None:
+        np.savez(_G["keep"](job), x=x, info=info, tr=tr, it=it)
     return job, x, info, tr, it
 
 
@@ -139,10 +179,21 @@ def main(cache, procs):
     print(f"pivoted Cholesky k={K_RANK}: {time.time() - t_all:.0f} s, min gap {gap.min():.3g}",
           flush=True)
     L = np.ascontiguousarray(L)
-    _G.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, L=L, T=panel(L, LAM, ""))
+    keep = None if cache is None else (lambda job: Path(cache).with_name(
+        Path(cache).stem + f"_{_name(job)}.npz"))
+    done, todo = [], []
+    for job in JOBS:
+        if keep is not None and keep(job).exists():
+            r = np.load(keep(job), allow_pickle=False)
+            done.append((job, r["x"], int(r["info"]), r["tr"], int(r["it"])))
+        else:
+            todo.append(job)
+    T = {g: panel(L, LAM, g) for g in sorted({g for _, g in todo})}
+    print(f"panels {sorted(T)}: {time.time() - t_all:.0f} s", flush=True)
+    _G.update(Rd=Rd, Rdd=Rdd, perms=perms, y=y, T=T, threads=max(1, 8 // procs), keep=keep)
     with mp.get_context("fork").Pool(procs) as pool:
-        results = pool.map(_solve, JOBS, chunksize=1)
-    runs = {(o if not g else f"panel_{g}"): (x, info, tr, it) for (o, g), x, info, tr, it in results}
+        results = done + pool.map(_solve, todo, chunksize=1)
+    runs = {_name(job): (x, info, tr, it) for job, x, info, tr, it in results}
     x0, info0, tr0, it0 = runs["mf"]
     out = {"n": n, "M": M, "k": K_RANK, "lam": LAM, "sig": SIG, "ref_order": "mf",
            "first_gap_below_1e-12": int(np.argmax(gap < 1e-12)) if np.any(gap < 1e-12) else None,
@@ -184,6 +235,6 @@ if __name__ == "__main__":
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--cache", default=None, help=".npz outside the repository for L (2.25 GB)")
-    ap.add_argument("--procs", type=int, default=4)
+    ap.add_argument("--procs", type=int, default=2)
     a = ap.parse_args()
     main(a.cache, a.procs)

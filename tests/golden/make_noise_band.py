@@ -100,9 +100,11 @@ def panel(f, precon, K, lam):
     return nystrom_panel(S[:, idx], idx, lam, 1 if precon.endswith("_custom") else 0)
 
 
-def kop_variant(Rd, Rdd, perms, sig, order):
+def kop_variant(Rd, Rdd, perms, sig, order, threads=1):
     """v -> K v by the reference's matrix-free formulation (predict.py:72-234, restated in
-    oracle.sgdml.kernel_matvec_matrix_free) in a given summation order."""
+    oracle.sgdml.kernel_matvec_matrix_free) in a given summation order.  `threads` > 1 splits the
+    independent output rows i over a thread pool (numpy releases the GIL in the per-row array
+    work); every y[i] keeps its summation order, so the result is bitwise the same."""
     from oracle.sgdml import desc_perm
 
     M, D = Rd.shape
@@ -128,7 +130,21 @@ def kop_variant(Rd, Rdd, perms, sig, order):
         Zt = z[:, P][jorder]                                  # j order of the sums
         Rtj = Rt[jorder]
         y = np.empty((M, n, 3))
-        for i in range(M):
+
+        def rows(i0, i1):
+            for i in range(i0, i1):
+                row(i, Zt, Rtj, y)
+        if threads > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            edges = np.linspace(0, M, 4 * threads + 1).astype(int)
+            with ThreadPoolExecutor(threads) as ex:
+                list(ex.map(lambda ab: rows(*ab), zip(edges[:-1], edges[1:])))
+        else:
+            rows(0, M)
+        return y.reshape(-1)
+
+    def row(i, Zt, Rtj, y):
+        if True:
             diff = Rd[i][None, None, :] - Rtj                 # M x n_perms x D
             norm = sqrt5 * np.sqrt(dot_d(diff, diff))
             m = np.exp(-norm / sig) * 5.0 / (3.0 * sig ** 4)
@@ -146,7 +162,6 @@ def kop_variant(Rd, Rdd, perms, sig, order):
             np.add.at(yi, t_at, contrib)
             np.add.at(yi, s_at, -contrib)
             y[i] = yi
-        return y.reshape(-1)
     return mv
 
 

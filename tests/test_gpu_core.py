@@ -451,3 +451,28 @@ def test_woodbury_refine_steps(sg, monkeypatch, steps):
         assert np.linalg.eigvalsh(T @ T.T).max() <= 1.0 + 1e-12, st
     d = np.abs(panels[steps].T @ panels[steps] - panels["1"].T @ panels["1"]).max()
     assert d <= 1e-12, d
+
+
+@pytest.mark.parametrize("k", [1, 13, 64, 200, 2701])
+def test_potrf_wave_diag_bitwise(sg, monkeypatch, k):
+    """The Woodbury build's Cholesky with the one-wave diagonal-block kernel (k_potrf_diag_wave,
+    default) against the workgroup form (MLFF_POTRF_DIAG=0): the same operations in the same
+    order, so the panel is bit-identical (and equals the LAPACK-pinned formula to rounding)."""
+    n = max(3 * k, 600)
+    rng = np.random.default_rng(k)
+    L = rng.standard_normal((n, k)) * np.logspace(0, -2, k)
+    X, _ = _rbf(n)
+    panels = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MLFF_POTRF_DIAG", mode)
+        with sg.KernelSolver(n) as s:
+            s.gen_rbf(X, 0.2)
+            s.set_operator(1.0, 1e-6)
+            s.precon_lowrank(np.ascontiguousarray(L.T))
+            panels[mode] = s.precon_panel()
+    np.testing.assert_array_equal(panels["1"], panels["0"])
+    import scipy.linalg
+
+    L2 = scipy.linalg.cholesky(1e-6 * np.eye(k) + L.T @ L, lower=True)
+    T = scipy.linalg.solve_triangular(L2, L.T, lower=True)
+    assert np.abs(panels["1"].T @ panels["1"] - T.T @ T).max() <= 1e-9
