@@ -205,16 +205,22 @@ __device__ __forceinline__ double gathered_rho(const PGather &pg, double *sh) {
 }
 
 // operand entries of the fused form: p = fma(beta, p_old, z) (z at iteration 1), z from the
-// gather buffer -- k_update_p_gathered's arithmetic, the same bits
+// gather buffer -- k_update_p_gathered's arithmetic, the same bits.  Entries past the ranks'
+// blocks (one rank: blk = round_up(n, 64) < Np = round_up(n, 512), the tile padding) are zero,
+// as the unfused operand's padding is: the gather buffer holds world blocks only.  blk is a
+// multiple of 64, so a d2 pair never straddles two blocks.
 __device__ __forceinline__ double pg_z(const PGather &pg, int64_t i) {
-  return pg.gb[(i / pg.blk) * pg.gstride + i % pg.blk];
+  const int64_t rk = i / pg.blk;
+  return rk < pg.world ? pg.gb[rk * pg.gstride + i % pg.blk] : 0.0;
 }
 __device__ __forceinline__ double pg_val(const PGather &pg, const double *v, int64_t i, double beta) {
   return pg.it > 1 ? fma(beta, v[i], pg_z(pg, i)) : pg_z(pg, i);
 }
 __device__ __forceinline__ d2 pg_val2(const PGather &pg, const double *v, int64_t i, double beta) {
   if (pg.gb == nullptr) return *reinterpret_cast<const d2 *>(v + i);
-  const d2 z = *reinterpret_cast<const d2 *>(pg.gb + (i / pg.blk) * pg.gstride + i % pg.blk);
+  const int64_t rk = i / pg.blk;
+  const d2 z = rk < pg.world ? *reinterpret_cast<const d2 *>(pg.gb + rk * pg.gstride + i % pg.blk)
+                             : d2{0.0, 0.0};
   if (pg.it <= 1) return z;
   const d2 po = *reinterpret_cast<const d2 *>(v + i);
   return d2{fma(beta, po.x, z.x), fma(beta, po.y, z.y)};
