@@ -63,6 +63,12 @@ struct SymPack {
   double *Pq = nullptr;
   unsigned char *split = nullptr;  // nb x nb: tile (I, J) is split
   int *own = nullptr;              // nb x nb owned slots per row block + nb counts (W > 1)
+  // the same slots as a flat load list per row block (W > 1, k_sym_reduce_wl): entry
+  // t | plane << 16 (plane 0 = P, h >= 1 = Pq plane h - 1; a split slot's planes follow it),
+  // pstride entries per row block, then nb counts; pmax = the largest count
+  int *plist = nullptr;
+  int64_t pstride = 0;
+  int pmax = 0;
   int64_t t_split = 0;             // smallest I of a split tile (nb if none)
   int64_t dyn = 0;                 // > 0: k_symv_dyn with this many workgroups
   unsigned long long *ticket = nullptr;  // its work counter (reset by the slot reduction)

@@ -619,6 +619,195 @@ __global__ __launch_bounds__(256) void k_sym_reduce_w(const double *__restrict__
   }
 }
 
+// k_sym_reduce_w with the slot loads of a row all in flight (round 6): at
+// W = 8 a rank's own row blocks hold 72 slots (+ the split tiles' planes) against 8 elsewhere,
+// and k_sym_reduce_w took them as 5 dependent batches of 16, each behind a scalar load of its
+// slot entries and a wait per split plane -- 25 us of the 0.38 ms per-rank step.  Here the
+// workgroup's row block (256 rows lie in one 512-row block) stages its flat load list (every
+// slot and, after a split slot, its planes: SymPack::plist) in LDS once, and a row's loads go
+// out in batches of kRwBatch with the next batch in flight while the current one is added:
+// unconditional loads (entries past the count re-read the last one), the additions in list
+// order -- each slot ((P + Pq0) + Pq1) + ..., the slots in ascending order: k_sym_reduce_w's
+// sums, the same bits (MLFF_SYM_REDUCE_LIST=0 restores it; test_sym_reduce_list_bitwise)
+constexpr int kRwBatch = 32;
+constexpr int kRwMaxList = 2048;
+
+template <bool PQ>
+__global__ __launch_bounds__(256) void k_sym_reduce_wl(const double *__restrict__ P,
+                                                       const double *__restrict__ Pq,
+                                                       int64_t Np, int nb,
+                                                       const int *__restrict__ plist,
+                                                       int64_t pstride, int rank,
+                                                       int64_t ld, int64_t blk, int64_t bstride,
+                                                       double *__restrict__ yg, double *p,
+                                                       double *__restrict__ pq_part,
+                                                       double *__restrict__ pp_part,
+                                                       unsigned long long *__restrict__ ticket,
+                                                       const int *__restrict__ status,
+                                                       PGather pg, PqPublish pub) {
+  if (status != nullptr && *status != ST_RUNNING) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0ull;  // k_symv_dyn's counter
+  __shared__ double sh[8];
+  __shared__ int s_last;
+  __shared__ int sl[kRwMaxList];
+  double apq = 0.0, app = 0.0;
+  double beta = 0.0;
+  if (PQ && pg.gb != nullptr) {
+    const double rho = pg.st->rho_new;
+    if (pg.it > 1) beta = rho / pg.st->rho1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) pg.st->rho = rho;
+  }
+  const int64_t lo = (int64_t)rank * blk, hi = lo + blk;
+  const int64_t plane = (int64_t)nb * Np;
+  for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < ld; c0 += (int64_t)gridDim.x * 256) {
+    const int64_t i = c0 + threadIdx.x;
+    const int bi = (int)(c0 / B);  // the workgroup's 256 rows lie in one row block
+    // the list, its count and the p update's operands are requested together (none waits for
+    // another): the list's whole stride (entries past the count are zeros, slot 0 of P)
+    const int cnt = plist[(int64_t)nb * pstride + bi];
+    int le[kRwMaxList / 256];
+#pragma unroll
+    for (int q = 0; q < kRwMaxList / 256; ++q) {
+      const int e = threadIdx.x + 256 * q;
+      le[q] = e < pstride ? plist[(int64_t)bi * pstride + e] : 0;
+    }
+    double pz = 0.0, pold = 0.0;
+    if (PQ && i < ld) {
+      if (pg.gb != nullptr) {
+        pz = pg_z(pg, i);
+        if (pg.it > 1) pold = p[i];
+      } else {
+        pold = p[i];
+      }
+    }
+    __syncthreads();  // the previous chunk's list reads are done
+#pragma unroll
+    for (int q = 0; q < kRwMaxList / 256; ++q)
+      if (threadIdx.x + 256 * q < pstride) sl[threadIdx.x + 256 * q] = le[q];
+    __syncthreads();
+    // a batch's list entries one per lane (lane & 31), read out with v_readlane: no LDS round
+    // trip between a batch's loads
+    const int lane32 = (int)(threadIdx.x & 31);
+    auto entries = [&](int e0) { return sl[e0 + lane32 < cnt ? e0 + lane32 : cnt - 1]; };
+    auto load = [&](int ent, int u) {
+      const int x = __builtin_amdgcn_readlane(ent, u);
+      const int h = x >> 16;
+      const double *base = h == 0 ? P : Pq + (int64_t)(h - 1) * plane;
+      return base[(int64_t)(x & 0xffff) * Np + i];
+    };
+    double s = 0.0, cur = 0.0;
+    if (cnt > 0 && i < ld) {
+      double v[kRwBatch];
+      int ev = entries(0);
+#pragma unroll
+      for (int u = 0; u < kRwBatch; ++u) v[u] = load(ev, u);
+      for (int e0 = 0; e0 < cnt; e0 += kRwBatch) {
+        double w[kRwBatch];
+        const int ew = entries(e0 + kRwBatch < cnt ? e0 + kRwBatch : e0);
+        if (e0 + kRwBatch < cnt) {  // uniform: the whole next batch in flight
+#pragma unroll
+          for (int u = 0; u < kRwBatch; ++u) w[u] = load(ew, u);
+        } else {
+#pragma unroll
+          for (int u = 0; u < kRwBatch; ++u) w[u] = 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kRwBatch; ++u) {
+          if (e0 + u < cnt) {
+            if (__builtin_amdgcn_readlane(ev, u) >> 16) {
+              cur += v[u];  // a split slot's next plane
+            } else {
+              s += cur;  // the previous slot is complete
+              cur = v[u];
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kRwBatch; ++u) v[u] = w[u];
+        ev = ew;
+      }
+    }
+    s += cur;
+    if (i >= ld) continue;
+    yg[(i / blk) * bstride + i % blk] = s;
+    if (PQ) {
+      double pv;
+      if (pg.gb != nullptr) {  // pg_val's arithmetic on the operands loaded above
+        pv = pg.it > 1 ? fma(beta, pold, pz) : pz;
+        p[i] = pv;
+      } else {
+        pv = pold;
+      }
+      apq = fma(pv, s, apq);
+      if (i >= lo && i < hi) app = fma(pv, pv, app);
+    }
+  }
+  if (PQ) {
+    double t = apq;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_down(t, o, 64);
+    double u = app;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) u += __shfl_down(u, o, 64);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+      sh[w] = t;
+      sh[4 + w] = u;
+    }
+    __syncthreads();
+    // the last-arriving workgroup publishes this rank's share.  Each workgroup's two partials are
+    // stored write-through (sc1: agent-scope relaxed atomic stores) and drained before its ticket
+    // add, and the last arriver reads them with sc1 loads only, so no agent-scope release fence
+    // (an L2 write-back per workgroup: k_sym_reduce_w's form) and no acquire are needed
+    // (cdna_hip_programming.md Guideline 16, R1 / the counter form)
+    if (threadIdx.x == 0) {
+      const double a0 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+      const double b0 = (sh[4] + sh[5]) + (sh[6] + sh[7]);
+      if (pub.world > 0) {
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(pq_part) + blockIdx.x,
+                           __builtin_bit_cast(unsigned long long, a0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(pp_part) + blockIdx.x,
+                           __builtin_bit_cast(unsigned long long, b0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = __hip_atomic_fetch_add(ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned long long)(gridDim.x - 1);
+      } else {
+        pq_part[blockIdx.x] = a0;
+        pp_part[blockIdx.x] = b0;
+      }
+    }
+    if (pub.world == 0) return;  // the separate k_pq_publish launch follows
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no loads above the ticket
+    const int np = (int)gridDim.x;
+    double a = 0.0, b = 0.0;
+    for (int q = threadIdx.x; q < np; q += 256) {
+      a += __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long *>(pq_part) + q,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      b += __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<unsigned long long *>(pp_part) + q,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_down(a, o, 64);
+      b += __shfl_down(b, o, 64);
+    }
+    __syncthreads();
+    if (lane == 0) {
+      sh[w] = a;
+      sh[4 + w] = b;
+    }
+    __syncthreads();
+    const double share = pub.sigma * ((sh[0] + sh[1]) + (sh[2] + sh[3])) +
+                         pub.lam * ((sh[4] + sh[5]) + (sh[6] + sh[7]));
+    for (int g = threadIdx.x; g < pub.world; g += 256) yg[(int64_t)g * bstride + blk + rank] = share;
+    if (threadIdx.x == 0) __hip_atomic_store(ticket + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // s_rank = sigma * sum(pq_part) + lam * sum(pp_part) (this rank's share of p.q), put
 // into tail slot `rank` of every rank block of the reduce-scatter operand; the other
 // tail slots stay zero, so the reduce-scatter hands every rank the exact vector of
@@ -834,6 +1023,12 @@ void launch_sym_reduce_pq(const SymPack &sp, int64_t n_out, double *y, double si
                      sp.ticket, status, pg, pg.gb != nullptr ? const_cast<double *>(p) : nullptr);
 }
 
+// k_sym_reduce_wl unless MLFF_SYM_REDUCE_LIST=0 at the operator's build (A/B: k_sym_reduce_w);
+// the list form needs the row block's list in LDS (kRwMaxList)
+static bool sym_reduce_list(const SymPack &sp) {
+  return sp.plist != nullptr && sp.pstride <= kRwMaxList && sp.nb <= 0xffff;
+}
+
 void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk,
                              const double *p_full, double *pq_part, double *pp_part,
                              double sigma, double lam, const int *status, hipStream_t s,
@@ -841,26 +1036,32 @@ void launch_sym_reduce_ranks(const SymPack &sp, int rank, int world, int64_t blk
   const int64_t ld = (int64_t)world * blk;
   const dim3 grid(kVecGrid);
   double *pw = const_cast<double *>(p_full);  // written only when the p update is fused
-  if (p_full == nullptr) {
+  const PqPublish pub = p_full == nullptr ? PqPublish{}
+                                          : PqPublish{sigma, lam, separate_publish ? 0 : world};
+  const PGather pgu = p_full == nullptr ? PGather{} : pg;
+  if (sym_reduce_list(sp)) {
+    if (p_full == nullptr)
+      hipLaunchKernelGGL((k_sym_reduce_wl<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.Np,
+                         (int)sp.nb, sp.plist, sp.pstride, rank, ld, blk, sp.ystride, sp.yg, pw,
+                         pq_part, pp_part, sp.ticket, status, pgu, pub);
+    else
+      hipLaunchKernelGGL((k_sym_reduce_wl<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.Np,
+                         (int)sp.nb, sp.plist, sp.pstride, rank, ld, blk, sp.ystride, sp.yg, pw,
+                         pq_part, pp_part, sp.ticket, status, pgu, pub);
+  } else if (p_full == nullptr) {
     hipLaunchKernelGGL((k_sym_reduce_w<false>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (1 << sp.lsub) - 1, (int)sp.nb, rank,
                        sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
                        sp.ticket, status, PGather{}, PqPublish{});
-    return;
-  }
-  if (!separate_publish) {  // MLFF_PQ_PUBLISH=1 (ctx->pq_publish): the separate launch (A/B)
+  } else {
     hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
                        (1 << sp.lsub) - 1, (int)sp.nb, rank,
                        sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
-                       sp.ticket, status, pg, PqPublish{sigma, lam, world});
-    return;
+                       sp.ticket, status, pg, pub);
   }
-  hipLaunchKernelGGL((k_sym_reduce_w<true>), grid, dim3(256), 0, s, sp.P, sp.Pq, sp.split, sp.Np,
-                     (1 << sp.lsub) - 1, (int)sp.nb, rank,
-                     sp.own, ld, blk, sp.ystride, sp.yg, pw, pq_part, pp_part,
-                     sp.ticket, status, pg, PqPublish{sigma, lam, 0});
-  hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
-                     rank, world, blk, sp.ystride, sp.yg, status);
+  if (p_full != nullptr && separate_publish)  // MLFF_PQ_PUBLISH=1 (ctx->pq_publish): A/B
+    hipLaunchKernelGGL(k_pq_publish, dim3(1), dim3(256), 0, s, pq_part, pp_part, kVecGrid, sigma, lam,
+                       rank, world, blk, sp.ystride, sp.yg, status);
 }
 
 void launch_axpby_loc(const double *src, double *y, int64_t n, double sigma, double lam,
@@ -986,6 +1187,34 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
       own[(size_t)nb * nb + bi] = c;
     }
     MLFF_HIP(ctx, hipMemcpyAsync(sp.own, own.data(), sizeof(int) * own.size(), hipMemcpyHostToDevice, s));
+    // the flat load list of k_sym_reduce_wl: each owned slot, a split slot followed by its planes;
+    // row blocks at a stride of the longest list (rounded to 64 entries)
+    std::vector<std::vector<int>> lists((size_t)nb);
+    sp.pmax = 0;
+    for (int bi = 0; bi < nb; ++bi) {
+      for (int j = 0; j < own[(size_t)nb * nb + bi]; ++j) {
+        const int e = own[(size_t)bi * nb + j];
+        const int t = e & (kOwnSplit - 1);
+        lists[bi].push_back(t);
+        if (e & kOwnSplit)
+          for (int h = 1; h <= nq; ++h) lists[bi].push_back(t | (h << 16));
+      }
+      sp.pmax = std::max(sp.pmax, (int)lists[bi].size());
+    }
+    sp.pstride = round_up(std::max(sp.pmax, 1), 64);
+    std::vector<int> plist((size_t)nb * (sp.pstride + 1), 0);
+    for (int bi = 0; bi < nb; ++bi) {
+      std::copy(lists[bi].begin(), lists[bi].end(), plist.begin() + (size_t)bi * sp.pstride);
+      plist[(size_t)nb * sp.pstride + bi] = (int)lists[bi].size();
+    }
+    if (sp.plist != nullptr) (void)hipFree(sp.plist);
+    sp.plist = nullptr;
+    const char *rl = std::getenv("MLFF_SYM_REDUCE_LIST");
+    if (ctx->world > 1 && (rl == nullptr || std::atoi(rl) != 0)) {
+      MLFF_HIP(ctx, hipMalloc(&sp.plist, sizeof(int) * plist.size()));
+      MLFF_HIP(ctx, hipMemcpyAsync(sp.plist, plist.data(), sizeof(int) * plist.size(),
+                                   hipMemcpyHostToDevice, s));
+    }
     MLFF_HIP(ctx, hipStreamSynchronize(s));
   }
   unsigned char *dtrans = nullptr;
@@ -1029,9 +1258,12 @@ int sym_build(mlff_ctx *ctx, bool check_symmetry, bool *symmetric_out) {
 
 void sym_free(SymPack &sp) {
   for (void *p : {(void *)sp.tiles, (void *)sp.list, (void *)sp.P, (void *)sp.yg, (void *)sp.yr,
-                  (void *)sp.Pq, (void *)sp.split, (void *)sp.ticket, (void *)sp.own})
+                  (void *)sp.Pq, (void *)sp.split, (void *)sp.ticket, (void *)sp.own,
+                  (void *)sp.plist})
     if (p) (void)hipFree(p);
   sp.own = nullptr;
+  sp.plist = nullptr;
+  sp.pmax = 0;
   sp.Pq = nullptr;
   sp.split = nullptr;
   sp.ticket = nullptr;

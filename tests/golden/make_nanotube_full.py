@@ -109,10 +109,13 @@ GRAM_ORDERS = ("rev", "blk8", "chunk64dd", "pair", "ld")
 
 def _dd_accumulate(parts):
     """fl(sum of fp64 matrices) with every addition exact (TwoSum into a double-double
-    accumulator, rounded once): the outer sum of a blocked Gram as k_gram_mfma_dd forms it."""
-    hi = np.zeros_like(parts[0])
-    lo = np.zeros_like(parts[0])
+    accumulator, rounded once): the outer sum of a blocked Gram as k_gram_mfma_dd forms it.
+    parts may be a generator (one k x k partial in memory at a time: 1172 of them at N = 74979)."""
+    hi = lo = None
     for p in parts:
+        if hi is None:
+            hi = np.zeros_like(p)
+            lo = np.zeros_like(p)
         s = hi + p
         bp = s - hi
         lo += (hi - (s - bp)) + (p - bp)
@@ -129,7 +132,7 @@ def gram_in_order(L, order):
     if order == "blk8":
         return sum(L[b].T @ L[b] for b in np.array_split(np.arange(L.shape[0]), 8))
     if order == "chunk64dd":  # 64-row chunks in fp64, the chunk partials added exactly
-        return _dd_accumulate([L[a:a + 64].T @ L[a:a + 64] for a in range(0, L.shape[0], 64)])
+        return _dd_accumulate(L[a:a + 64].T @ L[a:a + 64] for a in range(0, L.shape[0], 64))
     if order == "pair":  # pairwise over row halves down to 128-row leaves
         def pw(A):
             if A.shape[0] <= 128:

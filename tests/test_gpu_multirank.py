@@ -170,6 +170,29 @@ def test_sharded_pq_publish_folded_bitwise(world, precon, monkeypatch):
         np.testing.assert_array_equal(a["x"], b["x"])
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world,precon,n,lsub", [(2, "nystrom", 1003, "2"), (3, "pivchol", 1003, "2"),
+                                                 (8, "nystrom", 1003, "2"), (3, "nystrom", 1003, "4"),
+                                                 (4, "none", 9000, "2")])
+def test_sharded_sym_reduce_list_bitwise(world, precon, n, lsub, monkeypatch):
+    """The owned-slot reduction from the flat load list (k_sym_reduce_wl, default since round 6:
+    a row's slot and split-plane loads in batches of 32 with the next batch in flight) against
+    k_sym_reduce_w (MLFF_SYM_REDUCE_LIST=0, read at the operator's build): the same additions
+    in the same order, so iterates, residual curve and stop decisions are bit-identical.  Below
+    one round of resident workgroups every tile is split, so every slot carries 3 (lsub 2) or
+    15 (lsub 4) planes."""
+    monkeypatch.setenv("MLFF_SYM_LSUB", lsub)
+    out = {}
+    for lst in ("1", "0"):
+        monkeypatch.setenv("MLFF_SYM_REDUCE_LIST", lst)
+        out[lst] = run_ranks(world, lambda r, w, key: solve_case(r, w, key, n, precon))
+    for a, b in zip(out["1"], out["0"]):
+        assert a["iters"] == b["iters"] and a["info"] == b["info"] == 0
+        np.testing.assert_array_equal(a["trace"], b["trace"])
+        np.testing.assert_array_equal(a["x"], b["x"])
+        np.testing.assert_array_equal(a["y"], b["y"])
+
+
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("world,precon,n", [(2, "nystrom", 1003), (3, "pivchol", 1003),
                                             (8, "nystrom", 1003), (2, "nystrom", 9000),
