@@ -386,39 +386,62 @@ __global__ __launch_bounds__(256) void k_spec_top_part(const double *__restrict_
   }
 }
 
-// the block's candidates C[0..kSpecC): the best of the groups' kSpecGroups x kSpecPer picks,
-// by a bitonic sort of the 512 (value, row) pairs in LDS (one workgroup)
+// the block's candidates C[0..kSpecC): the best of the groups' kSpecGroups x kSpecPer picks in
+// candidate order, by rank counting: the (value, row) pairs are distinct rows, so cand_before is
+// a strict total order on them and a pair's rank -- how many pairs precede it -- is its position
+// in the sorted list; a pair ranked below kSpecC writes C[rank], and workgroup 0 writes -1 to the
+// slots past the non-empty count.  kSpecMergeWG workgroups of 64 pairs each (a wave per quarter
+// of the pairs they are compared with): the same C as a full sort of the 512 pairs.  Round 5's
+// one-workgroup bitonic network took 30 us per speculative block on the nanotube (5 ms of the
+// k = 2701 build): 512 x 512 comparisons on one CU are its VALU time, whatever the network
+constexpr int kSpecMergeWG = kSpecGroups * kSpecPer / 64;
 __global__ __launch_bounds__(256) void k_spec_top_merge(const double *__restrict__ cv,
                                                         const long long *__restrict__ ci,
                                                         int64_t *__restrict__ C) {
   constexpr int n = kSpecGroups * kSpecPer;
-  static_assert(n == 512, "two pairs per thread");
+  static_assert(n == 512 && n % 64 == 0, "two pairs per thread");
   __shared__ double sv[n];
   __shared__ long long si[n];
-  for (int t = threadIdx.x; t < n; t += 256) {
-    si[t] = ci[t];
-    sv[t] = si[t] >= 0 ? cv[t] : -INFINITY;
+  __shared__ int part[4][64];
+  __shared__ int s_ne;
+  if (threadIdx.x == 0) s_ne = 0;
+  // an empty slot (row < 0; its value was never written) as (-inf, max row): after every pair
+  long long li[2];
+  double lv[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    li[h] = ci[threadIdx.x + 256 * h];
+    lv[h] = cv[threadIdx.x + 256 * h];
   }
+  __syncthreads();  // s_ne
+  int ne = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const bool ok = li[h] >= 0;
+    sv[threadIdx.x + 256 * h] = ok ? lv[h] : -INFINITY;
+    si[threadIdx.x + 256 * h] = ok ? li[h] : LLONG_MAX;
+    ne += ok ? 1 : 0;
+  }
+  if (blockIdx.x == 0 && ne > 0) atomicAdd(&s_ne, ne);  // an integer count: any order
   __syncthreads();
-  for (int size = 2; size <= n; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < n / 2; t += 256) {
-        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-        const bool up = (lo & size) == 0;  // this sub-sequence sorts best-first
-        const bool swap = up ? cand_before(sv[hi], si[hi], sv[lo], si[lo])
-                             : cand_before(sv[lo], si[lo], sv[hi], si[hi]);
-        if (swap) {
-          const double tv = sv[lo];
-          sv[lo] = sv[hi];
-          sv[hi] = tv;
-          const long long ti = si[lo];
-          si[lo] = si[hi];
-          si[hi] = ti;
-        }
-      }
-      __syncthreads();
-    }
-  if (threadIdx.x < kSpecC) C[threadIdx.x] = si[threadIdx.x];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const double v = sv[e];
+  const long long i = si[e];
+  int r = 0;
+#pragma unroll 8
+  for (int f = q * (n / 4); f < (q + 1) * (n / 4); ++f) {
+    const double w = sv[f];
+    const long long j = si[f];
+    r += (w > v || (w == v && j < i)) ? 1 : 0;
+  }
+  part[q][lane] = r;
+  __syncthreads();
+  if (q == 0) {
+    r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (i != LLONG_MAX && r < kSpecC) C[r] = i;
+    if (blockIdx.x == 0 && lane < kSpecC && lane >= s_ne) C[lane] = -1;
+  }
 }
 
 // A[c, j] = Lt[c, C_j] for c < m0 (m0 x kSpecC, zero for an empty candidate)
@@ -1121,7 +1144,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
         } else {
           hipLaunchKernelGGL(k_spec_top_part, dim3(kSpecGroups), dim3(256), 0, s, ctx->dwork,
                              ctx->pivflag, nrows, cv, ci);
-          hipLaunchKernelGGL(k_spec_top_merge, dim3(1), dim3(256), 0, s, (const double *)cv,
+          hipLaunchKernelGGL(k_spec_top_merge, dim3(kSpecMergeWG), dim3(256), 0, s, (const double *)cv,
                              (const long long *)ci, Cspec);
           hipLaunchKernelGGL(k_spec_gather, dim3((unsigned)std::min<int64_t>((m * kSpecC + 255) / 256, 4096)),
                              dim3(256), 0, s, ctx->T, blk, m, Cspec, Aspec);
@@ -1220,7 +1243,7 @@ int pivoted_cholesky(mlff_ctx *ctx, int64_t k, int64_t *index_columns_out) {
       spec_m0 = m;
       hipLaunchKernelGGL(k_spec_top_part, dim3(kSpecGroups), dim3(256), 0, s, ctx->dwork,
                          ctx->pivflag, nrows, cv, ci);
-      hipLaunchKernelGGL(k_spec_top_merge, dim3(1), dim3(256), 0, s, (const double *)cv,
+      hipLaunchKernelGGL(k_spec_top_merge, dim3(kSpecMergeWG), dim3(256), 0, s, (const double *)cv,
                          (const long long *)ci, Cspec);
       hipLaunchKernelGGL(k_spec_gather, dim3((unsigned)std::min<int64_t>((m * kSpecC + 255) / 256, 4096)),
                          dim3(256), 0, s, ctx->T, blk, m, Cspec, Aspec);
