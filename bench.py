@@ -131,6 +131,9 @@ def parse():
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="--gpus N > 1 without WORLD_SIZE: seconds the self-launched ranks may "
                          "take before they are stopped (exit 124)")
+    ap.add_argument("--desc", choices=["host", "gpu"], default="host",
+                    help="sGDML descriptors on the host as the reference's trainer forms them "
+                         "(default) or on the device")
     ap.add_argument("--mf-form", choices=["pt", "rec", "pair"], default=None,
                     help="matrix-free sGDML operator form (MLFF_MF_FORM): pair-tile (few atoms), "
                          "record-factored (many atoms) or pair sums; default: the library's "
@@ -599,7 +602,10 @@ def sgdml_workload(args, rank, world, local, pg):
     if args.mf_form:
         os.environ["MLFF_MF_FORM"] = args.mf_form
     t0 = time.perf_counter()
-    Rd, Rdd = sgdml_amd.sgdml_descriptors(ds["R"])
+    # descriptors as the reference's trainer forms them (host Desc.from_R): the exact system of
+    # the oracle fixtures at their sizes; --desc gpu forms them on the device (equal to rounding)
+    Rd, Rdd = (sgdml_amd.sgdml_descriptors(ds["R"]) if args.desc == "gpu"
+               else sgdml_amd.host_descriptors(ds["R"]))
     solver = make_solver(n, rank, world, local, pg)
     if args.storage in ("sym", "dense"):
         # the stored-K forms of the same operator: K assembled on the GPU (train.py:1121-1308)
@@ -984,6 +990,7 @@ def main():
                        "cholesky (pivoted Cholesky + Woodbury, iterative_cholesky.py:115-150)",
                        "storage": storage,
                        **({"operator_form": mf_form} if mf_form else {}),
+                       **({"descriptors": args.desc} if sg_info is not None else {}),
                        "parallelism": f"row-shard x{world} (RCCL allgather/allreduce"
                        + ("/reduce-scatter)" if storage == "sym" else ")")},
             "roofline": roof_dominant,

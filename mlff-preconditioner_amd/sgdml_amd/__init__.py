@@ -6,7 +6,7 @@ Drop-in replacement of the solve path of bluecher31/mlff-preconditioner:
 numerics run in libmlffpcg.so (hand-written HIP kernels, include/mlffpcg.h).
 """
 from ._native import load_library, device_count, comm_unique_id  # noqa: F401
-from .solver import KernelSolver, PCGResult, sgdml_descriptors  # noqa: F401
+from .solver import KernelSolver, PCGResult, host_descriptors, sgdml_descriptors  # noqa: F401
 from .sharded import ShardedKernelSolver  # noqa: F401
 from .rule_of_thumb import get_params, rule_of_thumb  # noqa: F401
 

@@ -417,6 +417,18 @@ class KernelSolver:
         return fr.value, tot.value
 
 
+def host_descriptors(R: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Desc.from_R on the host, the way the reference's trainer forms the descriptors it hands
+    to Iterative.solve (desc.py:80-110 scipy pdist, :112-201 1/r and (r_a - r_b)/r^3; no cutoff,
+    no PBC): the same bits as the reference's, so a solve from them is the reference's system
+    exactly.  R: M x n_atoms x 3.  (sgdml_descriptors forms them on the GPU, equal to rounding.)"""
+    R = np.asarray(R, dtype=np.float64)
+    a, b = np.tril_indices(R.shape[1], k=-1)
+    diff = R[:, a, :] - R[:, b, :]
+    r = np.sqrt(np.sum(diff ** 2, axis=2))
+    return 1.0 / r, diff / (r ** 3)[:, :, None]
+
+
 def sgdml_descriptors(R: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     """Desc.from_R on the GPU (desc.py:292-358; no cutoff, no PBC).  R: M x n_atoms x 3."""
     lib = nat.load_library()
