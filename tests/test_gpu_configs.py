@@ -350,3 +350,54 @@ def test_ethanol_full_size_against_oracle_fixture(sg, golden_dir, monkeypatch, k
             assert_pcg_parity(r.iters, r.trace[1:], -r.x, int(f[key + sfx + "_iters"]),
                               f[key + sfx + "_trace"][1:], f[key + sfx + "_alphas"], band=b)
 
+
+@pytest.mark.timeout(900)
+def test_ethanol_n74979_against_oracle_fixture(sg, golden_dir):
+    """Ethanol at the reference's N = 75k point (BASELINE.md:24, data/rule_of_thumb.csv:9:
+    M = 2777, N = 74979, rule-of-thumb k = 3752) against the CPU oracle's run of it (tests/golden/
+    make_ethanol_75k.py -> ethanol_n74979.npz / _band.json): the pivoted
+    Cholesky on the matrix-free operator (incomplete_cholesky.py:24-93 with get_col = -K_op e_i,
+    iterative_cholesky.py:152-156; the oracle's columns from the one training point each touches),
+    the reference's one-step Woodbury panel (iterative_cholesky.py:141-143) and the scipy-1.7.3
+    PCG to 1e-6 (iterative_solver.py:995-1009).  Pivots identical up to the oracle's first
+    near-tie; the solve held to the band of the oracle's three operator orders and two Gram /
+    factorisation orders (tests/parity.py rule) at 1e-6, alpha included, and at the reference's
+    training tolerance 1e-4 (each trace's first crossing, as the band was measured)."""
+    import json
+
+    from oracle.sgdml import descriptors
+
+    path = golden_dir / "ethanol_n74979.npz"
+    if not path.exists():
+        pytest.fail("tests/golden/ethanol_n74979.npz missing (make_ethanol_75k.py)")
+    f = np.load(path, allow_pickle=False)
+    fx = json.loads((golden_dir / "ethanol_n74979_band.json").read_text())
+    Rd, Rdd = descriptors(f["R"])
+    y = f["y"]
+    n, k = y.size, int(fx["k"])
+    with sg.KernelSolver(n) as s:
+        s.sgdml_operator(Rd, Rdd, np.arange(9)[None, :], SIG)
+        s.set_operator(-1.0, LAM)
+        piv, _ = s.precon_pivchol(k)
+        res = s.pcg(y, tol=1e-6, maxiter=12000)
+    ref_piv, gap = f["index_columns"][:k], f["pivot_gap"][:k]
+    diff = np.nonzero(piv[:k] != ref_piv)[0]
+    first_tie = np.nonzero(gap < 1e-12)[0]
+    limit = int(first_tie[0]) if first_tie.size else k
+    print(f"ethanol N={n} k={k} pivots: first difference at {diff[0] if diff.size else None}, "
+          f"first oracle near-tie at {limit if first_tie.size else None}")
+    assert diff.size == 0 or diff[0] >= limit, (diff[:5], limit)
+    assert res.info == int(f["info"]) == 0
+    tr, ref_tr = np.asarray(res.trace), np.asarray(f["trace"])
+    for tol in (1e-4, 1e-6):
+        b = fx["bands"][f"k{k}_tol{tol:g}"]
+        it = int(np.argmax(tr[1:] <= tol * tr[0])) + 1
+        print(f"ethanol N={n} k={k} tol={tol:g}: GPU {it} vs oracle {b['ref_iters']} iterations "
+              f"(band {b['band_iters']}, orders { {o: v['iters'] for o, v in b['variants'].items()} })")
+        if tol == 1e-6:
+            assert it == res.iters
+            assert_pcg_parity(res.iters, tr[1:], -res.x, int(f["iters"]), ref_tr[1:], f["alphas"],
+                              band=b)
+        else:
+            assert_pcg_parity(it, tr[1:it + 1], None, b["ref_iters"], ref_tr[1:b["ref_iters"] + 1],
+                              None, band=b)
