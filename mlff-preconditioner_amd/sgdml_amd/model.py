@@ -21,7 +21,7 @@ from pathlib import Path
 
 import numpy as np
 
-from .solver import sgdml_descriptors
+from .solver import host_descriptors, sgdml_descriptors  # noqa: F401
 
 CODE_VERSION = "0.4.10"  # the sGDML model format the reference writes (sgdml/__init__.py:25)
 
@@ -156,7 +156,9 @@ def train(task, cprsn_callback=None, save_progr_callback=None, callback=None,
     n_train, n_atoms = task["R_train"].shape[:2]
     perms = np.atleast_2d(np.asarray(task["perms"]))
     tpl = tril_perms_lin(perms)
-    R_desc, R_d_desc = sgdml_descriptors(np.asarray(task["R_train"], dtype=np.float64))
+    # the descriptors as the reference's trainer forms them, on the host (Desc.from_R): the
+    # reference's system bit for bit (sgdml_descriptors forms them on the GPU, equal to rounding)
+    R_desc, R_d_desc = host_descriptors(np.asarray(task["R_train"], dtype=np.float64))
     y = task["F_train"].ravel().copy()                    # train.py:837-845
     y_std = np.std(y)
     y /= y_std

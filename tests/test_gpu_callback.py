@@ -59,7 +59,7 @@ def test_progress_and_checkpoints(fx, monkeypatch):
     assert len(saved) >= 2, (len(saved), iters)
 
     # the same solve, stopped at each checkpoint's iterate
-    R_desc, R_d_desc = sgdml_amd.sgdml_descriptors(fx["R"])
+    R_desc, R_d_desc = sgdml_amd.host_descriptors(fx["R"])  # the trainer's descriptors
     y = fx["F"].ravel().copy()
     y_std = np.std(y)
     y /= y_std

@@ -114,7 +114,8 @@ def test_fused_dropin_checkpoints(sg, nanotube, monkeypatch):
     from sgdml_amd import model as mdl
     from sgdml_amd.solvers import iterative_solver as its
 
-    f, (Rd, Rdd) = nanotube
+    f, _ = nanotube
+    Rd, Rdd = sg.host_descriptors(f["R"])  # the trainer's descriptors (model.train)
     M = f["R"].shape[0]
     task = {"type": "t", "dataset_name": "nanotube", "dataset_theory": "synthetic", "z": f["z"],
             "R_train": f["R"], "F_train": f["F"], "E_train": f["E"], "idxs_train": np.arange(M),
